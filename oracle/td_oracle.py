@@ -1,0 +1,833 @@
+"""Pure-Python/NumPy restatement of the gym-TD board and env step.
+
+TEST INFRASTRUCTURE ONLY (see ``oracle/__init__.py``): the checker the HIP path
+is compared against, and the CPU baseline ``bench.py`` times.  Parity pinned
+against golden vectors generated from the reference (tests/golden/).
+
+Numeric conventions follow the reference exactly: Python floats (IEEE binary64,
+no FMA) for LP, margin, costs, progress and reward; numpy-2 float32 semantics
+for the observation and the ``enemy_LP`` aggregate planes.
+
+Every function cites the reference file:line it restates (paths relative to the
+upstream repository root).
+"""
+import random as _pyrandom
+
+import numpy as np
+
+# --------------------------------------------------------------------------
+# Parameters  (gym_TD/envs/TDParam.py:1-118)
+# --------------------------------------------------------------------------
+
+FAIL_SUCCESS, FAIL_COST, FAIL_POS, FAIL_LVMAX, FAIL_TARGET, FAIL_CLUSTER = range(6)  # utils/fail_code.py:1-6
+
+
+class Config(object):
+    """Mutable game parameters, defaults of TDParam.py:2-64."""
+
+    def __init__(self, **kw):
+        self.max_enemy_lv = 1
+        self.max_tower_lv = 1
+        self.enemy_types = 4
+        self.tower_types = 4
+        self.enemy_LP = [[820, 1700], [2050, 3000], [6000, 8000], [8000, 12000]]
+        self.enemy_speed = [[.25, .25], [.13, .13], [.1, .1], [.1, .1]]
+        self.enemy_defense = [[0, 0], [200, 250], [600, 800], [80, 100]]
+        self.enemy_cost = [[8, 8], [15, 15], [40, 40], [30, 30]]
+        self.tower_attack = [[454, 540], [651, 771], [566, 691], [358, 424]]
+        self.tower_range = [[3, 3], [2, 2], [4, 4], [3, 3]]
+        self.tower_splash_range = [[0, 0], [0, 0], [1, 1], [0, 0]]
+        self.tower_cost = [[10, 10], [17, 17], [23, 23], [12, 12]]
+        self.tower_attack_interval = [[2, 2], [4, 4], [7, 7], [4.75, 4.75]]
+        self.tower_destruct_return = .5
+        self.frozen_time = 2
+        self.frozen_ratio = .2
+        self.attacker_init_cost = 0
+        self.defender_init_cost = 10
+        self.base_LP = 5
+        self.max_cost = 100
+        self.reward_kill = 0.1
+        self.penalty_leak = 10.
+        self.reward_time = 0.001
+        self.attacker_cost_init_rate = .5
+        self.attacker_cost_final_rate = 1
+        self.defender_cost_rate = .2
+        self.tower_distance = 2
+        self.enemy_upgrade_at = 0.75
+        self.attacker_action_interval = 1
+        self.defender_action_interval = 1
+        for k, v in kw.items():
+            setattr(self, k, v)
+
+
+class Hyper(object):
+    """TDParam.py:105-111 (immutable in the reference; a plain record here)."""
+
+    def __init__(self, allow_multiple_actions=False):
+        self.max_episode_steps = 1200
+        self.allow_multiple_actions = allow_multiple_actions
+        self.max_cluster_length = 8
+        self.max_num_of_roads = 3
+
+
+def n_channels(cfg):
+    """TDBoard.py:146-154."""
+    return 15 + 2 * cfg.tower_types + cfg.max_tower_lv + 1 + 5 * cfg.enemy_types
+
+
+# --------------------------------------------------------------------------
+# Road generation  (gym_TD/envs/TDRoadGen.py:4-199, create_road = v2 at :261)
+# --------------------------------------------------------------------------
+
+class RoadGenError(Exception):
+    """The reference raises (IndexError/ValueError) or never terminates."""
+
+
+def create_road(rng, L, num_roads, max_attempts=None):
+    """Restates create_road_v2 (TDRoadGen.py:4-199) call for call on ``rng``.
+
+    ``max_attempts`` bounds each ``while not succ`` loop (the reference's are
+    unbounded, TDRoadGen.py:129,142,177); exceeding it raises RoadGenError.
+    """
+    assert 1 <= num_roads <= 3
+
+    def inner(p):  # :6-7
+        return 0 < p[0] < L - 1 and 0 < p[1] < L - 1
+
+    lo, hi = L // 3, (L * 2 + 2) // 3  # :9
+    center = [rng.randint(low=lo, high=hi), rng.randint(low=lo, high=hi)]  # :10-13
+    step = ((1, 0), (0, -1), (-1, 0), (0, 1))  # :15
+    field = np.zeros((L, L), dtype=np.int32)
+    rot = np.zeros((L, L), dtype=np.int32)
+    field[center[0], center[1]] = 1
+    d0 = rng.randint(4)  # :20
+
+    def walk(start, d):  # generate_road, :31-119
+        pos = list(start)
+        road = []
+        pending = None
+        loop = 0
+        while inner(pos) and loop < 100:
+            loop += 1
+            shape = rng.randint(2)
+            seg = rng.randint(low=L * 3 // 20, high=L // 4)
+            cross = False
+
+            def run(n, dd, reset_cross):
+                nonlocal cross
+                for _ in range(n):
+                    pos[0] += step[dd][0]
+                    pos[1] += step[dd][1]
+                    if field[pos[0], pos[1]] != 0:
+                        pos[0] -= step[dd][0]
+                        pos[1] -= step[dd][1]
+                        cross = True
+                        return
+                    if reset_cross:
+                        cross = False
+                    road.append(list(pos))
+                    field[pos[0], pos[1]] = 1
+                    if not inner(pos):
+                        return
+
+            if shape <= 0:  # straight segment of 2*seg, :43-59
+                run(seg * 2, d, False)
+            else:  # turn segment, :60-104
+                run(seg, d, False)
+                if not inner(pos):
+                    break
+                if pending is not None:
+                    rd, pending = pending, None
+                else:
+                    rd = rng.randint(2) * 2 - 1
+                    pending = -rd
+                rot[pos[0], pos[1]] = 1
+                d = (d + 4 + rd) % 4
+                run(seg, d, True)
+            if cross:  # :105-114
+                free = [i for i, (dx, dy) in enumerate(step) if field[pos[0] + dx, pos[1] + dy] == 0]
+                if not free:
+                    return road, False
+                d = free[rng.randint(low=0, high=len(free))]
+                pending = None
+                rot[pos[0], pos[1]] = 1
+        if loop >= 100:
+            return road, False
+        return road, True
+
+    def erase(road):  # clean_up, :121-124
+        for p in road:
+            field[p[0], p[1]] = 0
+            rot[p[0], p[1]] = 0
+
+    def bounded():
+        n = 0
+        while True:
+            n += 1
+            if max_attempts is not None and n > max_attempts:
+                raise RoadGenError("retry bound exceeded")
+            yield
+
+    # center -> end, :128-137
+    for _ in bounded():
+        road1, ok = walk(center, d0)
+        if not ok:
+            erase(road1)
+            continue
+        if len(road1) >= L:
+            erase(road1)
+            continue
+        break
+    # center -> start, :141-155
+    for _ in bounded():
+        road2, ok = walk(center, (d0 + 2) % 4)
+        if not ok:
+            erase(road2)
+            continue
+        if len(road1) + len(road2) + 1 >= L * 2:
+            erase(road2)
+            continue
+        if abs(road2[-1][0] - road1[-1][0]) + abs(road2[-1][1] - road1[-1][1]) < L * 3 // 4:
+            erase(road2)
+            continue
+        break
+    main = road2[::-1] + [list(center)] + road1  # :157-158
+    roads = [main]
+    picks = []  # :162-170
+    i = 0
+    while i < len(main):
+        if not rot[main[i][0], main[i][1]]:
+            if i < len(main) - 1 and not rot[main[i + 1][0], main[i + 1][1]]:
+                picks.append((main[i], i))
+            i += 1
+        else:
+            i += 2
+    for _r in range(1, num_roads):  # :174-197
+        for _ in bounded():
+            try:
+                k = rng.randint(low=len(picks) * 2 // 5, high=len(picks) * 4 // 5)
+            except ValueError as ex:
+                raise RoadGenError("randint: %s" % ex)
+            nd = rng.randint(4)
+            branch_start, k = picks[k]
+            branch, ok = walk(branch_start, nd)
+            if not ok:
+                erase(branch)
+                continue
+            if len(branch) + len(main) - k >= L * 2:
+                erase(branch)
+                continue
+            if not branch:
+                raise RoadGenError("empty branch road (IndexError at TDRoadGen.py:189)")
+            if abs(branch[-1][0] - main[-1][0]) + abs(branch[-1][1] - main[-1][1]) < L * 3 // 4:
+                erase(branch)
+                continue
+            break
+        roads.append(branch[::-1] + main[k:])
+    return roads
+
+
+def layout_from_roads(roads, L):
+    """Map planes 0-6, start list and end cell (TDBoard.py:31-59)."""
+    m = np.zeros((7, L, L), dtype=np.int32)
+    for i, road in enumerate(roads):
+        prev = None
+        for p in road:
+            m[0, p[0], p[1]] = 1
+            m[i + 1, p[0], p[1]] = 1
+            m[6, p[0], p[1]] = 1
+            if prev is not None:
+                dr, dc = p[0] - prev[0], p[1] - prev[1]
+                m[5, prev[0], prev[1]] = (0 if dc == 1 else 1) if dr == 0 else (2 if dr == 1 else 3)
+            prev = p
+        for dist, p in enumerate(reversed(road)):
+            m[4, p[0], p[1]] = dist
+    return m, [list(r[0]) for r in roads], list(roads[0][-1])
+
+
+# --------------------------------------------------------------------------
+# Board  (gym_TD/envs/TDBoard.py, TDElements.py)
+# --------------------------------------------------------------------------
+
+class Enemy(object):
+    """TDElements.py:4-43 (``lv`` kept explicitly; the reference derives stats from it)."""
+    __slots__ = ("type", "lv", "LP", "maxLP", "speed", "defense", "cost", "loc", "dist", "margin", "slowdown")
+
+    def __init__(self, cfg, t, lv, loc, dist):
+        self.type, self.lv = t, lv
+        self.maxLP = self.LP = cfg.enemy_LP[t][lv]
+        self.speed = cfg.enemy_speed[t][lv]
+        self.defense = cfg.enemy_defense[t][lv]
+        self.cost = cfg.enemy_cost[t][lv]
+        self.loc, self.dist = loc, dist
+        self.margin = 0.
+        self.slowdown = 0
+
+    def hit(self, atk, magic=False):  # Enemy.damage, TDElements.py:19-28
+        dmg = atk if magic else max(atk - self.defense, 0)
+        if dmg < atk * .05:
+            dmg = atk * .05
+        self.LP -= dmg
+        if self.LP <= 0:
+            self.LP = 0
+
+
+class Tower(object):
+    """TDElements.py:45-69, 134-170."""
+    __slots__ = ("type", "lv", "loc", "atk", "rge", "dmgrge", "intv", "cost", "cd")
+
+    def __init__(self, cfg, t, loc):  # create_tower, :134-150
+        self.type, self.lv, self.loc = t, 0, loc
+        self.atk = cfg.tower_attack[t][0]
+        self.rge = cfg.tower_range[t][0]
+        self.dmgrge = cfg.tower_splash_range[t][0]
+        self.intv = cfg.tower_attack_interval[t][0]
+        self.cost = cfg.tower_cost[t][0]
+        self.cd = 0
+
+    def upgrade(self, cfg):
+        """upgrade_tower (:152-170) -> Tower.lvup (:57-63).
+
+        Reference quirk reproduced: upgrade_tower passes (atk, rge, dmgrge, COST,
+        INTERVAL) into lvup(atk, rge, dmgrge, INTV, COST), so after an upgrade the
+        interval is tower_cost[t][l] and the cost grows by tower_attack_interval[t][l].
+        """
+        if self.lv >= cfg.max_tower_lv:
+            return False
+        t, l = self.type, self.lv + 1
+        self.lv += 1
+        self.atk = cfg.tower_attack[t][l]
+        self.rge = cfg.tower_range[t][l]
+        self.dmgrge = cfg.tower_splash_range[t][l]
+        self.intv = cfg.tower_cost[t][l]
+        self.cost += cfg.tower_attack_interval[t][l]
+        return True
+
+
+def _cheb(a, b):  # Tower.dist, TDElements.py:67-69 (Chebyshev)
+    return max(abs(a[0] - b[0]), abs(a[1] - b[1]))
+
+
+def _fire(tw, enemies, cfg):
+    """Tower*.attack, TDElements.py:71-132. Returns the enemies left at LP 0."""
+    target = None
+    for e in enemies:
+        if _cheb(e.loc, tw.loc) <= tw.rge:
+            target = e
+            break
+    if target is None:
+        return []
+    tw.cd += tw.intv
+    out = []
+    if tw.type in (0, 1):  # arrow / magic: single target, magic ignores defense
+        target.hit(tw.atk, tw.type == 1)
+        if not target.LP > 0:
+            out.append(target)
+    elif tw.type == 2:  # bomb: splash around the target
+        for e in enemies:
+            if _cheb(target.loc, e.loc) <= tw.dmgrge:
+                e.hit(tw.atk)
+                if not e.LP > 0:
+                    out.append(e)
+    else:  # frozen: first enemy within splash of the target
+        for e in enemies:
+            if _cheb(target.loc, e.loc) <= tw.dmgrge:
+                e.hit(tw.atk, True)
+                e.slowdown = cfg.frozen_time
+                if not e.LP > 0:
+                    out.append(e)
+                break
+    return out
+
+
+class Board(object):
+    """TDBoard (TDBoard.py:10-385), minus rendering."""
+
+    def __init__(self, L, num_roads, rng, cfg, hp, roads=None):
+        self.L, self.cfg, self.hp = L, cfg, hp
+        if roads is None:
+            roads = create_road(rng, L, num_roads)
+        self.roads = roads
+        self.map, self.start, self.end = layout_from_roads(roads, L)
+        self.num_roads = len(roads)
+        self.enemy_LP = np.zeros((4, cfg.enemy_types, L, L), dtype=np.float32)
+        self.enemies, self.towers = [], []
+        self.cost_def = cfg.defender_init_cost
+        self.cost_atk = cfg.attacker_init_cost
+        self.max_cost = cfg.max_cost
+        self.base_LP = cfg.base_LP
+        self.max_base_LP = cfg.base_LP
+        self.steps = 0
+        self.progress = 0.
+        self.fail_code = FAIL_SUCCESS
+
+    # ---- observation, TDBoard.py:85-144 ------------------------------------
+    def get_states(self):
+        cfg, L = self.cfg, self.L
+        s = np.zeros((n_channels(cfg), L, L), dtype=np.float32)
+        s[0:4] = self.map[0:4]
+        s[4, self.end[0], self.end[1]] = 1
+        s[5] = 1. if self.max_base_LP is None else self.base_LP / self.max_base_LP
+        for i, st in enumerate(self.start):
+            s[6 + i, st[0], st[1]] = 1
+        s[9] = self.map[4]
+        s[9] /= (np.max(self.map[4]) + 1)
+        s[11] = self.cost_def / self.max_cost
+        s[12] = self.cost_atk / self.max_cost
+        s[13] = self.progress
+        s[14] = (self.map[6] == 0)
+        lv0 = 15
+        ty0 = lv0 + cfg.max_tower_lv + 1
+        bd0 = ty0 + cfg.tower_types
+        for t in self.towers:
+            s[lv0 + t.lv, t.loc[0], t.loc[1]] = 1
+            s[ty0 + t.type, t.loc[0], t.loc[1]] = 1
+        for t in range(cfg.tower_types):
+            s[bd0 + t] = 1 if self.cost_def >= cfg.tower_cost[t][0] else 0
+        en0 = bd0 + cfg.tower_types
+        su0 = en0 + 4 * cfg.enemy_types
+        s[en0:su0] = self.enemy_LP.reshape((4 * cfg.enemy_types, L, L))
+        for t in range(cfg.enemy_types):
+            s[su0 + t] = self.cost_def / cfg.enemy_cost[t][0] / self.hp.max_cluster_length
+        return s
+
+    def done(self):  # :370-385
+        return (self.base_LP is not None and self.base_LP <= 0) or self.steps >= self.hp.max_episode_steps
+
+    def is_valid_pos(self, p):  # :166-182
+        return 0 <= p[0] < self.L and 0 <= p[1] < self.L
+
+    # ---- attacker, TDBoard.py:199-224 ---------------------------------------
+    def summon_cluster(self, types, road):
+        cfg = self.cfg
+        st = self.start[road]
+        lv = 1 if self.progress >= cfg.enemy_upgrade_at else 0
+        tried = summoned = False
+        real = []
+        for t in types:
+            t = int(t)
+            if t == cfg.enemy_types:
+                real.append(t)
+                continue
+            tried = True
+            e = Enemy(cfg, t, lv, st, int(self.map[4, st[0], st[1]]))
+            if self.cost_atk < e.cost:
+                real.append(cfg.enemy_types)
+            else:
+                self.cost_atk -= e.cost
+                self.enemies.append(e)
+                summoned = True
+                real.append(t)
+        if tried and not summoned:
+            self.fail_code = FAIL_COST
+            return False, real
+        self.fail_code = FAIL_SUCCESS
+        return True, real
+
+    # ---- defender, TDBoard.py:226-293 ---------------------------------------
+    def _diamond(self, loc, delta):
+        k = self.cfg.tower_distance
+        for i in range(-k, k + 1):
+            for j in range(-k, k + 1):
+                if abs(i) + abs(j) <= k:
+                    r, c = loc[0] + i, loc[1] + j
+                    if 0 <= r < self.L and 0 <= c < self.L:
+                        self.map[6, r, c] += delta
+
+    def tower_build(self, t, loc):
+        tw = Tower(self.cfg, t, loc)
+        if self.cost_def < tw.cost:
+            self.fail_code = FAIL_COST
+            return False
+        if self.map[6, loc[0], loc[1]] > 0:
+            self.fail_code = FAIL_POS
+            return False
+        self.towers.append(tw)
+        self.cost_def -= tw.cost
+        self._diamond(loc, 1)
+        self.fail_code = FAIL_SUCCESS
+        return True
+
+    def _tower_at(self, loc):
+        for tw in self.towers:
+            if tw.loc[0] == loc[0] and tw.loc[1] == loc[1]:
+                return tw
+        return None
+
+    def tower_lvup(self, loc):
+        tw = self._tower_at(loc)
+        if tw is None:
+            self.fail_code = FAIL_TARGET
+            return False
+        if tw.lv >= self.cfg.max_tower_lv:
+            self.fail_code = FAIL_LVMAX
+            return False
+        cost = self.cfg.tower_cost[tw.type][tw.lv + 1]
+        if self.cost_def < cost:
+            self.fail_code = FAIL_COST
+            return False
+        tw.upgrade(self.cfg)
+        self.cost_def -= cost
+        self.fail_code = FAIL_SUCCESS
+        return True
+
+    def tower_destruct(self, loc):
+        tw = self._tower_at(loc)
+        if tw is None:
+            self.fail_code = FAIL_TARGET
+            return False
+        self.cost_def += tw.cost * self.cfg.tower_destruct_return
+        self.cost_def = min(self.cost_def, self.max_cost)
+        self.towers.remove(tw)
+        self._diamond(loc, -1)
+        self.fail_code = FAIL_SUCCESS
+        return True
+
+    # ---- one time step, TDBoard.py:295-368 ----------------------------------
+    def step(self):
+        cfg, L = self.cfg, self.L
+        reward = 0.
+        reward += cfg.reward_time
+        self.steps += 1
+        self.progress = self.steps / self.hp.max_episode_steps
+        self.enemies.sort(key=lambda e: e.dist - e.margin)  # stable, f64 key
+        dead = []
+        for tw in self.towers:
+            tw.cd -= 1
+            if tw.cd > 0:
+                continue
+            for e in _fire(tw, self.enemies, cfg):
+                if not any(e is d for d in dead):
+                    dead.append(e)
+            if tw.cd < 0:
+                tw.cd = 0
+        reward += cfg.reward_kill * len(dead)
+        dead_ids = set(id(e) for e in dead)
+        self.enemies = [e for e in self.enemies if id(e) not in dead_ids]
+        move = ((0, 1), (0, -1), (1, 0), (-1, 0))  # :319
+        gone = set()
+        for e in self.enemies:
+            if e.slowdown > 0:
+                e.margin += e.speed * cfg.frozen_ratio
+                e.slowdown -= 1
+            else:
+                e.margin += e.speed
+            while e.margin >= 1.:
+                e.margin -= 1.
+                d = self.map[5, e.loc[0], e.loc[1]]
+                p = [e.loc[0] + move[d][0], e.loc[1] + move[d][1]]
+                e.loc, e.dist = p, int(self.map[4, p[0], p[1]])
+                if p[0] == self.end[0] and p[1] == self.end[1]:
+                    if self.base_LP is not None and self.base_LP > 0:
+                        reward -= cfg.penalty_leak
+                    gone.add(id(e))
+                    if self.base_LP is not None:
+                        self.base_LP = max(self.base_LP - 1, 0)
+                    break
+        self.enemies = [e for e in self.enemies if id(e) not in gone]
+        if self.progress >= 0.5:
+            rate = cfg.attacker_cost_final_rate
+        else:
+            rate = cfg.attacker_cost_init_rate * (1. - self.progress) + cfg.attacker_cost_final_rate * self.progress
+        self.cost_atk = min(self.cost_atk + rate, self.max_cost)
+        self.cost_def = min(self.cost_def + cfg.defender_cost_rate, self.max_cost)
+        # per-cell enemy LP statistics (:355-365), numpy float32 semantics
+        elp = self.enemy_LP
+        elp[:] = 0
+        elp[0] = 1.
+        for e in self.enemies:
+            r = e.LP / e.maxLP
+            i = (e.type, e.loc[0], e.loc[1])
+            elp[(0,) + i] = min(elp[(0,) + i], r)
+            elp[(1,) + i] = max(elp[(1,) + i], r)
+            elp[(2,) + i] += r
+            elp[(3,) + i] += 1
+        elp[0] = np.where(elp[3] > 0, elp[0], np.zeros_like(elp[0]))
+        elp[2] = np.where(elp[3] > 0, elp[2] / elp[3], np.zeros_like(elp[2]))
+        elp[3] /= self.hp.max_cluster_length
+        return reward
+
+
+# --------------------------------------------------------------------------
+# Envs  (TDGymBasic.py, TDDefense.py, TDAttack.py, TDMulti.py)
+# --------------------------------------------------------------------------
+
+MODE_DEF, MODE_ATK, MODE_2P = 0, 1, 2
+
+
+class Env(object):
+    """One TD-def / TD-atk / TD-2p env.
+
+    Seeding (build convention): ``np_random`` is
+    ``numpy.random.RandomState(seed)`` (what gym's seeding returns, minus gym's
+    version-specific seed hashing), and the built-in opponent draws from a
+    private ``random.Random(opp_seed)`` instead of the process-global ``random``
+    module (TDGymBasic.py:84-86, 98-100).
+    """
+
+    def __init__(self, L, mode=MODE_DEF, difficulty=1, seed=0, opp_seed=None, cfg=None, hp=None,
+                 random_agent=True, road_attempts=None):
+        self.L, self.mode, self.difficulty = L, mode, difficulty
+        self.cfg = cfg or Config()
+        self.hp = hp or Hyper()
+        self.random_agent = random_agent
+        self.np_random = np.random.RandomState(seed)
+        self.rnd = _pyrandom.Random(seed if opp_seed is None else opp_seed)
+        self.road_attempts = road_attempts
+        self._board = None
+        self.reset()
+
+    # TDGymBasic.reset, :37-55
+    def reset(self):
+        self.num_roads = self.np_random.randint(low=1, high=self.hp.max_num_of_roads + 1)
+        self._board = Board(self.L, self.num_roads, None, self.cfg, self.hp,
+                            roads=create_road(self.np_random, self.L, self.num_roads, self.road_attempts))
+        self.attacker_cd = 0
+        self.defender_cd = 0
+        return self._board.get_states()
+
+    def empty_def(self):
+        if self.hp.allow_multiple_actions:
+            return np.zeros((self.cfg.tower_types + 2, self.L, self.L), dtype=np.int64)
+        return self.L * self.L * (self.cfg.tower_types + 2)
+
+    def empty_atk(self):
+        return np.full((self.hp.max_num_of_roads, self.hp.max_cluster_length), self.cfg.enemy_types, dtype=np.int64)
+
+    # ---- built-in attacker, TDGymBasic.py:81-108 ----------------------------
+    def random_enemy_lv0(self):
+        if self.attacker_cd == 0:
+            if self.random_agent:
+                cluster = [self.rnd.randint(0, self.cfg.enemy_types) for _ in range(self.hp.max_cluster_length)]
+                road = self.rnd.randint(0, self.num_roads - 1)
+            else:
+                cluster = self.np_random.randint(0, self.cfg.enemy_types, [self.hp.max_cluster_length], dtype=np.int64)
+                road = self.np_random.randint(self.num_roads)
+            self._board.summon_cluster(cluster, road)  # (ok, real) tuple: always truthy
+            self.attacker_cd = self.cfg.attacker_action_interval
+
+    def random_enemy_lv1(self):
+        if self.attacker_cd == 0:
+            if self.random_agent:
+                t = self.rnd.randint(0, self.cfg.enemy_types - 1)
+                road = self.rnd.randint(0, self.num_roads - 1)
+            else:
+                t = self.np_random.randint(0, self.cfg.enemy_types)
+                road = self.np_random.randint(self.num_roads)
+            self._board.summon_cluster([t] * self.hp.max_cluster_length, road)
+            self.attacker_cd = self.cfg.attacker_action_interval
+
+    # ---- built-in defender, TDGymBasic.py:111-292 ---------------------------
+    def random_tower_lv0(self):
+        if self.defender_cd == 0:
+            if self.random_agent:
+                r = self.rnd.randint(0, self.L - 1)
+                c = self.rnd.randint(0, self.L - 1)
+                t = self.rnd.randint(0, self.cfg.tower_types - 1)
+            else:
+                r, c = self.np_random.randint(0, self.L, [2, ])
+                t = self.np_random.randint(0, self.cfg.tower_types)
+            if self._board.tower_build(t, [int(r), int(c)]):
+                self.defender_cd = self.cfg.defender_action_interval
+
+    def _road_cells(self):
+        return [[r, c] for r in range(self.L) for c in range(self.L) if self._board.map[0, r, c] == 1]
+
+    def _build_near_road(self, t, draw_type=False):
+        """Shuffle the road cells, try one random offset per cell (:142-170, :242-266).
+
+        lv1 draws the tower type after the shuffle (``draw_type``, :149-154).  The
+        reference's "wait for cost" branch (:127-134, :201-208) is dead code:
+        getattr(self, '__wait_for_cost_rt1') never sees the name-mangled attribute.
+        """
+        offs = [[r, c] for r in range(-2, 3) for c in range(-2, 3)]
+        cells = self._road_cells()
+        if self.random_agent:
+            self.rnd.shuffle(cells)
+            if draw_type:
+                t = self.rnd.randint(0, self.cfg.tower_types - 1)
+        else:
+            self.np_random.shuffle(cells)
+            if draw_type:
+                t = self.np_random.randint(0, self.cfg.tower_types)
+        for r, c in cells:
+            if self.random_agent:
+                d = offs[self.rnd.randint(0, len(offs) - 1)]
+            else:
+                d = offs[self.np_random.randint(0, len(offs))]
+            pos = [r + d[0], c + d[1]]
+            if not self._board.is_valid_pos(pos):
+                continue
+            if self._board.tower_build(t, pos):
+                self.defender_cd = self.cfg.defender_action_interval
+                return
+            if self._board.fail_code == FAIL_COST:
+                return
+
+    def _upgrade_or_destruct(self, act):
+        b = self._board
+        if not b.towers:
+            return
+        if act == 1:
+            i = self.rnd.randint(0, len(b.towers) - 1) if self.random_agent else self.np_random.randint(0, len(b.towers))
+            if b.tower_lvup(b.towers[i].loc):
+                self.defender_cd = self.cfg.defender_action_interval
+        else:
+            p = self.rnd.random() if self.random_agent else self.np_random.random()
+            if p > .01:
+                return
+            i = self.rnd.randint(0, len(b.towers) - 1)  # global random in both branches (:187,:191)
+            if b.tower_destruct(b.towers[i].loc):
+                self.defender_cd = self.cfg.defender_action_interval
+
+    def random_tower_lv1(self):
+        if self.defender_cd == 0:
+            act = self.rnd.randint(0, 2) if self.random_agent else self.np_random.randint(0, 3)
+            if act == 0:
+                self._build_near_road(None, draw_type=True)
+            else:
+                self._upgrade_or_destruct(act)
+
+    def random_tower_lv2(self):
+        if self.defender_cd == 0:
+            act = self.rnd.randint(0, 2) if self.random_agent else self.np_random.randint(0, 3)
+            if act == 0:
+                et = [e.type for e in self._board.enemies]
+                if len(et) == 0:
+                    return
+                types, nums = np.unique(et, return_counts=True)
+                ratio = nums.astype(np.float32) / np.sum(nums)
+                p = self.rnd.random() if self.random_agent else self.np_random.random()
+                t = None
+                for i in range(4):
+                    if p < ratio[i]:
+                        t = types[i]
+                        break
+                    p -= ratio[i]
+                t = [2, 0, 1, 0][t]
+                p = self.rnd.random() if self.random_agent else self.np_random.random()
+                if p < 0.2:
+                    t = 3
+                self._build_near_road(t)
+            else:
+                self._upgrade_or_destruct(act)
+
+    # ---- multi-action defender scan, TDDefense.py:41-60 / TDMulti.py:208-227
+    def _def_scan(self, a):
+        b, T = self._board, self.cfg.tower_types
+        real = np.zeros((T + 2, self.L, self.L), dtype=np.int64)
+        if self.defender_cd == 0:
+            for r in range(self.L):
+                for c in range(self.L):
+                    for t in range(T):
+                        if a[t][r][c] == 1 and b.tower_build(t, [r, c]):
+                            self.defender_cd = self.cfg.defender_action_interval
+                            real[t, r, c] = 1
+                    if a[T][r][c] == 1 and b.tower_lvup([r, c]):
+                        self.defender_cd = self.cfg.defender_action_interval
+                        real[T, r, c] = 1
+                    if a[T + 1][r][c] == 1 and b.tower_destruct([r, c]):
+                        self.defender_cd = self.cfg.defender_action_interval
+                        real[T + 1, r, c] = 1
+        return real
+
+    def _def_discrete(self, a):
+        """TDDefense.py:62-77 / TDMulti.py:243-258. Returns (acted, fail_code)."""
+        L, b = self.L, self._board
+        if self.defender_cd == 0 and a != L * L * (self.cfg.tower_types + 2):
+            act, r, c = a // (L * L), (a // L) % L, a % L
+            if act < self.cfg.tower_types:
+                res = b.tower_build(act, [r, c])
+            elif act == self.cfg.tower_types:
+                res = b.tower_lvup([r, c])
+            else:
+                res = b.tower_destruct([r, c])
+            if res:
+                self.defender_cd = self.cfg.defender_action_interval
+            return res, b.fail_code
+        return False, 0
+
+    def step(self, def_act=None, atk_act=None):
+        """One env step; returns (obs, reward, done, info).
+
+        Multi-action info: the reference raises UnboundLocalError while building
+        the info dict (TDDefense.py:87, TDMulti.py:134-135) after the board has
+        advanced; the oracle returns FailCode=None there instead.
+        """
+        cfg, hp, b = self.cfg, self.hp, self._board
+        self.attacker_cd = max(self.attacker_cd - 1, 0)
+        self.defender_cd = max(self.defender_cd - 1, 0)
+        info = {}
+        if self.mode == MODE_DEF:  # TDDefense.step, :34-87
+            if hp.allow_multiple_actions:
+                real = self._def_scan(def_act)
+                fc = None
+            else:
+                acted, fc = self._def_discrete(def_act)
+                real = def_act if acted else self.L * self.L * 6
+            getattr(self, "random_enemy_lv%d" % self.difficulty)()
+            info = {"RealAction": real, "FailCode": fc}
+        elif self.mode == MODE_ATK:  # TDAttack.step, :27-56
+            real = np.copy(atk_act)
+            fc = []
+            if self.attacker_cd == 0:
+                for i in range(self.num_roads):
+                    cl = atk_act[i]
+                    if np.all(cl == cfg.enemy_types):
+                        fc.append(0)
+                        continue
+                    ok, rr = b.summon_cluster(cl, i)  # unpacked: a real bool here (:42-44)
+                    if ok:
+                        self.attacker_cd = cfg.attacker_action_interval
+                    real[i] = rr
+                    fc.append(b.fail_code)
+            getattr(self, "random_tower_lv%d" % self.difficulty)()
+            info = {"RealAction": real, "FailCode": fc}
+        else:  # TDMulti.step, :46-138
+            real = {"Attacker": np.copy(atk_act)}
+            if hp.allow_multiple_actions:
+                if self.attacker_cd == 0:
+                    for i in range(self.num_roads):
+                        b.summon_cluster(atk_act[i], i)  # tuple: always truthy (:203)
+                        self.attacker_cd = cfg.attacker_action_interval
+                real["Defender"] = self._def_scan(def_act)
+                fc = None
+            else:
+                afail = []
+                if self.attacker_cd == 0:
+                    for i in range(self.num_roads):
+                        cl = atk_act[i]
+                        if np.all(cl == 4):
+                            afail.append(0)
+                            continue
+                        b.summon_cluster(cl, i)
+                        self.attacker_cd = cfg.attacker_action_interval
+                        afail.append(b.fail_code)
+                real["Defender"] = self.L * self.L * 6
+                acted, dfail = self._def_discrete(def_act)
+                if acted:
+                    real = def_act  # quirk: replaces the whole dict (:257)
+                fc = {"Attacker": afail, "Defender": dfail}
+            info = {"RealAction": real, "FailCode": fc}
+        reward = b.step()
+        if self.mode == MODE_ATK:
+            reward = -reward
+        done = b.done()
+        obs = b.get_states()
+        win = None
+        if done:
+            if self.mode == MODE_DEF:
+                win = b.base_LP is None or b.base_LP > 0
+            elif self.mode == MODE_ATK:
+                win = b.base_LP is None or b.base_LP <= 0
+            else:
+                win = {"Defender": b.base_LP is None or b.base_LP > 0,
+                       "Attacker": b.base_LP is None or b.base_LP <= 0}
+        info["Win"] = win
+        if self.mode == MODE_2P:
+            info["AllowNextMove"] = {"Attacker": self.attacker_cd <= 1, "Defender": self.defender_cd <= 1}
+        elif self.mode == MODE_ATK:
+            info["AllowNextMove"] = self.attacker_cd <= 1
+        else:
+            info["AllowNextMove"] = self.defender_cd <= 1
+        return obs, reward, done, info
