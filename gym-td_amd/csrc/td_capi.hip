@@ -1,0 +1,584 @@
+// td_capi.hip -- the C-ABI (include/tdstep.h): handle, HBM buffers, launches, and
+// the host side of per-episode layouts (numpy-legacy streams + road generation).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/tdstep.h"
+#include "td_kernels.h"
+#include "td_layout.h"
+#include "td_rng.h"
+
+using namespace td;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
+int fail(const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return -1;
+}
+
+#define HIP_OK(expr)                                                                     \
+  do {                                                                                   \
+    hipError_t e_ = (expr);                                                              \
+    if (e_ != hipSuccess) return fail("%s: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, __LINE__); \
+  } while (0)
+
+constexpr int kMaxAttempts = 20000;  // bound for each of create_road_v2's retry loops
+constexpr int kRefillEvery = 4;      // steps between looks at the consumed-layout counters
+constexpr int kRefillMax = 4096;     // layouts generated per refill at most
+
+}  // namespace
+
+struct td_handle {
+  int L = 0, NC = 0, B = 0, mode = 0, multi = 0, difficulty = 1, device = 0, autoreset = 1;
+  int lw = 0;  // layout record words
+  TdDevCfg dcfg;
+  // device
+  TdDevCfg* d_cfg = nullptr;
+  TdHdr* d_hdr = nullptr;
+  double *d_en_lp = nullptr, *d_en_mg = nullptr, *d_tw_cd = nullptr;
+  uint32_t *d_en_inf = nullptr, *d_tw_inf = nullptr, *d_cells = nullptr, *d_opp = nullptr;
+  uint32_t *d_nxt = nullptr, *d_consumed = nullptr, *d_stage = nullptr;
+  int32_t* d_stage_ids = nullptr;
+  uint8_t* d_mask = nullptr;
+  // host
+  std::vector<uint32_t> np_state;   // [B][625] numpy-legacy stream per board (layouts)
+  std::vector<uint32_t> uploaded;   // layouts staged per board so far
+  uint32_t* h_consumed = nullptr;   // pinned copy of d_consumed
+  uint32_t* h_stage = nullptr;      // pinned staging, kRefillMax records
+  int32_t* h_stage_ids = nullptr;
+  hipEvent_t ev_consumed = nullptr, ev_stage = nullptr;
+  bool consumed_pending = false;
+  long long steps = 0;
+  long long roadgen_failures = 0;
+  std::vector<int32_t> last_reset_failed;
+  int nthreads = 1;
+  std::vector<std::vector<uint8_t>> scratch;  // per worker thread
+};
+
+namespace {
+
+void build_dev_cfg(const td_config& c, TdDevCfg& d) {
+  std::memset(&d, 0, sizeof d);
+  for (int t = 0; t < 4; ++t)
+    for (int l = 0; l < 2; ++l) {
+      d.e_lp[t][l] = c.enemy_LP[t][l];
+      d.e_speed[t][l] = c.enemy_speed[t][l];
+      d.e_def[t][l] = c.enemy_defense[t][l];
+      d.e_cost[t][l] = c.enemy_cost[t][l];
+      d.t_atk[t][l] = c.tower_attack[t][l];
+      d.t_rge[t][l] = c.tower_range[t][l];
+      d.t_dmg[t][l] = c.tower_splash_range[t][l];
+      d.t_price[t][l] = c.tower_cost[t][l];
+    }
+  // Tower attributes after create_tower / upgrade_tower (TDElements.py:134-170):
+  // lvup(atk, rge, dmgrge, intv=tower_cost[t][l], cost += tower_attack_interval[t][l]).
+  for (int t = 0; t < 4; ++t) {
+    d.t_intv[t][0] = c.tower_attack_interval[t][0];
+    d.t_value[t][0] = c.tower_cost[t][0];
+    d.t_intv[t][1] = c.tower_cost[t][1];
+    d.t_value[t][1] = c.tower_cost[t][0] + c.tower_attack_interval[t][1];
+  }
+  d.destruct_return = c.tower_destruct_return;
+  d.frozen_ratio = c.frozen_ratio;
+  d.max_cost = c.max_cost;
+  d.reward_kill = c.reward_kill;
+  d.penalty_leak = c.penalty_leak;
+  d.reward_time = c.reward_time;
+  d.atk_init_rate = c.attacker_cost_init_rate;
+  d.atk_final_rate = c.attacker_cost_final_rate;
+  d.def_rate = c.defender_cost_rate;
+  d.enemy_upgrade_at = c.enemy_upgrade_at;
+  d.def_init_cost = c.defender_init_cost;
+  d.atk_init_cost = c.attacker_init_cost;
+  d.frozen_time = (int32_t)c.frozen_time;
+  d.base_LP = (int32_t)c.base_LP;
+  d.tower_distance = (int32_t)c.tower_distance;
+  d.atk_interval = (int32_t)c.attacker_action_interval;
+  d.def_interval = (int32_t)c.defender_action_interval;
+  d.max_episode_steps = c.max_episode_steps;
+  d.max_cluster_length = c.max_cluster_length;
+  d.max_tower_lv = c.max_tower_lv;
+}
+
+int check_cfg(const td_config& c) {
+  if (c.enemy_types != 4 || c.tower_types != 4) return fail("enemy_types / tower_types must be 4 (obs has 45 channels)");
+  if (c.max_enemy_lv != 1 || c.max_tower_lv < 0 || c.max_tower_lv > 1) return fail("max_enemy_lv must be 1, max_tower_lv 0 or 1");
+  if (c.max_cluster_length != 8 || c.max_num_of_roads != 3) return fail("max_cluster_length must be 8, max_num_of_roads 3");
+  if (c.max_episode_steps <= 0) return fail("max_episode_steps must be > 0");
+  if (c.tower_distance < 0 || c.tower_distance > 15) return fail("tower_distance out of range");
+  if (c.frozen_time < 0 || c.frozen_time > 0xffff) return fail("frozen_time out of range");
+  if (c.base_LP < 1) return fail("base_LP must be a positive int (None is not supported)");
+  for (int t = 0; t < 4; ++t)
+    for (int l = 0; l < 2; ++l)
+      if (c.enemy_LP[t][l] <= 0) return fail("enemy_LP must be > 0");
+  return 0;
+}
+
+template <class T>
+int dalloc(T** p, size_t n) {
+  HIP_OK(hipMalloc((void**)p, std::max<size_t>(n, 1) * sizeof(T)));
+  HIP_OK(hipMemset(*p, 0, std::max<size_t>(n, 1) * sizeof(T)));
+  return 0;
+}
+
+StepArgs base_args(td_handle* h) {
+  StepArgs a;
+  std::memset(&a, 0, sizeof a);
+  a.B = h->B; a.L = h->L; a.mode = h->mode; a.multi = h->multi; a.difficulty = h->difficulty;
+  a.autoreset = h->autoreset;
+  a.hdr = h->d_hdr; a.en_lp = h->d_en_lp; a.en_mg = h->d_en_mg; a.en_inf = h->d_en_inf;
+  a.tw_cd = h->d_tw_cd; a.tw_inf = h->d_tw_inf; a.cells = h->d_cells; a.opp_mt = h->d_opp;
+  a.nxt = h->d_nxt; a.consumed = h->d_consumed; a.cfg = h->d_cfg;
+  return a;
+}
+
+// Draw the next episode layout of board b from its numpy stream.  A draw whose
+// road generation fails (the reference raises / hangs) is skipped and the stream
+// continues; failures are counted.
+int gen_next(td_handle* h, int b, uint32_t* rec, std::vector<uint8_t>& scratch, bool retry) {
+  for (int tries = 0; tries < 64; ++tries) {
+    int st = episode_layout(&h->np_state[(size_t)b * (MT_N + 1)], h->L, scratch.data(), kMaxAttempts, rec);
+    if (st == ROAD_OK) return 0;
+    __atomic_fetch_add(&h->roadgen_failures, 1, __ATOMIC_RELAXED);
+    if (!retry) return st;
+  }
+  return ROAD_ERR_BOUND;
+}
+
+// fn(i, worker) for i in [0, n) on up to h->nthreads host threads.
+template <class F>
+void parallel_for(td_handle* h, int n, F fn) {
+  int nt = std::max(1, std::min(h->nthreads, (n + 7) / 8));
+  if (nt == 1) {
+    for (int i = 0; i < n; ++i) fn(i, 0);
+    return;
+  }
+  std::vector<std::thread> pool;
+  for (int w = 0; w < nt; ++w)
+    pool.emplace_back([&, w]() {
+      for (int i = w; i < n; i += nt) fn(i, w);
+    });
+  for (auto& t : pool) t.join();
+}
+
+// Stage the records of boards ids[0..n) from h_stage into their nxt slots.
+int stage(td_handle* h, int n, hipStream_t s) {
+  if (n <= 0) return 0;
+  HIP_OK(hipMemcpyAsync(h->d_stage, h->h_stage, (size_t)n * h->lw * 4, hipMemcpyHostToDevice, s));
+  HIP_OK(hipMemcpyAsync(h->d_stage_ids, h->h_stage_ids, (size_t)n * 4, hipMemcpyHostToDevice, s));
+  HIP_OK(launch_stage_layouts(h->d_nxt, h->d_stage, h->d_stage_ids, n, h->lw, s));
+  HIP_OK(hipEventRecord(h->ev_stage, s));
+  return 0;
+}
+
+// Top up the next-episode layouts of boards whose staged layout was consumed.
+int refill(td_handle* h, hipStream_t s) {
+  if (!h->consumed_pending) return 0;
+  if (hipEventQuery(h->ev_consumed) != hipSuccess) return 0;  // copy not landed yet: try later
+  h->consumed_pending = false;
+  std::vector<int> need;
+  for (int b = 0; b < h->B; ++b)
+    if (h->h_consumed[b] >= h->uploaded[b]) need.push_back(b);
+  if (need.empty()) return 0;
+  HIP_OK(hipEventSynchronize(h->ev_stage));  // previous staging copy done with h_stage
+  int n = (int)std::min<size_t>(need.size(), kRefillMax);
+  parallel_for(h, n, [&](int i, int w) {
+    int b = need[(size_t)i];
+    gen_next(h, b, h->h_stage + (size_t)i * h->lw, h->scratch[(size_t)w], true);
+    h->h_stage_ids[i] = b;
+  });
+  for (int i = 0; i < n; ++i) h->uploaded[need[i]] += 1;
+  return stage(h, n, s);
+}
+
+}  // namespace
+
+extern "C" {
+
+int td_abi_version(void) { return TD_ABI_VERSION; }
+
+const char* td_last_error(void) { return g_err.c_str(); }
+
+void td_config_default(td_config* c) {
+  // gym_TD/envs/TDParam.py:2-64, :105-111
+  std::memset(c, 0, sizeof *c);
+  const double lp[4][2] = {{820, 1700}, {2050, 3000}, {6000, 8000}, {8000, 12000}};
+  const double sp[4][2] = {{.25, .25}, {.13, .13}, {.1, .1}, {.1, .1}};
+  const double df[4][2] = {{0, 0}, {200, 250}, {600, 800}, {80, 100}};
+  const double ec[4][2] = {{8, 8}, {15, 15}, {40, 40}, {30, 30}};
+  const double ta[4][2] = {{454, 540}, {651, 771}, {566, 691}, {358, 424}};
+  const double tr[4][2] = {{3, 3}, {2, 2}, {4, 4}, {3, 3}};
+  const double ts[4][2] = {{0, 0}, {0, 0}, {1, 1}, {0, 0}};
+  const double tc[4][2] = {{10, 10}, {17, 17}, {23, 23}, {12, 12}};
+  const double ti[4][2] = {{2, 2}, {4, 4}, {7, 7}, {4.75, 4.75}};
+  std::memcpy(c->enemy_LP, lp, sizeof lp);
+  std::memcpy(c->enemy_speed, sp, sizeof sp);
+  std::memcpy(c->enemy_defense, df, sizeof df);
+  std::memcpy(c->enemy_cost, ec, sizeof ec);
+  std::memcpy(c->tower_attack, ta, sizeof ta);
+  std::memcpy(c->tower_range, tr, sizeof tr);
+  std::memcpy(c->tower_splash_range, ts, sizeof ts);
+  std::memcpy(c->tower_cost, tc, sizeof tc);
+  std::memcpy(c->tower_attack_interval, ti, sizeof ti);
+  c->tower_destruct_return = .5;
+  c->frozen_time = 2;
+  c->frozen_ratio = .2;
+  c->attacker_init_cost = 0;
+  c->defender_init_cost = 10;
+  c->base_LP = 5;
+  c->max_cost = 100;
+  c->reward_kill = 0.1;
+  c->penalty_leak = 10.;
+  c->reward_time = 0.001;
+  c->attacker_cost_init_rate = .5;
+  c->attacker_cost_final_rate = 1;
+  c->defender_cost_rate = .2;
+  c->tower_distance = 2;
+  c->enemy_upgrade_at = 0.75;
+  c->attacker_action_interval = 1;
+  c->defender_action_interval = 1;
+  c->max_enemy_lv = 1;
+  c->max_tower_lv = 1;
+  c->enemy_types = 4;
+  c->tower_types = 4;
+  c->max_episode_steps = 1200;
+  c->max_cluster_length = 8;
+  c->max_num_of_roads = 3;
+}
+
+td_handle* td_create(const td_config* cfg, int map_size, int n_boards, int mode, int multi_action, int difficulty,
+                     int device) {
+  if (!cfg) { fail("td_create: cfg is NULL"); return nullptr; }
+  if (check_cfg(*cfg)) return nullptr;
+  if (map_size < 4 || map_size > 32) { fail("map_size must be in [4, 32], got %d", map_size); return nullptr; }
+  if (n_boards < 1) { fail("n_boards must be >= 1"); return nullptr; }
+  if (mode < 0 || mode > 2) { fail("mode must be 0 (def), 1 (atk) or 2 (2p)"); return nullptr; }
+  if (mode == TD_MODE_DEF && (difficulty < 0 || difficulty > 1)) { fail("TD-def difficulty must be 0 or 1 (random_enemy_lv0/lv1)"); return nullptr; }
+  if (mode == TD_MODE_ATK && (difficulty < 0 || difficulty > 2)) { fail("TD-atk difficulty must be 0, 1 or 2 (random_tower_lv0/1/2)"); return nullptr; }
+  if (mode == TD_MODE_ATK && multi_action) { fail("TD-atk has no multi-action defender"); return nullptr; }
+  if (hipSetDevice(device) != hipSuccess) { fail("hipSetDevice(%d) failed", device); return nullptr; }
+  td_handle* h = new td_handle();
+  h->L = map_size; h->NC = map_size * map_size; h->B = n_boards; h->mode = mode; h->multi = multi_action ? 1 : 0;
+  h->difficulty = difficulty; h->device = device; h->lw = layout_words(map_size);
+  build_dev_cfg(*cfg, h->dcfg);
+  const size_t B = (size_t)n_boards;
+  int rc = 0;
+  rc |= dalloc(&h->d_cfg, 1);
+  rc |= dalloc(&h->d_hdr, B);
+  rc |= dalloc(&h->d_en_lp, B * ECAP);
+  rc |= dalloc(&h->d_en_mg, B * ECAP);
+  rc |= dalloc(&h->d_en_inf, B * ECAP);
+  rc |= dalloc(&h->d_tw_cd, B * TCAP);
+  rc |= dalloc(&h->d_tw_inf, B * TCAP);
+  rc |= dalloc(&h->d_cells, B * h->NC);
+  rc |= dalloc(&h->d_opp, B * (MT_N + 1));
+  rc |= dalloc(&h->d_nxt, B * h->lw);
+  rc |= dalloc(&h->d_consumed, B);
+  rc |= dalloc(&h->d_stage, (size_t)kRefillMax * h->lw);
+  rc |= dalloc(&h->d_stage_ids, (size_t)kRefillMax);
+  rc |= dalloc(&h->d_mask, B);
+  if (!rc && hipMemcpy(h->d_cfg, &h->dcfg, sizeof(TdDevCfg), hipMemcpyHostToDevice) != hipSuccess) rc = fail("cfg upload");
+  if (!rc && hipHostMalloc((void**)&h->h_consumed, B * 4, hipHostMallocDefault) != hipSuccess) rc = fail("pinned alloc");
+  if (!rc && hipHostMalloc((void**)&h->h_stage, (size_t)kRefillMax * h->lw * 4, hipHostMallocDefault) != hipSuccess) rc = fail("pinned alloc");
+  if (!rc && hipHostMalloc((void**)&h->h_stage_ids, (size_t)kRefillMax * 4, hipHostMallocDefault) != hipSuccess) rc = fail("pinned alloc");
+  if (!rc && hipEventCreateWithFlags(&h->ev_consumed, hipEventDisableTiming) != hipSuccess) rc = fail("event");
+  if (!rc && hipEventCreateWithFlags(&h->ev_stage, hipEventDisableTiming) != hipSuccess) rc = fail("event");
+  if (rc) { std::string e = g_err; td_destroy(h); g_err = e; return nullptr; }
+  h->np_state.assign(B * (MT_N + 1), 0u);
+  h->uploaded.assign(B, 0u);
+  {
+    const char* env = getenv("TD_HOST_THREADS");
+    unsigned hw = std::thread::hardware_concurrency();
+    h->nthreads = env ? atoi(env) : (int)std::min(8u, hw ? hw : 1u);
+    if (h->nthreads < 1) h->nthreads = 1;
+  }
+  h->scratch.resize((size_t)h->nthreads);
+  for (auto& s : h->scratch) s.resize(road_scratch_bytes(map_size));
+  std::vector<uint32_t> seeds(B);
+  for (size_t b = 0; b < B; ++b) seeds[b] = (uint32_t)b;
+  if (td_seed(h, seeds.data(), seeds.data()) != 0) { std::string e = g_err; td_destroy(h); g_err = e; return nullptr; }
+  return h;
+}
+
+void td_destroy(td_handle* h) {
+  if (!h) return;
+  (void)hipSetDevice(h->device);
+  (void)hipDeviceSynchronize();
+  void* dptrs[] = {h->d_cfg, h->d_hdr, h->d_en_lp, h->d_en_mg, h->d_en_inf, h->d_tw_cd, h->d_tw_inf, h->d_cells,
+                   h->d_opp, h->d_nxt, h->d_consumed, h->d_stage, h->d_stage_ids, h->d_mask};
+  for (void* p : dptrs)
+    if (p) (void)hipFree(p);
+  if (h->h_consumed) (void)hipHostFree(h->h_consumed);
+  if (h->h_stage) (void)hipHostFree(h->h_stage);
+  if (h->h_stage_ids) (void)hipHostFree(h->h_stage_ids);
+  if (h->ev_consumed) (void)hipEventDestroy(h->ev_consumed);
+  if (h->ev_stage) (void)hipEventDestroy(h->ev_stage);
+  delete h;
+}
+
+int td_set_config(td_handle* h, const td_config* cfg) {
+  if (!h || !cfg) return fail("td_set_config: NULL argument");
+  if (check_cfg(*cfg)) return -1;
+  build_dev_cfg(*cfg, h->dcfg);
+  HIP_OK(hipDeviceSynchronize());
+  HIP_OK(hipMemcpy(h->d_cfg, &h->dcfg, sizeof(TdDevCfg), hipMemcpyHostToDevice));
+  return 0;
+}
+
+int td_set_autoreset(td_handle* h, int on) {
+  if (!h) return fail("NULL handle");
+  h->autoreset = on ? 1 : 0;
+  return 0;
+}
+
+int td_seed(td_handle* h, const uint32_t* np_seeds, const uint32_t* py_seeds) {
+  if (!h) return fail("NULL handle");
+  const size_t B = (size_t)h->B, W = MT_N + 1;
+  if (np_seeds) {
+    for (size_t b = 0; b < B; ++b) np_seed(&h->np_state[b * W], np_seeds[b]);
+    // staged next layouts came from the old streams: drop them
+    HIP_OK(hipDeviceSynchronize());
+    HIP_OK(hipMemcpy(h->h_consumed, h->d_consumed, B * 4, hipMemcpyDeviceToHost));
+    for (size_t b = 0; b < B; ++b) h->uploaded[b] = h->h_consumed[b];
+    std::vector<uint32_t> zero(B * (size_t)h->lw, 0u);
+    HIP_OK(hipMemcpy(h->d_nxt, zero.data(), zero.size() * 4, hipMemcpyHostToDevice));
+    h->consumed_pending = false;
+  }
+  if (py_seeds) {
+    std::vector<uint32_t> opp(B * W);
+    parallel_for(h, (int)B, [&](int b, int) { py_seed(&opp[(size_t)b * W], py_seeds[b]); });
+    HIP_OK(hipDeviceSynchronize());
+    HIP_OK(hipMemcpy(h->d_opp, opp.data(), B * W * 4, hipMemcpyHostToDevice));
+  }
+  return 0;
+}
+
+int td_set_py_state(td_handle* h, int b, const uint32_t* mt) {
+  if (!h || b < 0 || b >= h->B) return fail("bad board");
+  HIP_OK(hipDeviceSynchronize());
+  HIP_OK(hipMemcpy(h->d_opp + (size_t)b * (MT_N + 1), mt, (MT_N + 1) * 4, hipMemcpyHostToDevice));
+  return 0;
+}
+
+int td_get_py_state(td_handle* h, int b, uint32_t* mt) {
+  if (!h || b < 0 || b >= h->B) return fail("bad board");
+  HIP_OK(hipDeviceSynchronize());
+  HIP_OK(hipMemcpy(mt, h->d_opp + (size_t)b * (MT_N + 1), (MT_N + 1) * 4, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int td_set_np_state(td_handle* h, int b, const uint32_t* mt) {
+  if (!h || b < 0 || b >= h->B) return fail("bad board");
+  std::memcpy(&h->np_state[(size_t)b * (MT_N + 1)], mt, (MT_N + 1) * 4);
+  // a staged next layout was drawn from the old stream: drop it
+  HIP_OK(hipDeviceSynchronize());
+  uint32_t c = 0;
+  HIP_OK(hipMemcpy(&c, h->d_consumed + b, 4, hipMemcpyDeviceToHost));
+  h->uploaded[(size_t)b] = c;
+  uint32_t zero = 0;
+  HIP_OK(hipMemcpy(h->d_nxt + (size_t)b * h->lw, &zero, 4, hipMemcpyHostToDevice));
+  return 0;
+}
+
+int td_get_np_state(td_handle* h, int b, uint32_t* mt) {
+  if (!h || b < 0 || b >= h->B) return fail("bad board");
+  std::memcpy(mt, &h->np_state[(size_t)b * (MT_N + 1)], (MT_N + 1) * 4);
+  return 0;
+}
+
+// Stage records h_stage[0..n) (board ids in h_stage_ids) into the next-layout slots.
+static int stage_sync(td_handle* h, int n, hipStream_t s) {
+  if (stage(h, n, s)) return -1;
+  HIP_OK(hipStreamSynchronize(s));
+  return 0;
+}
+
+// Run the reset kernel on the boards with mask[b] != 0 (their staged layout is consumed).
+static int run_reset(td_handle* h, const std::vector<uint8_t>& mask, float* obs, hipStream_t s) {
+  HIP_OK(hipMemcpy(h->d_mask, mask.data(), (size_t)h->B, hipMemcpyHostToDevice));
+  StepArgs a = base_args(h);
+  a.obs = obs;
+  a.reset_mask = h->d_mask;
+  HIP_OK(launch_step(a, s, true));
+  HIP_OK(hipStreamSynchronize(s));
+  return 0;
+}
+
+// Generate (one draw sequence each, from the boards' numpy streams) and stage the
+// next-episode layout of boards ``bs``; returns the boards that failed (no retry)
+// or 0 with ``retry``.
+static int gen_and_stage(td_handle* h, const std::vector<int>& bs, bool retry, std::vector<int>* failed, hipStream_t s) {
+  for (size_t j0 = 0; j0 < bs.size(); j0 += kRefillMax) {
+    int m = (int)std::min<size_t>(kRefillMax, bs.size() - j0);
+    std::vector<int> st((size_t)m);
+    parallel_for(h, m, [&](int j, int w) {
+      st[(size_t)j] = gen_next(h, bs[j0 + j], h->h_stage + (size_t)j * h->lw, h->scratch[(size_t)w], retry);
+    });
+    int k = 0;
+    for (int j = 0; j < m; ++j) {
+      int b = bs[j0 + j];
+      if (st[(size_t)j] != ROAD_OK) { if (failed) failed->push_back(b); continue; }
+      if (k != j) std::memcpy(h->h_stage + (size_t)k * h->lw, h->h_stage + (size_t)j * h->lw, (size_t)h->lw * 4);
+      h->h_stage_ids[k++] = b;
+      h->uploaded[(size_t)b] += 1;
+    }
+    if (stage_sync(h, k, s)) return -1;
+  }
+  return 0;
+}
+
+int td_reset(td_handle* h, const uint8_t* host_mask, float* obs, void* stream) {
+  if (!h) return fail("NULL handle");
+  hipStream_t s = (hipStream_t)stream;
+  HIP_OK(hipDeviceSynchronize());
+  HIP_OK(hipMemcpy(h->h_consumed, h->d_consumed, (size_t)h->B * 4, hipMemcpyDeviceToHost));
+  h->consumed_pending = false;
+  std::vector<int> ids, gen;
+  for (int b = 0; b < h->B; ++b) {
+    if (host_mask && !host_mask[b]) continue;
+    ids.push_back(b);
+    // TDGymBasic.reset draws the layout that follows on the board's stream: the
+    // staged one when present, otherwise a fresh draw now.
+    if (h->h_consumed[b] >= h->uploaded[(size_t)b]) gen.push_back(b);
+  }
+  std::vector<int> failed;
+  if (gen_and_stage(h, gen, false, &failed, s)) return -1;
+  h->last_reset_failed.assign(failed.begin(), failed.end());
+  std::vector<uint8_t> mask((size_t)h->B, 0);
+  for (int b : ids) mask[(size_t)b] = 1;
+  for (int b : failed) mask[(size_t)b] = 0;
+  std::vector<int> done;
+  for (int b : ids) if (mask[(size_t)b]) done.push_back(b);
+  if (!done.empty() && run_reset(h, mask, obs, s)) return -1;
+  // the layout for the episode after this one, consumed by the auto-reset
+  if (gen_and_stage(h, done, true, nullptr, s)) return -1;
+  return (int)failed.size();
+}
+
+int td_last_reset_failures(td_handle* h, int32_t* boards, int cap) {
+  if (!h) return fail("NULL handle");
+  int n = (int)h->last_reset_failed.size();
+  for (int i = 0; i < n && i < cap && boards; ++i) boards[i] = h->last_reset_failed[(size_t)i];
+  return n;
+}
+
+int td_reset_layouts(td_handle* h, const uint32_t* recs, const int32_t* boards, int n, float* obs, void* stream) {
+  if (!h || (n > 0 && (!recs || !boards))) return fail("td_reset_layouts: bad arguments");
+  hipStream_t s = (hipStream_t)stream;
+  for (int i = 0; i < n; ++i)
+    if (boards[i] < 0 || boards[i] >= h->B || recs[(size_t)i * h->lw] != TD_LAYOUT_MAGIC)
+      return fail("td_reset_layouts: bad board id or layout record %d", i);
+  HIP_OK(hipDeviceSynchronize());
+  std::vector<uint8_t> mask((size_t)h->B, 0);
+  for (int i0 = 0; i0 < n; i0 += kRefillMax) {
+    int m = std::min(kRefillMax, n - i0);
+    std::memcpy(h->h_stage, recs + (size_t)i0 * h->lw, (size_t)m * h->lw * 4);
+    std::memcpy(h->h_stage_ids, boards + i0, (size_t)m * 4);
+    if (stage_sync(h, m, s)) return -1;
+  }
+  for (int i = 0; i < n; ++i) mask[(size_t)boards[i]] = 1;
+  if (n > 0 && run_reset(h, mask, obs, s)) return -1;
+  // explicit layouts leave no staged next layout: the next refill draws from the stream
+  HIP_OK(hipMemcpy(h->h_consumed, h->d_consumed, (size_t)h->B * 4, hipMemcpyDeviceToHost));
+  for (int i = 0; i < n; ++i) h->uploaded[(size_t)boards[i]] = h->h_consumed[boards[i]];
+  h->consumed_pending = false;
+  return 0;
+}
+
+int td_step(td_handle* h, const td_step_io* io, void* stream) {
+  if (!h || !io) return fail("td_step: NULL argument");
+  if (!io->obs || !io->reward || !io->done) return fail("td_step: obs, reward and done are required");
+  if (h->mode != TD_MODE_ATK && !io->def_act) return fail("td_step: def_act required in this mode");
+  if (h->mode != TD_MODE_DEF && !io->atk_act) return fail("td_step: atk_act required in this mode");
+  hipStream_t s = (hipStream_t)stream;
+  if (h->autoreset && refill(h, s)) return -1;
+  StepArgs a = base_args(h);
+  a.def_act = io->def_act; a.atk_act = io->atk_act; a.obs = io->obs; a.reward = io->reward; a.done = io->done;
+  a.real_def = io->real_def; a.real_atk = io->real_atk; a.fail_def = io->fail_def; a.fail_atk = io->fail_atk;
+  a.win = io->win; a.allow_next = io->allow_next; a.ep_return = io->ep_return; a.ep_len = io->ep_len;
+  HIP_OK(launch_step(a, s, false));
+  h->steps += 1;
+  if (h->autoreset && !h->consumed_pending && (h->steps % kRefillEvery) == 0) {
+    HIP_OK(hipMemcpyAsync(h->h_consumed, h->d_consumed, (size_t)h->B * 4, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipEventRecord(h->ev_consumed, s));
+    h->consumed_pending = true;
+  }
+  return 0;
+}
+
+int td_layout_words(int map_size) { return layout_words(map_size); }
+
+int td_layout_from_roads(int map_size, int num_roads, const int32_t* cells, const int32_t* offsets, uint32_t* rec) {
+  int st = layout_from_roads(map_size, num_roads, cells, offsets, rec);
+  return st == ROAD_OK ? 0 : fail("td_layout_from_roads: invalid roads (status %d)", st);
+}
+
+int td_layout_generate(uint32_t* np_state625, int map_size, int max_attempts, uint32_t* rec) {
+  if (map_size < 4 || map_size > MAX_L) return fail("map_size out of range");
+  std::vector<uint8_t> scratch(road_scratch_bytes(map_size));
+  return episode_layout(np_state625, map_size, scratch.data(), max_attempts > 0 ? max_attempts : kMaxAttempts, rec);
+}
+
+size_t td_state_bytes(td_handle* h, int count) {
+  if (!h || count < 0) return 0;
+  return (size_t)count * (sizeof(TdHdr) + ECAP * (8 + 8 + 4) + TCAP * (8 + 4) + (size_t)h->NC * 4 + (MT_N + 1) * 4);
+}
+
+static int state_copy(td_handle* h, int b0, int count, void* host, bool to_host) {
+  if (!h || b0 < 0 || count < 0 || b0 + count > h->B) return fail("state copy: bad board range");
+  HIP_OK(hipDeviceSynchronize());
+  uint8_t* p = (uint8_t*)host;
+  auto cp = [&](void* dev, size_t elem) -> int {
+    size_t bytes = (size_t)count * elem;
+    uint8_t* d = (uint8_t*)dev + (size_t)b0 * elem;
+    HIP_OK(hipMemcpy(to_host ? (void*)p : (void*)d, to_host ? (void*)d : (void*)p, bytes,
+                     to_host ? hipMemcpyDeviceToHost : hipMemcpyHostToDevice));
+    p += bytes;
+    return 0;
+  };
+  if (cp(h->d_hdr, sizeof(TdHdr)) || cp(h->d_en_lp, ECAP * 8) || cp(h->d_en_mg, ECAP * 8) ||
+      cp(h->d_en_inf, ECAP * 4) || cp(h->d_tw_cd, TCAP * 8) || cp(h->d_tw_inf, TCAP * 4) ||
+      cp(h->d_cells, (size_t)h->NC * 4) || cp(h->d_opp, (MT_N + 1) * 4))
+    return -1;
+  return 0;
+}
+
+int td_export_state(td_handle* h, int b0, int count, void* host_dst) { return state_copy(h, b0, count, host_dst, true); }
+
+int td_import_state(td_handle* h, int b0, int count, const void* host_src) {
+  return state_copy(h, b0, count, const_cast<void*>(host_src), false);
+}
+
+int td_get_flags(td_handle* h, int32_t* host_flags) {
+  if (!h || !host_flags) return fail("td_get_flags: NULL argument");
+  std::vector<TdHdr> hdr((size_t)h->B);
+  HIP_OK(hipDeviceSynchronize());
+  HIP_OK(hipMemcpy(hdr.data(), h->d_hdr, hdr.size() * sizeof(TdHdr), hipMemcpyDeviceToHost));
+  for (int b = 0; b < h->B; ++b) host_flags[b] = hdr[(size_t)b].flags;
+  return 0;
+}
+
+void td_py_seed(uint32_t* mt, uint32_t seed) { py_seed(mt, seed); }
+void td_np_seed(uint32_t* mt, uint32_t seed) { np_seed(mt, seed); }
+uint32_t td_mt_next(uint32_t* mt) { return MtRef{mt}.next(); }
+int64_t td_py_randint(uint32_t* mt, int64_t a, int64_t b) { return MtRef{mt}.py_randint(a, b); }
+int64_t td_np_randint(uint32_t* mt, int64_t lo, int64_t hi) { return MtRef{mt}.np_randint(lo, hi); }
+
+}  // extern "C"

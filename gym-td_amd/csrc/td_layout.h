@@ -1,0 +1,284 @@
+// td_layout.h -- per-episode board layout: road generation and the packed
+// layout record shared by host and device.
+//
+// Road generation restates create_road_v2 (TDRoadGen.py:4-199) draw for draw on a
+// numpy-legacy MT19937 stream (td_rng.h), so a board seeded with RandomState(s)
+// gets the reference's exact roads.  The reference's three ``while not succ``
+// loops are unbounded (TDRoadGen.py:129,142,177) and can raise (ValueError at
+// :178, IndexError at :189); here every loop is bounded and each failure mode is
+// a status code.
+//
+// Layout record (uint32 words), the unit the device resets a board from:
+//   [0] TD_LAYOUT_MAGIC   [1] num_roads   [2] end cell   [3] max dist
+//   [4..6] start cell of road 0..2 (row*L+col)  [7] status
+//   [8 + cell] cell word:
+//      bits 0-3  road planes (map[0], map[1..3])       TDBoard.py:41-42
+//      bit  4    end point                              TDBoard.py:114
+//      bits 5-7  start point of road 0..2               TDBoard.py:119-120
+//      bits 8-9  next direction map[5] (0:+c 1:-c 2:+r 3:-r)  TDBoard.py:44-54
+//      bits 16-23 distance to end map[4]                TDBoard.py:56-59
+//      bits 24-31 build-block counter map[6] (=1 on road at reset)  TDBoard.py:43
+#pragma once
+#include <stdint.h>
+#include "td_rng.h"
+
+namespace td {
+
+constexpr uint32_t TD_LAYOUT_MAGIC = 0x7D1A0001u;
+constexpr int LAYOUT_HDR = 8;
+constexpr int MAX_L = 64;
+
+enum RoadStatus : int {
+  ROAD_OK = 0,
+  ROAD_ERR_RANDINT = 1,   // ValueError at TDRoadGen.py:178 (empty pick range)
+  ROAD_ERR_EMPTY = 2,     // IndexError at TDRoadGen.py:189 (branch road of length 0)
+  ROAD_ERR_BOUND = 3,     // retry bound exceeded (the reference loops forever)
+  ROAD_ERR_ARGS = 4,
+};
+
+TD_HD inline int layout_words(int L) { return LAYOUT_HDR + L * L; }
+
+// Scratch for one road generation: 14 * L * L bytes.
+struct RoadScratch {
+  uint8_t* field;   // [NC]
+  uint8_t* rot;     // [NC]
+  uint16_t* r1;     // [NC] center -> end
+  uint16_t* r2;     // [NC] center -> start
+  uint16_t* rb;     // [NC] branch
+  uint16_t* mainr;  // [NC]
+  uint32_t* picks;  // [NC] (index << 16) | cell
+};
+
+TD_HD inline size_t road_scratch_bytes(int L) { return (size_t)L * L * 14 + 64; }
+
+TD_HD inline RoadScratch road_scratch_carve(void* base, int L) {
+  int nc = L * L;
+  RoadScratch s;
+  uint8_t* p = (uint8_t*)base;
+  s.picks = (uint32_t*)p; p += 4 * nc;
+  s.r1 = (uint16_t*)p; p += 2 * nc;
+  s.r2 = (uint16_t*)p; p += 2 * nc;
+  s.rb = (uint16_t*)p; p += 2 * nc;
+  s.mainr = (uint16_t*)p; p += 2 * nc;
+  s.field = p; p += nc;
+  s.rot = p;
+  return s;
+}
+
+struct RoadGen {
+  MtRef rng;
+  int L;
+  RoadScratch s;
+  int max_attempts;
+
+  TD_HD bool inner(int r, int c) const { return r > 0 && r < L - 1 && c > 0 && c < L - 1; }
+
+  // generate_road (TDRoadGen.py:31-119): walk from (r0,c0) in direction d.
+  // Returns 1 on success, 0 on failure; *len = cells appended to out.
+  TD_HD int walk(int r0, int c0, int d, uint16_t* out, int* len) {
+    const int DR[4] = {1, 0, -1, 0}, DC[4] = {0, -1, 0, 1};  // :15 up,left,down,right
+    int pr = r0, pc = c0, n = 0, pending = 0, loop = 0;  // pending: 0 = None, else +-1
+    while (inner(pr, pc) && loop < 100) {
+      ++loop;
+      int shape = (int)rng.np_randint(0, 2);
+      int seg = (int)rng.np_randint(L * 3 / 20, L / 4);
+      bool cross = false;
+      // one run of moves; reset_cross mirrors the `cross = False` at :98
+      auto run = [&](int cnt, int dd, bool reset_cross) {
+        for (int k = 0; k < cnt; ++k) {
+          pr += DR[dd]; pc += DC[dd];
+          if (s.field[pr * L + pc] != 0) { pr -= DR[dd]; pc -= DC[dd]; cross = true; return; }
+          if (reset_cross) cross = false;
+          out[n++] = (uint16_t)(pr * L + pc);
+          s.field[pr * L + pc] = 1;
+          if (!inner(pr, pc)) return;
+        }
+      };
+      if (shape <= 0) {
+        run(seg * 2, d, false);
+      } else {
+        run(seg, d, false);
+        if (!inner(pr, pc)) break;
+        int rd;
+        if (pending != 0) { rd = pending; pending = 0; }
+        else { rd = (int)rng.np_randint(0, 2) * 2 - 1; pending = -rd; }
+        s.rot[pr * L + pc] = 1;
+        d = (d + 4 + rd) % 4;
+        run(seg, d, true);
+      }
+      if (cross) {
+        int freed[4], nf = 0;
+        for (int i = 0; i < 4; ++i)
+          if (s.field[(pr + DR[i]) * L + pc + DC[i]] == 0) freed[nf++] = i;
+        if (nf == 0) { *len = n; return 0; }
+        d = freed[rng.np_randint(0, nf)];
+        pending = 0;
+        s.rot[pr * L + pc] = 1;
+      }
+    }
+    *len = n;
+    return loop >= 100 ? 0 : 1;
+  }
+
+  TD_HD void erase(const uint16_t* road, int n) {
+    for (int i = 0; i < n; ++i) { s.field[road[i]] = 0; s.rot[road[i]] = 0; }
+  }
+
+  static TD_HD int iabs(int x) { return x < 0 ? -x : x; }
+
+  // create_road_v2 + TDBoard map planes; writes the layout record ``rec``.
+  TD_HD int generate(int num_roads, uint32_t* rec) {
+    if (L < 4 || L > MAX_L || num_roads < 1 || num_roads > 3) return ROAD_ERR_ARGS;
+    if (L / 4 <= L * 3 / 20) return ROAD_ERR_RANDINT;  // segment randint raises (TDRoadGen.py:41)
+    const int NC = L * L;
+    for (int i = 0; i < NC; ++i) { s.field[i] = 0; s.rot[i] = 0; }
+    int lo = L / 3, hi = (L * 2 + 2) / 3;
+    int cr = (int)rng.np_randint(lo, hi), cc = (int)rng.np_randint(lo, hi);
+    s.field[cr * L + cc] = 1;
+    int d0 = (int)rng.np_randint(0, 4);
+    int n1 = 0, n2 = 0, att;
+    for (att = 0;; ++att) {  // :128-137
+      if (att >= max_attempts) return ROAD_ERR_BOUND;
+      int ok = walk(cr, cc, d0, s.r1, &n1);
+      if (!ok || n1 >= L) { erase(s.r1, n1); continue; }
+      break;
+    }
+    for (att = 0;; ++att) {  // :141-155
+      if (att >= max_attempts) return ROAD_ERR_BOUND;
+      int ok = walk(cr, cc, (d0 + 2) % 4, s.r2, &n2);
+      if (!ok || n1 + n2 + 1 >= L * 2) { erase(s.r2, n2); continue; }
+      int e2 = s.r2[n2 - 1], e1 = s.r1[n1 - 1];
+      if (iabs(e2 / L - e1 / L) + iabs(e2 % L - e1 % L) < L * 3 / 4) { erase(s.r2, n2); continue; }
+      break;
+    }
+    int nm = 0;  // main = reversed(road2) + [center] + road1  (:157-158)
+    for (int i = n2 - 1; i >= 0; --i) s.mainr[nm++] = s.r2[i];
+    s.mainr[nm++] = (uint16_t)(cr * L + cc);
+    for (int i = 0; i < n1; ++i) s.mainr[nm++] = s.r1[i];
+    int np = 0;  // selectable (:162-170)
+    for (int i = 0; i < nm;) {
+      if (!s.rot[s.mainr[i]]) {
+        if (i < nm - 1 && !s.rot[s.mainr[i + 1]]) s.picks[np++] = ((uint32_t)i << 16) | s.mainr[i];
+        i += 1;
+      } else {
+        i += 2;
+      }
+    }
+    // map planes from main road first (roads[0])
+    for (int i = 0; i < NC; ++i) rec[LAYOUT_HDR + i] = 0;
+    uint32_t* cw = rec + LAYOUT_HDR;
+    int maxdist = 0;
+    int starts[3] = {0, 0, 0};
+    stamp_road(cw, s.mainr, nm, 0, nullptr, 0, &maxdist);
+    starts[0] = s.mainr[0];
+    int endc = s.mainr[nm - 1];
+    for (int ri = 1; ri < num_roads; ++ri) {  // :174-197
+      int k = 0, nb = 0;
+      for (att = 0;; ++att) {
+        if (att >= max_attempts) return ROAD_ERR_BOUND;
+        int klo = np * 2 / 5, khi = np * 4 / 5;
+        if (khi <= klo) return ROAD_ERR_RANDINT;
+        k = (int)rng.np_randint(klo, khi);
+        int nd = (int)rng.np_randint(0, 4);
+        int bcell = s.picks[k] & 0xffffu;
+        k = (int)(s.picks[k] >> 16);
+        int ok = walk(bcell / L, bcell % L, nd, s.rb, &nb);
+        if (!ok) { erase(s.rb, nb); continue; }
+        if (nb + nm - k >= L * 2) { erase(s.rb, nb); continue; }
+        if (nb == 0) return ROAD_ERR_EMPTY;
+        int eb = s.rb[nb - 1];
+        if (iabs(eb / L - endc / L) + iabs(eb % L - endc % L) < L * 3 / 4) { erase(s.rb, nb); continue; }
+        break;
+      }
+      // road = reversed(branch) + main[k:]
+      for (int i = 0; i < nb / 2; ++i) { uint16_t t = s.rb[i]; s.rb[i] = s.rb[nb - 1 - i]; s.rb[nb - 1 - i] = t; }
+      stamp_road(cw, s.rb, nb, ri, s.mainr + k, nm - k, &maxdist);
+      starts[ri] = nb > 0 ? s.rb[0] : s.mainr[k];
+    }
+    for (int ri = 0; ri < num_roads; ++ri) cw[starts[ri]] |= 1u << (5 + ri);
+    cw[endc] |= 1u << 4;
+    rec[0] = TD_LAYOUT_MAGIC;
+    rec[1] = (uint32_t)num_roads;
+    rec[2] = (uint32_t)endc;
+    rec[3] = (uint32_t)maxdist;
+    rec[4] = (uint32_t)starts[0];
+    rec[5] = (uint32_t)starts[1];
+    rec[6] = (uint32_t)starts[2];
+    rec[7] = ROAD_OK;
+    return ROAD_OK;
+  }
+
+  // One road's cells: rd[0..n) then tail[0..nt).  TDBoard.py:38-59.
+  TD_HD void stamp_road(uint32_t* cw, const uint16_t* rd, int n, int ri, const uint16_t* tail, int nt, int* maxdist) {
+    int tot = n + nt, prev = -1;
+    for (int k = 0; k < tot; ++k) {
+      int p = k < n ? rd[k] : tail[k - n];
+      uint32_t w = cw[p] | 1u | (1u << (1 + ri));
+      w = (w & 0x00ffffffu) | (1u << 24);
+      int dist = tot - 1 - k;
+      w = (w & ~(0xffu << 16)) | ((uint32_t)dist << 16);
+      cw[p] = w;
+      if (prev >= 0) {
+        int dr = p / L - prev / L, dc = p % L - prev % L;
+        uint32_t dir = dr == 0 ? (dc == 1 ? 0u : 1u) : (dr == 1 ? 2u : 3u);
+        cw[prev] = (cw[prev] & ~(3u << 8)) | (dir << 8);
+      }
+      if (dist > *maxdist) *maxdist = dist;
+      prev = p;
+    }
+  }
+};
+
+// Build a layout record from explicit road cell lists (road i = cells[off[i] .. off[i+1])),
+// exactly as TDBoard.__init__ fills its map planes (TDBoard.py:31-59).
+TD_HD inline int layout_from_roads(int L, int num_roads, const int32_t* cells, const int32_t* off, uint32_t* rec) {
+  if (L < 2 || L > MAX_L || num_roads < 1 || num_roads > 3) return ROAD_ERR_ARGS;
+  for (int i = 0; i < L * L; ++i) rec[LAYOUT_HDR + i] = 0;
+  uint32_t* cw = rec + LAYOUT_HDR;
+  int maxdist = 0;
+  for (int ri = 0; ri < num_roads; ++ri) {
+    int a = off[ri], b = off[ri + 1], prev = -1;
+    if (b <= a) return ROAD_ERR_ARGS;
+    for (int k = a; k < b; ++k) {
+      int p = cells[k];
+      if (p < 0 || p >= L * L) return ROAD_ERR_ARGS;
+      uint32_t w = cw[p] | 1u | (1u << (1 + ri));
+      w = (w & 0x00ffffffu) | (1u << 24);
+      int dist = b - 1 - k;
+      w = (w & ~(0xffu << 16)) | ((uint32_t)dist << 16);
+      cw[p] = w;
+      if (prev >= 0) {
+        int dr = p / L - prev / L, dc = p % L - prev % L;
+        uint32_t dir = dr == 0 ? (dc == 1 ? 0u : 1u) : (dr == 1 ? 2u : 3u);
+        cw[prev] = (cw[prev] & ~(3u << 8)) | (dir << 8);
+      }
+      if (dist > maxdist) maxdist = dist;
+      prev = p;
+    }
+  }
+  for (int ri = 0; ri < num_roads; ++ri) cw[cells[off[ri]]] |= 1u << (5 + ri);
+  int endc = cells[off[1] - 1];
+  cw[endc] |= 1u << 4;
+  rec[0] = TD_LAYOUT_MAGIC;
+  rec[1] = (uint32_t)num_roads;
+  rec[2] = (uint32_t)endc;
+  rec[3] = (uint32_t)maxdist;
+  for (int ri = 0; ri < 3; ++ri) rec[4 + ri] = ri < num_roads ? (uint32_t)cells[off[ri]] : 0u;
+  rec[7] = ROAD_OK;
+  return ROAD_OK;
+}
+
+// TDGymBasic.reset (:42-51): num_roads = randint(1, 4) then create_road_v2, on one stream.
+TD_HD inline int episode_layout(uint32_t* np_state, int L, void* scratch, int max_attempts, uint32_t* rec) {
+  RoadGen g;
+  g.rng.w = np_state;
+  g.L = L;
+  g.s = road_scratch_carve(scratch, L);
+  g.max_attempts = max_attempts;
+  int nr = (int)g.rng.np_randint(1, 4);
+  int st = g.generate(nr, rec);
+  if (st != ROAD_OK) { rec[0] = 0; rec[1] = (uint32_t)nr; rec[7] = (uint32_t)st; }
+  return st;
+}
+
+}  // namespace td

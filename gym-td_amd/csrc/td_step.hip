@@ -1,0 +1,974 @@
+// td_step.hip -- the batched gym-TD step on CDNA4 (gfx950).
+//
+// One 64-lane wavefront (= one workgroup) owns one board for the whole step:
+// the board's slice of the SoA record is staged in LDS, every serial phase of the
+// reference runs wave-uniform with wave ballots standing in for the reference's
+// "first enemy in list order" scans, and the (45, L, L) float32 observation is
+// written with 16-byte coalesced stores straight from LDS tables.
+//
+// Reference order of one env step:
+//   cool-downs                     TDDefense.py:38-39 / TDAttack.py:31-32 / TDMulti.py:50-51
+//   defender action                TDDefense.py:40-77, TDMulti.py:208-258
+//   attacker action / opponent     TDGymBasic.py:81-108, TDAttack.py:36-48, TDMulti.py:199-241
+//   TDBoard.step                   TDBoard.py:295-368
+//   done / get_states / info       TDBoard.py:370-385, 85-144, TDDefense.py:81-87
+//
+// Floating point: the file is compiled with -ffp-contract=off and every f64/f32
+// operation is an explicit correctly-rounded intrinsic where the reference's
+// Python/numpy rounding order matters.
+#include <hip/hip_runtime.h>
+
+#include "td_kernels.h"
+#include "td_layout.h"
+#include "td_rng.h"
+
+namespace td {
+
+enum : int { FC_OK = 0, FC_COST = 1, FC_POS = 2, FC_LVMAX = 3, FC_TARGET = 4, FC_CAP = 6 };  // utils/fail_code.py
+
+// ---------------------------------------------------------------------------
+// exact-rounding helpers (Python float / numpy float32 semantics)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double dadd(double a, double b) { return __dadd_rn(a, b); }
+__device__ __forceinline__ double dsub(double a, double b) { return __dsub_rn(a, b); }
+__device__ __forceinline__ double dmul(double a, double b) { return __dmul_rn(a, b); }
+__device__ __forceinline__ double ddiv(double a, double b) { return __ddiv_rn(a, b); }
+__device__ __forceinline__ double pymin(double a, double b) { return b < a ? b : a; }  // min(a, b)
+__device__ __forceinline__ float f32(double x) { return __double2float_rn(x); }
+
+__device__ __forceinline__ int ctz64(uint64_t m) { return __builtin_ctzll(m); }
+__device__ __forceinline__ int popc64(uint64_t m) { return __popcll(m); }
+__device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+
+// ---------------------------------------------------------------------------
+// per-board LDS image
+// ---------------------------------------------------------------------------
+template <int NC>
+struct Smem {
+  uint32_t cell[NC];      // cell words (td_layout.h)
+  uint8_t twr[NC];        // tower at cell: 0 none, else 0x80 | lv << 2 | type
+  uint8_t grp[4][NC];     // enemy group (head enemy index) per (type, cell), 0xFF none
+  double eLP[ECAP];
+  double eMg[ECAP];
+  uint32_t eInf[ECAP];
+  float eR[ECAP];         // f32(LP / maxLP)
+  union {
+    double key[ECAP];     // sort keys
+    float gst[ECAP][4];   // group stats: min, max, avg, count/8
+    uint32_t scratch[4 * ECAP];
+  };
+  double tCd[TCAP];
+  uint32_t tInf[TCAP];
+  float chv[48];          // broadcast channel values
+  float d9[256];          // channel 9 by distance
+};
+
+// Wave-uniform scalar board state (identical in every lane).
+struct U {
+  double cost_def, cost_atk, ep_ret, progress;
+  int steps, base_LP, atk_cd, def_cd, n, nt, num_roads, end_cell, maxdist, flags, episodes;
+  int start[3];
+};
+
+struct Ctx {
+  const TdDevCfg& C;
+  int L, NCr, lane;
+};
+
+// ---------------------------------------------------------------------------
+// CPython MT19937 for the built-in opponent, state in HBM, wave-parallel twist
+// ---------------------------------------------------------------------------
+struct WaveMt {
+  uint32_t* w;
+  uint32_t pos;
+  int lane;
+  __device__ void twist() {
+    // chunks of 64 in index order: w[i+1] and w[i+397] (i < 227) are still old,
+    // w[i-227] (i >= 227) was rewritten by an earlier chunk -- the sequential result.
+    for (int base = 0; base < MT_N; base += 64) {
+      int i = base + lane;
+      uint32_t nv = 0;
+      if (i < MT_N) {
+        uint32_t y = (w[i] & 0x80000000u) | (w[(i + 1) % MT_N] & 0x7fffffffu);
+        nv = w[(i + MT_M) % MT_N] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+      }
+      __syncthreads();
+      if (i < MT_N) w[i] = nv;
+      __threadfence_block();
+      __syncthreads();
+    }
+  }
+  __device__ uint32_t next() {
+    if (pos >= (uint32_t)MT_N) { twist(); pos = 0; }
+    uint32_t y = w[pos];
+    ++pos;
+    return mt_temper(y);
+  }
+  __device__ int64_t randbelow(int64_t n) {
+    int k = 64 - __builtin_clzll((unsigned long long)n);
+    uint32_t r = next() >> (32 - k);
+    while ((int64_t)r >= n) r = next() >> (32 - k);
+    return r;
+  }
+  __device__ int64_t randint(int64_t a, int64_t b) { return a + randbelow(b - a + 1); }
+  __device__ double random() {
+    uint32_t x = next() >> 5, y = next() >> 6;
+    return (x * 67108864.0 + y) * (1.0 / 9007199254740992.0);
+  }
+};
+
+// ---------------------------------------------------------------------------
+// defender operations (TDBoard.py:226-293), wave-uniform
+// ---------------------------------------------------------------------------
+template <int NC>
+__device__ void diamond(Smem<NC>& S, const Ctx& x, int cell, int delta) {
+  const int k = x.C.tower_distance, W = 2 * k + 1, L = x.L;
+  const int r0 = cell / L, c0 = cell % L;
+  for (int idx = x.lane; idx < W * W; idx += 64) {
+    int i = idx / W - k, j = idx % W - k;
+    int ai = i < 0 ? -i : i, aj = j < 0 ? -j : j;
+    int r = r0 + i, c = c0 + j;
+    if (ai + aj <= k && r >= 0 && r < L && c >= 0 && c < L) {
+      uint32_t w = S.cell[r * L + c];
+      int cnt = (int)(w >> 24) + delta;
+      S.cell[r * L + c] = (w & 0x00ffffffu) | ((uint32_t)(cnt & 0xff) << 24);
+    }
+  }
+  __syncthreads();
+}
+
+template <int NC>
+__device__ int tower_build(Smem<NC>& S, U& u, const Ctx& x, int t, int cell) {
+  const double price = x.C.t_price[t][0];
+  if (u.cost_def < price) return FC_COST;                 // :228
+  if (cw_block(S.cell[cell]) > 0) return FC_POS;          // :232
+  if (u.nt >= TCAP) { u.flags |= FLAG_TW_OVERFLOW; return FC_CAP; }
+  if (x.lane == 0) {
+    S.tInf[u.nt] = tw_pack(cell, t, 0);
+    S.tCd[u.nt] = 0.0;
+    S.twr[cell] = (uint8_t)(0x80 | t);
+  }
+  u.nt += 1;
+  u.cost_def = dsub(u.cost_def, price);                   // :238
+  __syncthreads();
+  diamond(S, x, cell, +1);                                // :239-245
+  return FC_OK;
+}
+
+template <int NC>
+__device__ int find_tower(Smem<NC>& S, const U& u, const Ctx& x, int cell) {
+  bool hit = x.lane < u.nt && (int)(S.tInf[x.lane] & 0xfffu) == cell;
+  uint64_t m = ballot(hit);
+  return m ? ctz64(m) : -1;
+}
+
+template <int NC>
+__device__ int tower_lvup(Smem<NC>& S, U& u, const Ctx& x, int cell) {
+  int k = find_tower(S, u, x, cell);
+  if (k < 0) return FC_TARGET;                            // :269-271
+  uint32_t ti = S.tInf[k];
+  int t = (ti >> 12) & 3, lv = (ti >> 14) & 1;
+  if (lv >= x.C.max_tower_lv) return FC_LVMAX;            // :252
+  double price = x.C.t_price[t][lv + 1];                  // :256
+  if (u.cost_def < price) return FC_COST;
+  __syncthreads();
+  if (x.lane == 0) {
+    S.tInf[k] = tw_pack(cell, t, lv + 1);
+    S.twr[cell] = (uint8_t)(0x80 | ((lv + 1) << 2) | t);
+  }
+  u.cost_def = dsub(u.cost_def, price);                   // :266
+  __syncthreads();
+  return FC_OK;
+}
+
+template <int NC>
+__device__ int tower_destruct(Smem<NC>& S, U& u, const Ctx& x, int cell) {
+  int k = find_tower(S, u, x, cell);
+  if (k < 0) return FC_TARGET;                            // :291-293
+  uint32_t ti = S.tInf[k];
+  int t = (ti >> 12) & 3, lv = (ti >> 14) & 1;
+  u.cost_def = dadd(u.cost_def, dmul(x.C.t_value[t][lv], x.C.destruct_return));  // :276
+  u.cost_def = pymin(u.cost_def, x.C.max_cost);                                  // :277
+  // towers.remove(t): keep the order of the rest (:278)
+  uint32_t vi = 0;
+  double vc = 0.0;
+  int j = x.lane;
+  if (j >= k && j + 1 < u.nt) { vi = S.tInf[j + 1]; vc = S.tCd[j + 1]; }
+  __syncthreads();
+  if (j >= k && j + 1 < u.nt) { S.tInf[j] = vi; S.tCd[j] = vc; }
+  if (x.lane == 0) S.twr[cell] = 0;
+  u.nt -= 1;
+  __syncthreads();
+  diamond(S, x, cell, -1);                                // :281-287
+  return FC_OK;
+}
+
+template <int NC>
+__device__ int defender_op(Smem<NC>& S, U& u, const Ctx& x, int op, int cell) {
+  if (op < 4) return tower_build(S, u, x, op, cell);
+  if (op == 4) return tower_lvup(S, u, x, cell);
+  return tower_destruct(S, u, x, cell);
+}
+
+// Multi-action defender: the serial (r, c, t) scan of TDDefense.py:42-60 /
+// TDMulti.py:209-227.  Cells where no operation can change the board are skipped:
+// per 64-cell chunk a ballot marks the cells whose flagged build / lvup / destruct
+// would succeed in the CURRENT state, the first such cell runs the reference's
+// exact serial sequence, and the ballot is recomputed.  Skipped cells would only
+// have produced failures, which leave no trace in multi-action mode.
+template <int NC>
+__device__ void defender_scan(Smem<NC>& S, U& u, const Ctx& x, const int64_t* A, int64_t* R, bool active) {
+  const TdDevCfg& C = x.C;
+  for (int base = 0; base < x.NCr; base += 64) {
+    const int cell = base + x.lane;
+    const bool valid = cell < x.NCr;
+    uint32_t fl = 0;
+    bool bad = false;
+    if (valid) {
+#pragma unroll
+      for (int ch = 0; ch < 6; ++ch) {
+        int64_t v = A[(size_t)ch * x.NCr + cell];
+        if (v == 1) fl |= 1u << ch;
+        if (v < 0 || v > 2) bad = true;
+      }
+    }
+    if (ballot(bad)) u.flags |= FLAG_BAD_ACTION;
+    uint32_t rl = 0;
+    int last = -1;
+    while (active) {
+      bool cand = false;
+      if (valid && fl && x.lane > last) {
+        uint32_t w = S.cell[cell];
+        uint32_t tw = S.twr[cell];
+        bool canb = false;
+        if (cw_block(w) == 0) {
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+            if (((fl >> t) & 1u) && !(u.cost_def < C.t_price[t][0])) canb = true;
+        }
+        bool hasT = (tw & 0x80u) != 0;
+        int tlv = (tw >> 2) & 1, tty = tw & 3;
+        bool canl = hasT && ((fl >> 4) & 1u) && tlv < C.max_tower_lv && !(u.cost_def < C.t_price[tty][tlv + 1]);
+        bool cand_d = hasT && ((fl >> 5) & 1u);
+        cand = canb || canl || cand_d;
+      }
+      uint64_t m = ballot(cand);
+      if (!m) break;
+      const int j = ctz64(m);
+      const int c = base + j;
+      const uint32_t f = __shfl(fl, j);
+      uint32_t rb = 0;
+      for (int t = 0; t < 4; ++t)
+        if ((f >> t) & 1u)
+          if (tower_build(S, u, x, t, c) == FC_OK) { rb |= 1u << t; u.def_cd = C.def_interval; }
+      if ((f >> 4) & 1u)
+        if (tower_lvup(S, u, x, c) == FC_OK) { rb |= 16u; u.def_cd = C.def_interval; }
+      if ((f >> 5) & 1u)
+        if (tower_destruct(S, u, x, c) == FC_OK) { rb |= 32u; u.def_cd = C.def_interval; }
+      if (x.lane == j) rl = rb;
+      last = j;
+    }
+    if (R && valid) {
+#pragma unroll
+      for (int ch = 0; ch < 6; ++ch) R[(size_t)ch * x.NCr + cell] = (rl >> ch) & 1u;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// attacker: summon_cluster (TDBoard.py:199-224)
+// ---------------------------------------------------------------------------
+template <int NC>
+__device__ int summon_cluster(Smem<NC>& S, U& u, const Ctx& x, const int* types, int road, int* real) {
+  const TdDevCfg& C = x.C;
+  const int lv = u.progress >= C.enemy_upgrade_at ? 1 : 0;  // :201
+  const int st = u.start[road];
+  bool tried = false, summoned = false;
+  for (int k = 0; k < 8; ++k) {
+    int t = types[k];
+    if (t == 4) { real[k] = 4; continue; }                  // :207-209
+    tried = true;
+    double cost = C.e_cost[t][lv];
+    if (u.cost_atk < cost) { real[k] = 4; continue; }       // :212-213
+    if (u.n >= ECAP) { u.flags |= FLAG_EN_OVERFLOW; real[k] = 4; continue; }
+    u.cost_atk = dsub(u.cost_atk, cost);                    // :215
+    if (x.lane == 0) {
+      S.eLP[u.n] = C.e_lp[t][lv];
+      S.eMg[u.n] = 0.0;
+      S.eInf[u.n] = en_pack(st, t, lv, 0);
+    }
+    u.n += 1;
+    summoned = true;
+    real[k] = t;
+  }
+  return (tried && !summoned) ? FC_COST : FC_OK;            // :219-224
+}
+
+// ---------------------------------------------------------------------------
+// TDBoard.step (TDBoard.py:295-368) + enemy_LP statistics
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int cheb(int a, int b, int L) {
+  int dr = a / L - b / L, dc = a % L - b % L;
+  dr = dr < 0 ? -dr : dr;
+  dc = dc < 0 ? -dc : dc;
+  return dr > dc ? dr : dc;
+}
+
+// Enemy.damage, TDElements.py:19-28
+__device__ __forceinline__ double damage(double LP, double atk, double def, bool magic) {
+  double dmg = magic ? atk : (dsub(atk, def) < 0.0 ? 0.0 : dsub(atk, def));
+  double lo = dmul(atk, 0.05);
+  if (dmg < lo) dmg = lo;
+  LP = dsub(LP, dmg);
+  if (LP <= 0.0) LP = 0.0;
+  return LP;
+}
+
+template <int NC>
+__device__ double board_step(Smem<NC>& S, U& u, const Ctx& x) {
+  const TdDevCfg& C = x.C;
+  const int L = x.L, lane = x.lane;
+  double reward = dadd(0.0, C.reward_time);                 // :298-299
+  u.steps += 1;                                             // :300
+  u.progress = ddiv((double)u.steps, (double)C.max_episode_steps);  // :301
+
+  // --- stable sort by f64 key dist - margin (:305): rank = #smaller + #equal-before
+  const int n = u.n;
+  double lp[2], mg[2], key[2];
+  uint32_t inf[2];
+  bool val[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    int i = lane + 64 * s;
+    val[s] = i < n;
+    lp[s] = val[s] ? S.eLP[i] : 0.0;
+    mg[s] = val[s] ? S.eMg[i] : 0.0;
+    inf[s] = val[s] ? S.eInf[i] : 0u;
+    key[s] = val[s] ? dsub((double)cw_dist(S.cell[en_cell(inf[s])]), mg[s]) : 0.0;
+    if (val[s]) S.key[i] = key[s];
+  }
+  __syncthreads();
+  int rank[2] = {0, 0};
+  for (int j = 0; j < n; ++j) {
+    double kj = S.key[j];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      int i = lane + 64 * s;
+      if (kj < key[s] || (kj == key[s] && j < i)) rank[s] += 1;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+    if (val[s]) { S.eLP[rank[s]] = lp[s]; S.eMg[rank[s]] = mg[s]; S.eInf[rank[s]] = inf[s]; }
+  __syncthreads();
+  // lane owns sorted enemies lane and lane + 64
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    int i = lane + 64 * s;
+    lp[s] = val[s] ? S.eLP[i] : 0.0;
+    mg[s] = val[s] ? S.eMg[i] : 0.0;
+    inf[s] = val[s] ? S.eInf[i] : 0u;
+  }
+
+  // --- towers fire in list order (:306-313); dead enemies stay targetable
+  for (int k = 0; k < u.nt; ++k) {
+    double cd = dsub(S.tCd[k], 1.0);                        // :307
+    if (!(cd > 0.0)) {
+      const uint32_t ti = S.tInf[k];
+      const int tt = (ti >> 12) & 3, tl = (ti >> 14) & 1, tc = ti & 0xfff;
+      const double rge = C.t_rge[tt][tl];
+      bool in0 = val[0] && (double)cheb(en_cell(inf[0]), tc, L) <= rge;
+      bool in1 = val[1] && (double)cheb(en_cell(inf[1]), tc, L) <= rge;
+      uint64_t m0 = ballot(in0), m1 = ballot(in1);
+      if (m0 | m1) {
+        const int tgt = m0 ? ctz64(m0) : 64 + ctz64(m1);
+        cd = dadd(cd, C.t_intv[tt][tl]);                    // cd += intv
+        const double atk = C.t_atk[tt][tl];
+        if (tt <= 1) {  // TowerArrow / TowerMagic (TDElements.py:71-93)
+          if (lane == (tgt & 63)) {
+            const int s = tgt >> 6;
+            const uint32_t e = inf[s];
+            lp[s] = damage(lp[s], atk, C.e_def[en_type(e)][en_lv(e)], tt == 1);
+          }
+        } else {
+          const uint32_t tinf = (tgt >> 6) ? __shfl(inf[1], tgt & 63) : __shfl(inf[0], tgt & 63);
+          const int tgc = en_cell(tinf);
+          const double dr = C.t_dmg[tt][tl];
+          if (tt == 2) {  // TowerBomb splash (:95-110)
+#pragma unroll
+            for (int s = 0; s < 2; ++s)
+              if (val[s] && (double)cheb(tgc, en_cell(inf[s]), L) <= dr)
+                lp[s] = damage(lp[s], atk, C.e_def[en_type(inf[s])][en_lv(inf[s])], false);
+          } else {  // TowerFrozen: first enemy within splash of the target (:112-132)
+            bool h0 = val[0] && (double)cheb(tgc, en_cell(inf[0]), L) <= dr;
+            bool h1 = val[1] && (double)cheb(tgc, en_cell(inf[1]), L) <= dr;
+            uint64_t q0 = ballot(h0), q1 = ballot(h1);
+            if (q0 | q1) {
+              const int f = q0 ? ctz64(q0) : 64 + ctz64(q1);
+              if (lane == (f & 63)) {
+                const int s = f >> 6;
+                lp[s] = damage(lp[s], atk, 0.0, true);
+                inf[s] = (inf[s] & 0xffffu) | ((uint32_t)C.frozen_time << 16);
+              }
+            }
+          }
+        }
+      }
+      if (cd < 0.0) cd = 0.0;                               // :311-312
+    }
+    if (lane == 0) S.tCd[k] = cd;
+  }
+
+  // --- kills (:313-317): every enemy at LP 0 was hit this step
+  bool dead0 = val[0] && lp[0] == 0.0, dead1 = val[1] && lp[1] == 0.0;
+  const int nk = popc64(ballot(dead0)) + popc64(ballot(dead1));
+  reward = dadd(reward, dmul(C.reward_kill, (double)nk));  // :315
+
+  // --- march (:319-344)
+  bool alive[2] = {val[0] && !dead0, val[1] && !dead1};
+  bool leak[2] = {false, false};
+  const int DR[4] = {0, 0, 1, -1}, DC[4] = {1, -1, 0, 0};
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    if (!alive[s]) continue;
+    const uint32_t e = inf[s];
+    const int t = en_type(e), lv = en_lv(e);
+    int slow = en_slow(e), cell = en_cell(e);
+    const double sp = C.e_speed[t][lv];
+    if (slow > 0) { mg[s] = dadd(mg[s], dmul(sp, C.frozen_ratio)); slow -= 1; }
+    else mg[s] = dadd(mg[s], sp);
+    while (mg[s] >= 1.0) {
+      mg[s] = dsub(mg[s], 1.0);
+      const int d = cw_dir(S.cell[cell]);
+      int r = cell / L + DR[d], c = cell % L + DC[d];
+      if (r < 0 || r >= L || c < 0 || c >= L) { u.flags |= FLAG_BAD_MOVE; break; }
+      cell = r * L + c;
+      if (cell == u.end_cell) { leak[s] = true; break; }
+    }
+    inf[s] = en_pack(cell, t, lv, slow);
+  }
+  // a bad move is rare and lane-local: fold the flag into the uniform copy
+  if (ballot((u.flags & FLAG_BAD_MOVE) != 0)) u.flags |= FLAG_BAD_MOVE;
+  const int nl = popc64(ballot(leak[0])) + popc64(ballot(leak[1]));
+  for (int p = 0; p < nl; ++p) {                            // :336-343, in list order
+    if (u.base_LP > 0) reward = dsub(reward, C.penalty_leak);
+    u.base_LP = u.base_LP - 1 > 0 ? u.base_LP - 1 : 0;
+  }
+  // --- compact survivors, list order kept (:316-317, :345-346)
+  bool keep0 = alive[0] && !leak[0], keep1 = alive[1] && !leak[1];
+  const uint64_t k0 = ballot(keep0), k1 = ballot(keep1);
+  const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  const int n2 = popc64(k0) + popc64(k1);
+  __syncthreads();
+  if (keep0) { int d = popc64(k0 & lt); S.eLP[d] = lp[0]; S.eMg[d] = mg[0]; S.eInf[d] = inf[0]; }
+  if (keep1) { int d = popc64(k0) + popc64(k1 & lt); S.eLP[d] = lp[1]; S.eMg[d] = mg[1]; S.eInf[d] = inf[1]; }
+  u.n = n2;
+
+  // --- costs (:348-353)
+  double rate;
+  if (u.progress >= 0.5) rate = C.atk_final_rate;
+  else rate = dadd(dmul(C.atk_init_rate, dsub(1.0, u.progress)), dmul(C.atk_final_rate, u.progress));
+  u.cost_atk = pymin(dadd(u.cost_atk, rate), C.max_cost);
+  u.cost_def = pymin(dadd(u.cost_def, C.def_rate), C.max_cost);
+  __syncthreads();
+  return reward;
+}
+
+// enemy_LP planes (TDBoard.py:355-365): per (type, cell) min / max / sum in list
+// order / count, all in numpy float32.  The first enemy of each group (its
+// "head") walks the list and owns the group's stats.
+template <int NC>
+__device__ void enemy_stats(Smem<NC>& S, const U& u, const Ctx& x) {
+  const TdDevCfg& C = x.C;
+  const int n = u.n;
+  for (int i = x.lane; i < 4 * NC; i += 64) (&S.grp[0][0])[i] = 0xFF;
+  uint32_t key[2];
+  bool val[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    int i = x.lane + 64 * s;
+    val[s] = i < n;
+    key[s] = 0;
+    if (val[s]) {
+      uint32_t e = S.eInf[i];
+      key[s] = e & 0x3fffu;  // cell | type << 12
+      S.eR[i] = f32(ddiv(S.eLP[i], C.e_lp[en_type(e)][en_lv(e)]));  // r = LP / maxLP (:358)
+    }
+  }
+  __syncthreads();
+  float mn[2] = {1.0f, 1.0f}, mx[2] = {0.0f, 0.0f}, sm[2] = {0.0f, 0.0f};
+  int cnt[2] = {0, 0};
+  bool head[2] = {val[0], val[1]};
+  for (int j = 0; j < n; ++j) {
+    uint32_t kj = S.eInf[j] & 0x3fffu;
+    float rj = S.eR[j];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      int i = x.lane + 64 * s;
+      if (val[s] && kj == key[s]) {
+        if (j < i) head[s] = false;
+        else {
+          mn[s] = rj < mn[s] ? rj : mn[s];
+          mx[s] = rj > mx[s] ? rj : mx[s];
+          sm[s] = __fadd_rn(sm[s], rj);
+          cnt[s] += 1;
+        }
+      }
+    }
+  }
+  const float mcl = (float)C.max_cluster_length;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    int i = x.lane + 64 * s;
+    if (head[s]) {
+      S.gst[i][0] = mn[s];
+      S.gst[i][1] = mx[s];
+      S.gst[i][2] = __fdiv_rn(sm[s], (float)cnt[s]);
+      S.gst[i][3] = __fdiv_rn((float)cnt[s], mcl);
+      S.grp[key[s] >> 12][key[s] & 0xfffu] = (uint8_t)i;
+    }
+  }
+  __syncthreads();
+}
+
+// Broadcast channels and the channel-9 table (TDBoard.py:115-142).
+template <int NC>
+__device__ void channel_scalars(Smem<NC>& S, const U& u, const Ctx& x) {
+  const TdDevCfg& C = x.C;
+  const int l = x.lane;
+  if (l < 48) {
+    float v = 0.0f;
+    if (l == 5) v = f32(ddiv((double)u.base_LP, (double)C.base_LP));
+    else if (l == 11) v = f32(ddiv(u.cost_def, C.max_cost));
+    else if (l == 12) v = f32(ddiv(u.cost_atk, C.max_cost));
+    else if (l == 13) v = f32(u.progress);
+    else if (l >= 21 && l < 25) v = (u.cost_def >= C.t_price[l - 21][0]) ? 1.0f : 0.0f;
+    else if (l >= 41 && l < 45) v = f32(ddiv(ddiv(u.cost_def, C.e_cost[l - 41][0]), (double)C.max_cluster_length));
+    S.chv[l] = v;
+  }
+  // s[9] = map[4] / (max(map[4]) + 1): int32 scalar divisor promotes to f64, rounded once to f32
+  for (int d = l; d <= u.maxdist && d < 256; d += 64) S.d9[d] = f32(ddiv((double)d, (double)(u.maxdist + 1)));
+  __syncthreads();
+}
+
+template <int NC>
+__device__ __forceinline__ float obs_value(const Smem<NC>& S, int ch, int cell) {
+  const uint32_t w = S.cell[cell];
+  if (ch < 5) return (float)((w >> ch) & 1u);                      // 0-3 roads, 4 end
+  if (ch >= 6 && ch < 9) return (float)((w >> (ch - 1)) & 1u);     // 6-8 starts (bits 5-7)
+  if (ch == 9) return S.d9[cw_dist(w)];
+  if (ch == 14) return cw_block(w) == 0 ? 1.0f : 0.0f;
+  if (ch >= 15 && ch < 21) {
+    const uint32_t tw = S.twr[cell];
+    if (!(tw & 0x80u)) return 0.0f;
+    if (ch < 17) return ((int)((tw >> 2) & 1u) == ch - 15) ? 1.0f : 0.0f;
+    return ((int)(tw & 3u) == ch - 17) ? 1.0f : 0.0f;
+  }
+  if (ch >= 25 && ch < 41) {
+    const int q = ch - 25, st = q >> 2, t = q & 3;
+    const uint32_t g = S.grp[t][cell];
+    return g == 0xFFu ? 0.0f : S.gst[g][st];
+  }
+  return S.chv[ch];  // 5, 10-13, 21-24, 41-44
+}
+
+template <int NC>
+__device__ void write_obs(const Smem<NC>& S, const Ctx& x, float* out) {
+  const int ncr = x.NCr;
+  if ((ncr & 3) == 0) {
+    float4* o4 = reinterpret_cast<float4*>(out);
+    const int nq = NCH * ncr / 4;
+    for (int q = x.lane; q < nq; q += 64) {
+      const int f = q * 4, ch = f / ncr, cell = f - ch * ncr;
+      float4 v;
+      v.x = obs_value(S, ch, cell);
+      v.y = obs_value(S, ch, cell + 1);
+      v.z = obs_value(S, ch, cell + 2);
+      v.w = obs_value(S, ch, cell + 3);
+      o4[q] = v;
+    }
+  } else {
+    const int nf = NCH * ncr;
+    for (int f = x.lane; f < nf; f += 64) {
+      const int ch = f / ncr;
+      out[f] = obs_value(S, ch, f - ch * ncr);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// board load / reset / store
+// ---------------------------------------------------------------------------
+template <int NC>
+__device__ void load_board(Smem<NC>& S, U& u, const Ctx& x, const StepArgs& a, int b) {
+  const TdHdr& h = a.hdr[b];
+  u.cost_def = h.cost_def; u.cost_atk = h.cost_atk; u.ep_ret = h.ep_return;
+  u.steps = h.steps; u.base_LP = h.base_LP; u.atk_cd = h.atk_cd; u.def_cd = h.def_cd;
+  u.n = h.n_en; u.nt = h.n_tw; u.num_roads = h.num_roads; u.end_cell = h.end_cell;
+  u.start[0] = h.start_cell[0]; u.start[1] = h.start_cell[1]; u.start[2] = h.start_cell[2];
+  u.maxdist = h.maxdist; u.flags = h.flags; u.episodes = h.episodes;
+  u.progress = ddiv((double)u.steps, (double)x.C.max_episode_steps);
+  const size_t eb = (size_t)b * ECAP, tb = (size_t)b * TCAP, cb = (size_t)b * x.NCr;
+  for (int i = x.lane; i < x.NCr; i += 64) { S.cell[i] = a.cells[cb + i]; S.twr[i] = 0; }
+  for (int i = x.lane; i < u.n; i += 64) { S.eLP[i] = a.en_lp[eb + i]; S.eMg[i] = a.en_mg[eb + i]; S.eInf[i] = a.en_inf[eb + i]; }
+  if (x.lane < u.nt) { S.tCd[x.lane] = a.tw_cd[tb + x.lane]; S.tInf[x.lane] = a.tw_inf[tb + x.lane]; }
+  __syncthreads();
+  if (x.lane < u.nt) {
+    uint32_t ti = S.tInf[x.lane];
+    S.twr[ti & 0xfffu] = (uint8_t)(0x80u | (((ti >> 14) & 1u) << 2) | ((ti >> 12) & 3u));
+  }
+  __syncthreads();
+}
+
+// Fresh board from a layout record (TDGymBasic.reset :43-53, TDBoard.__init__ :14-79).
+template <int NC>
+__device__ void reset_board(Smem<NC>& S, U& u, const Ctx& x, const uint32_t* rec) {
+  const TdDevCfg& C = x.C;
+  for (int i = x.lane; i < x.NCr; i += 64) { S.cell[i] = rec[LAYOUT_HDR + i]; S.twr[i] = 0; }
+  u.num_roads = (int)rec[1]; u.end_cell = (int)rec[2]; u.maxdist = (int)rec[3];
+  u.start[0] = (int)rec[4]; u.start[1] = (int)rec[5]; u.start[2] = (int)rec[6];
+  u.cost_def = C.def_init_cost; u.cost_atk = C.atk_init_cost;
+  u.base_LP = C.base_LP; u.steps = 0; u.progress = 0.0;
+  u.atk_cd = 0; u.def_cd = 0; u.n = 0; u.nt = 0; u.ep_ret = 0.0;
+  __syncthreads();
+}
+
+template <int NC>
+__device__ void store_board(const Smem<NC>& S, const U& u, const Ctx& x, const StepArgs& a, int b) {
+  if (x.lane == 0) {
+    TdHdr h;
+    h.cost_def = u.cost_def; h.cost_atk = u.cost_atk; h.ep_return = u.ep_ret;
+    h.steps = u.steps; h.base_LP = u.base_LP; h.atk_cd = u.atk_cd; h.def_cd = u.def_cd;
+    h.n_en = u.n; h.n_tw = u.nt; h.num_roads = u.num_roads; h.end_cell = u.end_cell;
+    h.start_cell[0] = u.start[0]; h.start_cell[1] = u.start[1]; h.start_cell[2] = u.start[2];
+    h.maxdist = u.maxdist; h.flags = u.flags; h.episodes = u.episodes;
+    h.pad[0] = h.pad[1] = h.pad[2] = h.pad[3] = 0;
+    a.hdr[b] = h;
+  }
+  const size_t eb = (size_t)b * ECAP, tb = (size_t)b * TCAP, cb = (size_t)b * x.NCr;
+  for (int i = x.lane; i < x.NCr; i += 64) a.cells[cb + i] = S.cell[i];
+  for (int i = x.lane; i < u.n; i += 64) { a.en_lp[eb + i] = S.eLP[i]; a.en_mg[eb + i] = S.eMg[i]; a.en_inf[eb + i] = S.eInf[i]; }
+  if (x.lane < u.nt) { a.tw_cd[tb + x.lane] = S.tCd[x.lane]; a.tw_inf[tb + x.lane] = S.tInf[x.lane]; }
+}
+
+// ---------------------------------------------------------------------------
+// built-in opponents
+// ---------------------------------------------------------------------------
+template <int NC>
+__device__ void opponent_enemy(Smem<NC>& S, U& u, const Ctx& x, WaveMt& R, int difficulty) {
+  // random_enemy_lv0 / lv1 with random_agent=True (TDGymBasic.py:81-108)
+  if (u.atk_cd != 0) return;
+  int types[8], real[8];
+  int road;
+  if (difficulty == 0) {
+    for (int k = 0; k < 8; ++k) types[k] = (int)R.randint(0, 4);
+    road = (int)R.randint(0, u.num_roads - 1);
+  } else {
+    int t = (int)R.randint(0, 3);
+    road = (int)R.randint(0, u.num_roads - 1);
+    for (int k = 0; k < 8; ++k) types[k] = t;
+  }
+  summon_cluster(S, u, x, types, road, real);
+  __syncthreads();
+  u.atk_cd = x.C.atk_interval;  // the (ok, real) tuple is always truthy
+}
+
+template <int NC>
+__device__ void opponent_tower_lv0(Smem<NC>& S, U& u, const Ctx& x, WaveMt& R) {
+  // random_tower_lv0 with random_agent=True (TDGymBasic.py:111-122)
+  if (u.def_cd != 0) return;
+  int r = (int)R.randint(0, x.L - 1);
+  int c = (int)R.randint(0, x.L - 1);
+  int t = (int)R.randint(0, 3);
+  if (tower_build(S, u, x, t, r * x.L + c) == FC_OK) u.def_cd = x.C.def_interval;
+}
+
+// random_tower_lv1 / lv2 with random_agent=True (TDGymBasic.py:124-292).
+template <int NC>
+__device__ void build_near_road(Smem<NC>& S, U& u, const Ctx& x, WaveMt& R, int t, bool draw_type) {
+  // road cells in row-major order, then random.shuffle (Fisher-Yates on randbelow)
+  // The list lives in the sort-key scratch as cell indices (<= L*L <= 4096 > 4*ECAP,
+  // so it is kept in the group map instead: grp has 4*NC bytes -> store u16 cells).
+  uint16_t* cells = reinterpret_cast<uint16_t*>(&S.grp[0][0]);
+  int nroad = 0;
+  for (int base = 0; base < x.NCr; base += 64) {
+    int c = base + x.lane;
+    bool isr = c < x.NCr && (S.cell[c] & 1u);
+    uint64_t m = ballot(isr);
+    const uint64_t lt = (x.lane == 0) ? 0ull : (~0ull >> (64 - x.lane));
+    if (isr) cells[nroad + popc64(m & lt)] = (uint16_t)c;
+    nroad += popc64(m);
+  }
+  __syncthreads();
+  for (int i = nroad - 1; i >= 1; --i) {
+    int j = (int)R.randbelow(i + 1);
+    if (x.lane == 0) { uint16_t tmp = cells[i]; cells[i] = cells[j]; cells[j] = tmp; }
+    __syncthreads();
+  }
+  if (draw_type) t = (int)R.randint(0, 3);
+  for (int i = 0; i < nroad; ++i) {
+    int k = (int)R.randint(0, 24);
+    int dr = k / 5 - 2, dc = k % 5 - 2;
+    int cc = cells[i];
+    int r = cc / x.L + dr, c = cc % x.L + dc;
+    if (r < 0 || r >= x.L || c < 0 || c >= x.L) continue;
+    int fc = tower_build(S, u, x, t, r * x.L + c);
+    if (fc == FC_OK) { u.def_cd = x.C.def_interval; return; }
+    if (fc == FC_COST) return;
+  }
+}
+
+template <int NC>
+__device__ void upgrade_or_destruct(Smem<NC>& S, U& u, const Ctx& x, WaveMt& R, int act) {
+  if (u.nt == 0) return;
+  if (act == 1) {
+    int id = (int)R.randint(0, u.nt - 1);
+    int cell = (int)(S.tInf[id] & 0xfffu);
+    if (tower_lvup(S, u, x, cell) == FC_OK) u.def_cd = x.C.def_interval;
+  } else {
+    if (R.random() > 0.01) return;
+    int id = (int)R.randint(0, u.nt - 1);
+    int cell = (int)(S.tInf[id] & 0xfffu);
+    if (tower_destruct(S, u, x, cell) == FC_OK) u.def_cd = x.C.def_interval;
+  }
+}
+
+template <int NC>
+__device__ void opponent_tower(Smem<NC>& S, U& u, const Ctx& x, WaveMt& R, int difficulty) {
+  if (difficulty == 0) { opponent_tower_lv0(S, u, x, R); return; }
+  if (u.def_cd != 0) return;
+  int act = (int)R.randint(0, 2);
+  if (act != 0) { upgrade_or_destruct(S, u, x, R, act); return; }
+  if (difficulty == 1) { build_near_road(S, u, x, R, 0, true); return; }
+  // lv2: tower type from the enemy type mix (TDGymBasic.py:217-240)
+  if (u.n == 0) return;
+  int cnt[4] = {0, 0, 0, 0};
+  for (int i = 0; i < u.n; ++i) cnt[en_type(S.eInf[i])] += 1;
+  // np.unique -> present types ascending; ratio = nums.astype(float32) / np.sum(nums):
+  // float32 array / int64 scalar promotes to float64 (NEP 50), so the ratio is an f64 quotient
+  int types[4], nt = 0;
+  for (int t = 0; t < 4; ++t) if (cnt[t]) types[nt++] = t;
+  double p = R.random();
+  int chosen = -1;
+  for (int i = 0; i < 4; ++i) {
+    if (i >= nt) { u.flags |= FLAG_BAD_ACTION; break; }  // the reference raises IndexError here
+    double ratio = ddiv((double)cnt[types[i]], (double)u.n);
+    if (p < ratio) { chosen = types[i]; break; }
+    p = dsub(p, ratio);
+  }
+  if (chosen < 0) return;
+  const int remap[4] = {2, 0, 1, 0};
+  int t = remap[chosen];
+  if (R.random() < 0.2) t = 3;
+  build_near_road(S, u, x, R, t, false);
+}
+
+// ---------------------------------------------------------------------------
+// kernels
+// ---------------------------------------------------------------------------
+template <int NC>
+__device__ void step_board(Smem<NC>& S, const StepArgs& a, int b, int L) {
+  const Ctx x{*a.cfg, L, L * L, (int)threadIdx.x};
+  const TdDevCfg& C = x.C;
+  U u;
+  load_board(S, u, x, a, b);
+  WaveMt R{a.opp_mt + (size_t)b * (MT_N + 1), a.opp_mt[(size_t)b * (MT_N + 1) + MT_N], x.lane};
+
+  u.atk_cd = u.atk_cd - 1 > 0 ? u.atk_cd - 1 : 0;
+  u.def_cd = u.def_cd - 1 > 0 ? u.def_cd - 1 : 0;
+  const int64_t empty_def = (int64_t)6 * x.NCr;
+  int fail_def = 0;
+  int64_t real_def = empty_def;
+  int fail_atk[3] = {-1, -1, -1};
+  int real_atk[24];
+
+  // ---- defender
+  if (a.mode != MODE_ATK) {
+    if (a.multi) {
+      defender_scan(S, u, x, a.def_act + (size_t)b * 6 * x.NCr,
+                    a.real_def ? a.real_def + (size_t)b * 6 * x.NCr : nullptr, u.def_cd == 0);
+    } else {
+      int64_t act = a.def_act[b];
+      if (act < 0 || act > empty_def) { u.flags |= FLAG_BAD_ACTION; act = empty_def; }
+      if (u.def_cd == 0 && act != empty_def) {
+        const int op = (int)(act / x.NCr), r = (int)((act / L) % L), c = (int)(act % L);
+        fail_def = defender_op(S, u, x, op, r * L + c);
+        if (fail_def == FC_OK) { u.def_cd = C.def_interval; real_def = act; }
+      }
+    }
+  }
+  // ---- attacker
+  if (a.mode == MODE_DEF) {
+    opponent_enemy(S, u, x, R, a.difficulty);
+  } else {
+    const int64_t* A = a.atk_act + (size_t)b * 24;
+    int acts[24];
+    bool bad = false;
+    for (int k = 0; k < 24; ++k) {
+      int64_t v = A[k];
+      if (v < 0 || v > 4) { bad = true; v = 4; }
+      acts[k] = (int)v;
+      real_atk[k] = (int)v;
+    }
+    if (bad) u.flags |= FLAG_BAD_ACTION;
+    if (u.atk_cd == 0) {
+      for (int i = 0; i < u.num_roads; ++i) {
+        const int* cl = acts + 8 * i;
+        bool all4 = true;
+        for (int k = 0; k < 8; ++k) all4 = all4 && cl[k] == 4;
+        if (a.mode == MODE_2P && a.multi) {  // TDMulti multi: every road, always truthy (:201-206)
+          summon_cluster(S, u, x, cl, i, real_atk + 8 * i);
+          for (int k = 0; k < 8; ++k) real_atk[8 * i + k] = cl[k];
+          u.atk_cd = C.atk_interval;
+        } else if (all4) {
+          fail_atk[i] = 0;                                  // TDAttack.py:40-42, TDMulti.py:234-236
+        } else {
+          int fc = summon_cluster(S, u, x, cl, i, real_atk + 8 * i);
+          if (a.mode == MODE_ATK) {
+            if (fc == FC_OK) u.atk_cd = C.atk_interval;     // res is a real bool here (TDAttack.py:43-44)
+          } else {
+            u.atk_cd = C.atk_interval;                      // tuple truthiness (TDMulti.py:237-238)
+            for (int k = 0; k < 8; ++k) real_atk[8 * i + k] = cl[k];
+          }
+          fail_atk[i] = fc;
+        }
+        __syncthreads();
+      }
+    }
+    if (a.mode == MODE_ATK) opponent_tower(S, u, x, R, a.difficulty);
+  }
+  __syncthreads();
+
+  // ---- TDBoard.step
+  double reward = board_step(S, u, x);
+  if (a.mode == MODE_ATK) reward = -reward;                 // TDAttack.py:50
+  const bool done = (u.base_LP <= 0) || (u.steps >= C.max_episode_steps);  // :384-385
+  u.ep_ret = dadd(u.ep_ret, reward);
+  const int ep_steps = u.steps;
+  int8_t win = -1;
+  if (done) {
+    if (a.mode == MODE_ATK) win = u.base_LP <= 0 ? 1 : 0;
+    else win = u.base_LP > 0 ? 1 : 0;
+  }
+  const uint8_t allow = (uint8_t)((u.atk_cd <= 1 ? 1 : 0) | (u.def_cd <= 1 ? 2 : 0));
+  const double ep_ret = u.ep_ret;
+
+  if (done) u.episodes += 1;
+  bool was_reset = false;
+  if (done && a.autoreset) {
+    const uint32_t* rec = a.nxt + (size_t)b * (LAYOUT_HDR + x.NCr);
+    if (rec[0] == TD_LAYOUT_MAGIC) {
+      reset_board(S, u, x, rec);
+      was_reset = true;
+    } else {
+      u.flags |= FLAG_NO_LAYOUT;
+    }
+  }
+  if (!was_reset) enemy_stats(S, u, x);
+  else {
+    for (int i = x.lane; i < 4 * NC; i += 64) (&S.grp[0][0])[i] = 0xFF;
+    __syncthreads();
+  }
+  channel_scalars(S, u, x);
+  write_obs(S, x, a.obs + (size_t)b * NCH * x.NCr);
+  store_board(S, u, x, a, b);
+
+  if (x.lane == 0) {
+    if (was_reset) {
+      a.nxt[(size_t)b * (LAYOUT_HDR + x.NCr)] = 0u;  // staged layout consumed
+      a.consumed[b] += 1u;
+    }
+    a.opp_mt[(size_t)b * (MT_N + 1) + MT_N] = R.pos;
+    a.reward[b] = reward;
+    a.done[b] = done ? 1 : 0;
+    if (a.win) a.win[b] = win;
+    if (a.allow_next) a.allow_next[b] = allow;
+    if (a.fail_def) a.fail_def[b] = fail_def;
+    if (a.real_def && !a.multi) a.real_def[b] = real_def;
+    if (a.ep_return) a.ep_return[b] = ep_ret;
+    if (a.ep_len) a.ep_len[b] = ep_steps;
+  }
+  if (a.mode != MODE_DEF) {
+    if (a.fail_atk && x.lane < 3) a.fail_atk[(size_t)b * 3 + x.lane] = fail_atk[x.lane];
+    if (a.real_atk && x.lane < 24) {
+      int v = 0;
+      for (int k = 0; k < 24; ++k) if (k == x.lane) v = real_atk[k];
+      a.real_atk[(size_t)b * 24 + x.lane] = v;
+    }
+  }
+}
+
+template <int LT>
+__global__ __launch_bounds__(64) void td_step_kernel(StepArgs a) {
+  constexpr int NC = LT ? LT * LT : MAX_L * MAX_L / 4;
+  __shared__ Smem<NC> S;
+  const int b = blockIdx.x;
+  if (b >= a.B) return;
+  step_board<NC>(S, a, b, LT ? LT : a.L);
+}
+
+// Reset selected boards from their staged layout and write the initial obs.
+template <int LT>
+__global__ __launch_bounds__(64) void td_reset_kernel(StepArgs a) {
+  constexpr int NC = LT ? LT * LT : MAX_L * MAX_L / 4;
+  __shared__ Smem<NC> S;
+  const int b = blockIdx.x;
+  if (b >= a.B) return;
+  if (a.reset_mask && !a.reset_mask[b]) return;
+  const int L = LT ? LT : a.L;
+  const Ctx x{*a.cfg, L, L * L, (int)threadIdx.x};
+  U u;
+  u.episodes = a.hdr[b].episodes;
+  u.flags = 0;
+  const uint32_t* rec = a.nxt + (size_t)b * (LAYOUT_HDR + x.NCr);
+  if (rec[0] != TD_LAYOUT_MAGIC) {
+    if (x.lane == 0) a.hdr[b].flags |= FLAG_NO_LAYOUT;
+    return;
+  }
+  reset_board(S, u, x, rec);
+  for (int i = x.lane; i < 4 * NC; i += 64) (&S.grp[0][0])[i] = 0xFF;
+  __syncthreads();
+  channel_scalars(S, u, x);
+  if (a.obs) write_obs(S, x, a.obs + (size_t)b * NCH * x.NCr);
+  store_board(S, u, x, a, b);
+  if (x.lane == 0) {
+    a.nxt[(size_t)b * (LAYOUT_HDR + x.NCr)] = 0u;
+    a.consumed[b] += 1u;
+  }
+}
+
+// Copy staged layout records into the boards' next-episode slots.
+__global__ __launch_bounds__(64) void td_stage_layouts_kernel(uint32_t* nxt, const uint32_t* recs, const int32_t* boards,
+                                                          int n, int words) {
+  const int i = blockIdx.x;
+  if (i >= n) return;
+  uint32_t* dst = nxt + (size_t)boards[i] * words;
+  const uint32_t* src = recs + (size_t)i * words;
+  for (int k = (int)threadIdx.x; k < words; k += 64) dst[k] = src[k];
+}
+
+template <int LT>
+static hipError_t launch2(const StepArgs& a, hipStream_t s, bool reset) {
+  if (reset) hipLaunchKernelGGL(td_reset_kernel<LT>, dim3(a.B), dim3(64), 0, s, a);
+  else hipLaunchKernelGGL(td_step_kernel<LT>, dim3(a.B), dim3(64), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_step(const StepArgs& a, hipStream_t s, bool reset) {
+  switch (a.L) {
+    case 10: return launch2<10>(a, s, reset);
+    case 20: return launch2<20>(a, s, reset);
+    case 30: return launch2<30>(a, s, reset);
+    default: return launch2<0>(a, s, reset);
+  }
+}
+
+hipError_t launch_stage_layouts(uint32_t* nxt, const uint32_t* recs, const int32_t* boards, int n, int words,
+                                hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(td_stage_layouts_kernel, dim3(n), dim3(64), 0, s, nxt, recs, boards, n, words);
+  return hipGetLastError();
+}
+
+}  // namespace td

@@ -1,0 +1,326 @@
+"""TDEngine: B independent gym-TD boards in HBM, stepped by libtdstep.so.
+
+The batched counterpart of TDGymBasic + TDDefense / TDAttack / TDMulti
+(gym_TD/envs/TDGymBasic.py, TDDefense.py, TDAttack.py, TDMulti.py).  Actions and
+outputs are torch tensors on the engine's device; every step is one kernel
+launch on torch's current stream.
+"""
+import numpy as np
+import torch
+
+from . import _lib
+from . import params as P
+
+MODES = {"def": 0, "atk": 1, "2p": 2}
+
+HDR_DTYPE = np.dtype([
+    ("cost_def", "<f8"), ("cost_atk", "<f8"), ("ep_return", "<f8"), ("steps", "<i4"), ("base_LP", "<i4"),
+    ("atk_cd", "<i4"), ("def_cd", "<i4"), ("n_en", "<i4"), ("n_tw", "<i4"), ("num_roads", "<i4"),
+    ("end_cell", "<i4"), ("start_cell", "<i4", (3,)), ("maxdist", "<i4"), ("flags", "<i4"), ("episodes", "<i4"),
+    ("pad", "<i4", (4,))])
+assert HDR_DTYPE.itemsize == _lib.HDR_BYTES
+
+
+def _u32(a):
+    return np.ascontiguousarray(a, dtype=np.uint32)
+
+
+class TDEngine(object):
+    """B boards of one map size and mode.
+
+    mode: 'def' (TD-def: defender acts, built-in random_enemy_lv{difficulty}),
+          'atk' (TD-atk: attacker acts, built-in random_tower_lv{difficulty}),
+          '2p'  (TD-2p: both act).
+    multi_action: HyperParameters.allow_multiple_actions (defender flags (6, L, L)).
+    np_seeds / py_seeds: per-board seeds of the layout stream (numpy RandomState)
+          and of the built-in opponent's CPython ``random`` stream.
+    autoreset: a board that finishes starts its next episode inside the same
+          step and the returned obs is the new episode's first obs (gym 0.21
+          AsyncVectorEnv semantics); reward/done/info describe the finished step.
+    """
+
+    def __init__(self, map_size, n_boards, mode="def", multi_action=None, difficulty=1, device=None,
+                 np_seeds=None, py_seeds=None, autoreset=True, info=True, cfg=None, hp=None):
+        hp = hp or P.hyper_parameters
+        if multi_action is None:
+            multi_action = bool(hp.allow_multiple_actions)
+        if device is None:
+            device = torch.cuda.current_device()
+        self.device = torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
+        self.L, self.B, self.mode = int(map_size), int(n_boards), mode
+        self.multi = bool(multi_action)
+        self.difficulty = int(difficulty)
+        self._cfg_c = P.to_c(cfg or P.config, hp)
+        h = _lib.lib.td_create(self._cfg_c, self.L, self.B, MODES[mode], int(self.multi), self.difficulty,
+                               self.device.index or 0)
+        if not h:
+            raise _lib.TDError(_lib.lib.td_last_error().decode())
+        self._h = h
+        self.lw = _lib.lib.td_layout_words(self.L)
+        self.autoreset = bool(autoreset)
+        _lib.check(_lib.lib.td_set_autoreset(h, int(self.autoreset)))
+        B, L, dev = self.B, self.L, self.device
+        self.obs = torch.zeros((B, _lib.NCH, L, L), dtype=torch.float32, device=dev)
+        self.reward = torch.zeros(B, dtype=torch.float64, device=dev)
+        self.done = torch.zeros(B, dtype=torch.uint8, device=dev)
+        self.info_enabled = bool(info)
+        self.win = self.allow_next = self.ep_return = self.ep_len = None
+        self.real_def = self.fail_def = self.real_atk = self.fail_atk = None
+        if info:
+            self.win = torch.zeros(B, dtype=torch.int8, device=dev)
+            self.allow_next = torch.zeros(B, dtype=torch.uint8, device=dev)
+            self.ep_return = torch.zeros(B, dtype=torch.float64, device=dev)
+            self.ep_len = torch.zeros(B, dtype=torch.int32, device=dev)
+            if mode != "atk":
+                shape = (B, 6, L, L) if self.multi else (B,)
+                self.real_def = torch.zeros(shape, dtype=torch.int64, device=dev)
+                self.fail_def = torch.zeros(B, dtype=torch.int32, device=dev)
+            if mode != "def":
+                self.real_atk = torch.zeros((B, 3, 8), dtype=torch.int64, device=dev)
+                self.fail_atk = torch.zeros((B, 3), dtype=torch.int32, device=dev)
+        self._io = _lib.TdStepIO()
+        for name in ("obs", "reward", "done", "real_def", "real_atk", "fail_def", "fail_atk", "win",
+                     "allow_next", "ep_return", "ep_len"):
+            t = getattr(self, name)
+            setattr(self._io, name, t.data_ptr() if t is not None else None)
+        if np_seeds is not None or py_seeds is not None:
+            self.seed(np_seeds, py_seeds)
+        P._live.add(self)
+
+    # ------------------------------------------------------------------ setup
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib.lib.td_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_config(self, cfg=None, hp=None):
+        self._cfg_c = P.to_c(cfg or P.config, hp)
+        _lib.check(_lib.lib.td_set_config(self._h, self._cfg_c))
+
+    def seed(self, np_seeds=None, py_seeds=None):
+        """Per-board seeds (int or array of B)."""
+        def arr(s):
+            if s is None:
+                return None
+            a = np.asarray(s, dtype=np.int64)
+            if a.ndim == 0:
+                a = np.full(self.B, int(a), dtype=np.int64)
+            if a.shape != (self.B,) or (a < 0).any() or (a > 0xFFFFFFFF).any():
+                raise ValueError("seeds must be B ints in [0, 2**32)")
+            return _u32(a)
+        npa, pya = arr(np_seeds), arr(py_seeds)
+        _lib.check(_lib.lib.td_seed(self._h, _lib.ptr(npa, _lib.ctypes.c_uint32) if npa is not None else None,
+                                    _lib.ptr(pya, _lib.ctypes.c_uint32) if pya is not None else None))
+
+    def set_py_state(self, b, state):
+        """Import a CPython ``random.getstate()`` (or 625 words) as board b's opponent stream."""
+        w = _mt_words(state)
+        _lib.check(_lib.lib.td_set_py_state(self._h, int(b), _lib.ptr(w, _lib.ctypes.c_uint32)))
+
+    def get_py_state(self, b):
+        w = np.zeros(_lib.MT_WORDS, dtype=np.uint32)
+        _lib.check(_lib.lib.td_get_py_state(self._h, int(b), _lib.ptr(w, _lib.ctypes.c_uint32)))
+        return w
+
+    def set_np_state(self, b, state):
+        """Import a ``RandomState.get_state()`` (or 625 words) as board b's layout stream."""
+        w = _mt_words(state)
+        _lib.check(_lib.lib.td_set_np_state(self._h, int(b), _lib.ptr(w, _lib.ctypes.c_uint32)))
+
+    def get_np_state(self, b):
+        w = np.zeros(_lib.MT_WORDS, dtype=np.uint32)
+        _lib.check(_lib.lib.td_get_np_state(self._h, int(b), _lib.ptr(w, _lib.ctypes.c_uint32)))
+        return w
+
+    # ------------------------------------------------------------------- run
+    def _stream(self):
+        return torch.cuda.current_stream(self.device).cuda_stream
+
+    def reset(self, mask=None):
+        """TDGymBasic.reset for the boards in ``mask`` (None = all).  Returns the
+        obs tensor (B, 45, L, L) and the list of boards whose road generation
+        failed (the reference raises or hangs there; those boards are unchanged)."""
+        m = None
+        if mask is not None:
+            m = np.ascontiguousarray(np.asarray(mask, dtype=np.uint8).reshape(self.B))
+        torch.cuda.synchronize(self.device)
+        rc = _lib.lib.td_reset(self._h, _lib.ptr(m, _lib.ctypes.c_uint8) if m is not None else None,
+                               self.obs.data_ptr(), self._stream())
+        _lib.check(rc)
+        failed = []
+        if rc > 0:
+            ids = np.zeros(rc, dtype=np.int32)
+            _lib.lib.td_last_reset_failures(self._h, _lib.ptr(ids, _lib.ctypes.c_int32), rc)
+            failed = ids.tolist()
+        return self.obs, failed
+
+    def reset_layouts(self, recs, boards):
+        recs = _u32(recs).reshape(-1, self.lw)
+        ids = np.ascontiguousarray(boards, dtype=np.int32)
+        torch.cuda.synchronize(self.device)
+        _lib.check(_lib.lib.td_reset_layouts(self._h, _lib.ptr(recs, _lib.ctypes.c_uint32),
+                                             _lib.ptr(ids, _lib.ctypes.c_int32), len(ids), self.obs.data_ptr(),
+                                             self._stream()))
+        return self.obs
+
+    def step(self, def_act=None, atk_act=None):
+        """One step of every board; returns (obs, reward, done) device tensors.
+
+        The tensors are the engine's own buffers, overwritten by the next step
+        (clone them to keep a history)."""
+        io = self._io
+        keep = []
+        if self.mode != "atk":
+            d = _as_dev(def_act, torch.int64, self.device)
+            exp = (self.B, 6, self.L, self.L) if self.multi else (self.B,)
+            if tuple(d.shape) != exp:
+                raise ValueError("defender action must have shape %r" % (exp,))
+            keep.append(d)
+            io.def_act = d.data_ptr()
+        if self.mode != "def":
+            a = _as_dev(atk_act, torch.int64, self.device)
+            if tuple(a.shape) != (self.B, 3, 8):
+                raise ValueError("attacker action must have shape (B, 3, 8)")
+            keep.append(a)
+            io.atk_act = a.data_ptr()
+        _lib.check(_lib.lib.td_step(self._h, io, self._stream()))
+        self._keep = keep  # actions stay alive until the next call
+        return self.obs, self.reward, self.done
+
+    # ----------------------------------------------------------------- state
+    def state_bytes(self, count):
+        return _lib.lib.td_state_bytes(self._h, count)
+
+    def export_state(self, b0=0, count=None):
+        """Raw SoA state of boards [b0, b0+count) as numpy arrays."""
+        count = self.B - b0 if count is None else count
+        buf = np.zeros(self.state_bytes(count), dtype=np.uint8)
+        torch.cuda.synchronize(self.device)
+        _lib.check(_lib.lib.td_export_state(self._h, b0, count, buf.ctypes.data))
+        return _decode_state(buf, count, self.L)
+
+    def import_state(self, st, b0=0):
+        count = len(st["hdr"])
+        buf = _encode_state(st, count, self.L)
+        torch.cuda.synchronize(self.device)
+        _lib.check(_lib.lib.td_import_state(self._h, b0, count, buf.ctypes.data))
+
+    def flags(self):
+        f = np.zeros(self.B, dtype=np.int32)
+        _lib.check(_lib.lib.td_get_flags(self._h, _lib.ptr(f, _lib.ctypes.c_int32)))
+        return f
+
+    def board_state(self, b, st=None):
+        """Canonical state of board b (same record as the reference's board attributes)."""
+        if st is None:
+            st = self.export_state(b, 1)
+            i = 0
+        else:
+            i = b
+        h = st["hdr"][i]
+        n, nt, L = int(h["n_en"]), int(h["n_tw"]), self.L
+        inf = st["en_inf"][i][:n]
+        ens = [(int((u >> 12) & 3), int((u >> 14) & 1), int(u & 0xFFF) // L, int(u & 0xFFF) % L, int(u >> 16),
+                float(st["en_lp"][i][k]), float(st["en_mg"][i][k])) for k, u in enumerate(inf)]
+        tinf = st["tw_inf"][i][:nt]
+        tws = [(int((u >> 12) & 3), int((u >> 14) & 1), int(u & 0xFFF) // L, int(u & 0xFFF) % L,
+                float(st["tw_cd"][i][k])) for k, u in enumerate(tinf)]
+        return {"steps": int(h["steps"]), "base_LP": int(h["base_LP"]), "cost_def": float(h["cost_def"]),
+                "cost_atk": float(h["cost_atk"]), "attacker_cd": int(h["atk_cd"]), "defender_cd": int(h["def_cd"]),
+                "enemies": ens, "towers": tws, "map6": (st["cells"][i] >> 24).astype(np.int64).tolist(),
+                "num_roads": int(h["num_roads"]), "flags": int(h["flags"])}
+
+    def map_planes(self, b, st=None):
+        """TDBoard.map planes 0-6 of board b (int32 (7, L, L)), start list, end."""
+        if st is None:
+            st = self.export_state(b, 1)
+            b = 0
+        cw = st["cells"][b].astype(np.int64)
+        L = self.L
+        m = np.zeros((7, L, L), dtype=np.int32)
+        for p in range(4):
+            m[p] = ((cw >> p) & 1).reshape(L, L)
+        m[4] = ((cw >> 16) & 0xFF).reshape(L, L)
+        m[5] = ((cw >> 8) & 3).reshape(L, L)
+        m[6] = (cw >> 24).reshape(L, L)
+        h = st["hdr"][b]
+        nr = int(h["num_roads"])
+        start = [[int(c) // L, int(c) % L] for c in h["start_cell"][:nr]]
+        end = [int(h["end_cell"]) // L, int(h["end_cell"]) % L]
+        return m, start, end
+
+
+def _as_dev(x, dtype, device):
+    if isinstance(x, torch.Tensor):
+        if x.device != device or x.dtype != dtype or not x.is_contiguous():
+            x = x.to(device=device, dtype=dtype).contiguous()
+        return x
+    return torch.as_tensor(np.asarray(x), dtype=dtype).to(device).contiguous()
+
+
+def _mt_words(state):
+    """random.getstate() / RandomState.get_state() / 625 words -> uint32[625]."""
+    if isinstance(state, tuple) and len(state) == 3 and isinstance(state[1], tuple):  # CPython random
+        return _u32(list(state[1]))
+    if isinstance(state, tuple) and len(state) >= 3 and state[0] == "MT19937":  # numpy RandomState
+        return _u32(list(state[1]) + [int(state[2])])
+    w = _u32(state)
+    if w.shape != (_lib.MT_WORDS,):
+        raise ValueError("expected 625 words")
+    return w
+
+
+def _layout(count, L):
+    return [("hdr", HDR_DTYPE, ()), ("en_lp", np.float64, (_lib.ECAP,)), ("en_mg", np.float64, (_lib.ECAP,)),
+            ("en_inf", np.uint32, (_lib.ECAP,)), ("tw_cd", np.float64, (_lib.TCAP,)),
+            ("tw_inf", np.uint32, (_lib.TCAP,)), ("cells", np.uint32, (L * L,)),
+            ("opp_mt", np.uint32, (_lib.MT_WORDS,))]
+
+
+def _decode_state(buf, count, L):
+    out, off = {}, 0
+    for name, dt, shape in _layout(count, L):
+        dt = np.dtype(dt)
+        n = count * int(np.prod(shape, dtype=np.int64)) if shape else count
+        a = np.frombuffer(buf, dtype=dt, count=n, offset=off)
+        out[name] = a.reshape((count,) + shape) if shape else a
+        off += n * dt.itemsize
+    return out
+
+
+def _encode_state(st, count, L):
+    parts = []
+    for name, dt, shape in _layout(count, L):
+        parts.append(np.ascontiguousarray(st[name], dtype=dt).tobytes())
+    return np.frombuffer(b"".join(parts), dtype=np.uint8).copy()
+
+
+def layout_planes(rec, L):
+    """Layout record (td_layout.h) -> (map planes int32 (7, L, L), start list, end, num_roads)."""
+    rec = np.asarray(rec, dtype=np.uint32)
+    cw = rec[8:8 + L * L].astype(np.int64)
+    m = np.zeros((7, L, L), dtype=np.int32)
+    for p in range(4):
+        m[p] = ((cw >> p) & 1).reshape(L, L)
+    m[4] = ((cw >> 16) & 0xFF).reshape(L, L)
+    m[5] = ((cw >> 8) & 3).reshape(L, L)
+    m[6] = (cw >> 24).reshape(L, L)
+    nr = int(rec[1])
+    start = [[int(c) // L, int(c) % L] for c in rec[4:4 + nr]]
+    end = [int(rec[2]) // L, int(rec[2]) % L]
+    return m, start, end, nr
+
+
+def generate_layout(np_state, L, max_attempts=20000):
+    """TDGymBasic.reset's draws (num_roads + create_road_v2) on a 625-word numpy
+    stream, in place; returns (status, record)."""
+    rec = np.zeros(8 + L * L, dtype=np.uint32)
+    st = _lib.lib.td_layout_generate(_lib.ptr(np_state, _lib.ctypes.c_uint32), L, max_attempts,
+                                     _lib.ptr(rec, _lib.ctypes.c_uint32))
+    return st, rec

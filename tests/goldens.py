@@ -102,5 +102,5 @@ def replay_oracle(tr, max_steps=None):
         obs, rew, done, info = env.step(da, aa)
         got = {"r": canon.fhex(rew), "d": int(bool(done)), "o": canon.obs_digest(obs),
                "s": canon.state_digest(canon.oracle_state(env)), "_obs": obs, "_env": env, "_k": k,
-               "_info": info, "_da": da}
+               "_info": info, "_da": da, "_aa": aa}
         yield i, rec, got

@@ -1,0 +1,218 @@
+"""GPU parity: the HIP step (through the C-ABI) against the reference's golden
+vectors and the CPU oracle, bit-exact (rewards, state, observation bytes)."""
+import contextlib
+
+import numpy as np
+import pytest
+import torch
+
+import goldens as G
+from oracle import canon, policies
+from oracle import td_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+if not torch.cuda.is_available():  # collected on CPU too, so skip cleanly
+    pytest.skip("needs a GPU", allow_module_level=True)
+
+import gym_TD  # noqa: E402
+from gym_TD import envs as E  # noqa: E402
+from gym_TD import params as P  # noqa: E402
+from gym_TD.engine import TDEngine  # noqa: E402
+
+from test_oracle_golden import _info_view  # noqa: E402
+
+
+@contextlib.contextmanager
+def reference_settings(overrides, multi):
+    saved = {k: (v if not isinstance(v, list) else [list(x) for x in v]) for k, v in P.config.__dict__.items()}
+    saved_multi = P.hyper_parameters.allow_multiple_actions
+    try:
+        for k, v in overrides.items():
+            setattr(P.config, k, v)
+        object.__setattr__(P.hyper_parameters, "allow_multiple_actions", bool(multi))
+        yield
+    finally:
+        for k, v in saved.items():
+            setattr(P.config, k, v)
+        object.__setattr__(P.hyper_parameters, "allow_multiple_actions", saved_multi)
+
+
+def _make_env(tr):
+    cls = {"def": E.TDDefense, "atk": E.TDAttack, "2p": E.TDMulti}[tr["mode"]]
+    kw = dict(seed=tr["seed"], opponent_seed=tr["opp_seed"])
+    if tr["mode"] != "2p":
+        kw["difficulty"] = tr["difficulty"]
+    return cls(tr["L"], **kw)
+
+
+@pytest.mark.parametrize("name", G.traj_names())
+def test_device_replays_golden(name):
+    tr = G.load_traj(name)
+    L = tr["L"]
+    with reference_settings(tr["overrides"], tr["multi"]):
+        env = _make_env(tr)
+        try:
+            rep = G.replay_oracle(tr)
+            _, init, _ = next(rep)
+            st = env._engine.board_state(0)
+            m, start, end = env._engine.map_planes(0)
+            assert canon.layout_digest(m, start, end) == init["lay"]
+            assert env.num_roads == init["nr"]
+            # the cool-downs are env attributes in the reference; the device keeps them in the board header
+            assert canon.state_digest(st) == init["s"]
+            assert canon.obs_digest(env._obs) == init["o"]
+            for i, rec, got in rep:
+                if "reset_error" in rec:
+                    with pytest.raises(RuntimeError):
+                        env.reset()
+                    break
+                if "reset" in rec:
+                    o = env.reset()
+                    m, start, end = env._engine.map_planes(0)
+                    assert canon.layout_digest(m, start, end) == rec["lay"], (name, i)
+                    assert canon.obs_digest(o) == rec["o"], (name, i)
+                    assert canon.state_digest(env._engine.board_state(0)) == rec["s"], (name, i)
+                    continue
+                k = got["_k"]
+                if tr["mode"] == "def":
+                    act = got["_da"]
+                elif tr["mode"] == "atk":
+                    act = got["_aa"]
+                else:
+                    act = {"Attacker": got["_aa"], "Defender": got["_da"]}
+                obs, r, d, info = env.step(act)
+                st = env._engine.board_state(0)
+                if canon.state_digest(st) != rec["s"] or canon.obs_digest(obs) != rec["o"] or canon.fhex(r) != rec["r"]:
+                    want = canon.oracle_state(got["_env"])
+                    bad = np.argwhere(obs != got["_obs"])
+                    pytest.fail("%s step %d: reward %s vs %s\nwant %r\nhave %r\nobs diff %r" % (
+                        name, k, canon.fhex(r), rec["r"], want, st, bad[:10].tolist()))
+                assert int(d) == rec["d"], (name, k)
+                if "info" in rec:
+                    assert _info_view(info) == rec["info"], (name, k, _info_view(info), rec["info"])
+                assert st["flags"] == 0
+        finally:
+            env.close()
+
+
+def _oracle_envs(L, seeds, mode="def", multi=False, difficulty=1):
+    hp = O.Hyper(allow_multiple_actions=multi)
+    return [O.Env(L, G.MODES[mode], difficulty, int(s), int(s), O.Config(), hp, road_attempts=20000) for s in seeds]
+
+
+@pytest.mark.parametrize("L,B,steps", [(10, 96, 260), (20, 32, 160), (30, 16, 120)])
+def test_batched_vs_oracle(L, B, steps):
+    """B boards in one launch vs B oracle envs, random + smart defender actions."""
+    seeds = [s for s in range(1000, 1000 + 3 * B) if L > 10 or s not in (1045,)]
+    orc, ok = [], []
+    for s in seeds:
+        try:
+            orc.append(_oracle_envs(L, [s])[0])
+            ok.append(s)
+        except O.RoadGenError:
+            pass
+        if len(ok) == B:
+            break
+    eng = TDEngine(L, B, "def", False, 1, np_seeds=ok, py_seeds=ok, autoreset=False)
+    try:
+        obs, failed = eng.reset()
+        assert not failed
+        rng = np.random.RandomState(L)
+        for k in range(steps):
+            acts = np.array([policies.discrete_def(rng, L, o._board.map[0], 0.5) for o in orc], dtype=np.int64)
+            eng.step(def_act=torch.from_numpy(acts))
+            want = [o.step(int(a)) for o, a in zip(orc, acts)]
+            ob = eng.obs.cpu().numpy()
+            rw = eng.reward.cpu().numpy()
+            dn = eng.done.cpu().numpy()
+            st = eng.export_state()
+            for b in range(B):
+                wo, wr, wd, _ = want[b]
+                assert canon.fhex(rw[b]) == canon.fhex(wr), (L, k, b)
+                assert canon.state_digest(eng.board_state(b, st)) == canon.state_digest(canon.oracle_state(orc[b])), (L, k, b)
+                assert np.array_equal(ob[b], wo), (L, k, b, np.argwhere(ob[b] != wo)[:5].tolist())
+                assert bool(dn[b]) == wd
+        assert (eng.flags() == 0).all()
+    finally:
+        eng.close()
+
+
+def test_autoreset_matches_explicit_reset():
+    """Auto-reset obs == the obs of an explicit reset on the same streams, and
+    episode stats equal the oracle's episode return/length."""
+    L, B = 10, 8
+    seeds = list(range(500, 500 + B))
+    cfg = O.Config(base_LP=1)  # short episodes
+    with reference_settings({"base_LP": 1}, False):
+        ea = TDEngine(L, B, "def", False, 1, np_seeds=seeds, py_seeds=seeds, autoreset=True)
+        eb = TDEngine(L, B, "def", False, 1, np_seeds=seeds, py_seeds=seeds, autoreset=False)
+    try:
+        ea.reset()
+        eb.reset()
+        orc = [O.Env(L, O.MODE_DEF, 1, s, s, cfg, O.Hyper(), road_attempts=20000) for s in seeds]
+        rets = [0.0] * B
+        rng = np.random.RandomState(3)
+        finished = 0
+        for k in range(400):
+            acts = rng.randint(0, 6 * L * L + 1, size=B).astype(np.int64)
+            ea.step(def_act=torch.from_numpy(acts))
+            eb.step(def_act=torch.from_numpy(acts))
+            da = ea.done.cpu().numpy().copy()
+            assert np.array_equal(da, eb.done.cpu().numpy())
+            assert np.array_equal(ea.reward.cpu().numpy(), eb.reward.cpu().numpy())
+            for b in range(B):
+                _, r, d, _ = orc[b].step(int(acts[b]))
+                rets[b] += r
+                assert bool(d) == bool(da[b])
+                if d:
+                    assert canon.fhex(ea.ep_return[b].item()) == canon.fhex(rets[b])
+                    assert ea.ep_len[b].item() == orc[b]._board.steps
+                    rets[b] = 0.0
+                    orc[b].reset()
+                    finished += 1
+            if da.any():
+                eb.reset(da)
+                assert torch.equal(ea.obs, eb.obs)
+            else:
+                assert torch.equal(ea.obs, eb.obs)
+        assert finished > 0
+    finally:
+        ea.close()
+        eb.close()
+
+
+@pytest.mark.parametrize("L,B,mode,multi", [(10, 65536, "def", False), (20, 16384, "2p", True)])
+def test_full_size_properties(L, B, mode, multi):
+    """BASELINE-sized batches: invariants over every board, bit-exact spot checks vs the oracle."""
+    seeds = np.arange(B, dtype=np.int64) + 7000
+    eng = TDEngine(L, B, mode, multi, 1, np_seeds=seeds, py_seeds=seeds, autoreset=True)
+    try:
+        obs, failed = eng.reset()
+        good = np.ones(B, bool)
+        good[failed] = False
+        picks = [b for b in np.random.RandomState(1).choice(B, 24, replace=False) if good[b]][:12]
+        orc = _oracle_envs(L, [int(seeds[b]) for b in picks], mode, multi)
+        g = torch.Generator(device="cuda").manual_seed(5)
+        for k in range(40):
+            if multi:
+                d = torch.randint(0, 3, (B, 6, L, L), device="cuda", generator=g, dtype=torch.int64)
+            else:
+                d = torch.randint(0, 6 * L * L + 1, (B,), device="cuda", generator=g, dtype=torch.int64)
+            a = torch.randint(0, 5, (B, 3, 8), device="cuda", generator=g, dtype=torch.int64) if mode == "2p" else None
+            eng.step(def_act=d, atk_act=a)
+            ob = eng.obs
+            assert float(ob.min()) >= 0.0 and float(ob.max()) <= 1.0
+            assert torch.equal(ob[:, 0], (ob[:, 1:4].sum(1) > 0).float())
+            dh = d[picks].cpu().numpy()
+            ah = a[picks].cpu().numpy() if a is not None else [None] * len(picks)
+            obh = ob[picks].cpu().numpy()
+            rwh = eng.reward[picks].cpu().numpy()
+            for j, o in enumerate(orc):
+                wo, wr, wd, _ = o.step(dh[j] if multi else int(dh[j]), ah[j])
+                assert canon.fhex(rwh[j]) == canon.fhex(wr)
+                assert np.array_equal(obh[j], wo)
+        fl = eng.flags()
+        assert (fl[good] == 0).all()
+    finally:
+        eng.close()

@@ -1,0 +1,135 @@
+"""CPU tests of libtdstep.so's host side (no GPU): exported symbols, the two
+MT19937 streams, native road generation and layout records, pinned against
+CPython ``random``, numpy ``RandomState`` and the reference's golden road table."""
+import random
+import re
+
+import numpy as np
+import pytest
+
+import goldens as G
+from oracle import canon
+from oracle import td_oracle as O
+
+from gym_TD import _lib
+from gym_TD.engine import generate_layout, layout_planes
+
+lib = _lib.lib
+U32 = _lib.ctypes.c_uint32
+
+
+def _p(a):
+    return _lib.ptr(a, U32)
+
+
+def test_header_symbols_exported():
+    hdr = open(G.GOLDEN + "/../../include/tdstep.h").read()
+    names = set(re.findall(r"\b(td_[a-z_0-9]+)\s*\(", hdr))
+    assert len(names) >= 25
+    for n in sorted(names):
+        assert hasattr(lib, n), n
+
+
+def test_config_default_matches_reference_defaults():
+    c = _lib.TdConfig()
+    lib.td_config_default(c)
+    ref = O.Config()
+    for name in ("enemy_LP", "enemy_speed", "enemy_defense", "enemy_cost", "tower_attack", "tower_range",
+                 "tower_splash_range", "tower_cost", "tower_attack_interval"):
+        assert [[getattr(c, name)[t][l] for l in range(2)] for t in range(4)] == getattr(ref, name)
+    for name in ("tower_destruct_return", "frozen_time", "frozen_ratio", "attacker_init_cost",
+                 "defender_init_cost", "base_LP", "max_cost", "reward_kill", "penalty_leak", "reward_time",
+                 "attacker_cost_init_rate", "attacker_cost_final_rate", "defender_cost_rate", "tower_distance",
+                 "enemy_upgrade_at"):
+        assert getattr(c, name) == getattr(ref, name), name
+    assert c.max_episode_steps == 1200 and c.max_cluster_length == 8 and c.max_num_of_roads == 3
+
+
+@pytest.mark.parametrize("seed", [0, 1, 42, 2 ** 31 + 7, 2 ** 32 - 1])
+def test_cpython_random_stream(seed):
+    w = np.zeros(625, np.uint32)
+    lib.td_py_seed(_p(w), seed)
+    r = random.Random(seed)
+    st = r.getstate()[1]
+    assert list(w[:624]) == list(st[:624]) and int(w[624]) == st[624]
+    for n in (1, 2, 3, 4, 5, 8, 25, 100, 1000):
+        for _ in range(50):
+            assert lib.td_py_randint(_p(w), 0, n - 1) == r.randint(0, n - 1)
+    for _ in range(2000):
+        assert lib.td_mt_next(_p(w)) == r.getrandbits(32)
+
+
+@pytest.mark.parametrize("seed", [0, 3, 1024, 2 ** 32 - 1])
+def test_numpy_legacy_stream(seed):
+    w = np.zeros(625, np.uint32)
+    lib.td_np_seed(_p(w), seed)
+    rs = np.random.RandomState(seed)
+    st = rs.get_state()
+    assert list(w[:624]) == list(st[1]) and int(w[624]) == st[2]
+    for lo, hi in ((0, 1), (0, 2), (0, 4), (1, 4), (3, 7), (1, 2), (0, 3), (5, 17), (0, 1000)):
+        for _ in range(40):
+            assert lib.td_np_randint(_p(w), lo, hi) == rs.randint(lo, hi)
+
+
+def test_roadgen_matches_reference_table():
+    """Native create_road_v2 vs the reference's reset outcome, 1200 env seeds."""
+    table = G.load_roadgen()
+    for Ls, rows in table.items():
+        L = int(Ls)
+        for s, row in rows.items():
+            w = np.zeros(625, np.uint32)
+            lib.td_np_seed(_p(w), int(s))
+            st, rec = generate_layout(w, L)
+            if "err" in row:
+                assert st != 0, (L, s)
+                continue
+            assert st == 0, (L, s, st)
+            m, start, end, nr = layout_planes(rec, L)
+            assert nr == row["nr"]
+            assert canon.layout_digest(m, start, end) == row["lay"], (L, s)
+            # the stream is left where the reference leaves it
+            assert lib.td_np_randint(_p(w), 0, 2 ** 31 - 1) == row["next"], (L, s)
+
+
+def test_roadgen_error_kinds_match_oracle():
+    """Failing L=10 seeds: same failure, same stream position as the oracle restatement."""
+    for s in (1, 45, 54, 55, 217):
+        w = np.zeros(625, np.uint32)
+        lib.td_np_seed(_p(w), s)
+        st, _ = generate_layout(w, 10)
+        rng = np.random.RandomState(s)
+        nr = rng.randint(1, 4)
+        with pytest.raises(O.RoadGenError):
+            O.create_road(rng, 10, nr, max_attempts=20000)
+        assert st in (1, 2)
+        assert lib.td_np_randint(_p(w), 0, 2 ** 31 - 1) == rng.randint(0, 2 ** 31 - 1)
+
+
+def test_layout_from_roads_matches_board_planes():
+    rng = np.random.RandomState(7)
+    for L in (10, 20, 30):
+        for _ in range(5):
+            nr = rng.randint(1, 4)
+            try:
+                roads = O.create_road(rng, L, nr, max_attempts=20000)
+            except O.RoadGenError:
+                continue
+            m, start, end = O.layout_from_roads(roads, L)
+            cells = np.asarray([p[0] * L + p[1] for r in roads for p in r], dtype=np.int32)
+            off = np.cumsum([0] + [len(r) for r in roads]).astype(np.int32)
+            rec = np.zeros(8 + L * L, np.uint32)
+            assert lib.td_layout_from_roads(L, len(roads), _lib.ptr(cells, _lib.ctypes.c_int32),
+                                            _lib.ptr(off, _lib.ctypes.c_int32), _p(rec)) == 0
+            m2, s2, e2, nr2 = layout_planes(rec, L)
+            assert np.array_equal(m, m2) and s2 == start and e2 == end and nr2 == len(roads)
+
+
+def test_create_without_gpu_fails_cleanly():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    c = _lib.TdConfig()
+    lib.td_config_default(c)
+    h = lib.td_create(c, 10, 4, 0, 0, 1, 0)
+    assert not h
+    assert lib.td_last_error()
