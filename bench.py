@@ -64,10 +64,12 @@ def _cpu_worker(args):
             _, _, d, _ = env.step(int(rng.randint(0, 6 * L * L + 1)))
             n += 1
             if d:
-                try:
-                    env.reset()
-                except O.RoadGenError:
-                    env.reset()
+                while True:  # the reference raises here for a few L=10 draws; draw again
+                    try:
+                        env.reset()
+                        break
+                    except O.RoadGenError:
+                        pass
     return n, time.perf_counter() - t0
 
 
@@ -117,13 +119,7 @@ def main():
     B, L, K, W = args.boards, args.map_size, args.steps, args.warmup
     seeds = np.arange(B, dtype=np.int64) + args.seed + rank * B
     eng = TDEngine(L, B, "def", False, 1, device=dev, np_seeds=seeds, py_seeds=seeds, autoreset=True, info=True)
-    obs, failed = eng.reset()
-    tries = 0
-    while failed and tries < 64:  # the reference raises/hangs on these draws; redraw from the same stream
-        m = np.zeros(B, np.uint8)
-        m[failed] = 1
-        obs, failed = eng.reset(m)
-        tries += 1
+    obs, _ = eng.reset_all()  # failing road draws (the reference raises/hangs) are redrawn
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     n_act = 6 * L * L + 1
     burn = torch.randint(0, n_act, (max(args.burnin, 1), B), device=dev, generator=g, dtype=torch.int64)

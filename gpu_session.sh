@@ -14,6 +14,6 @@ run() {  # name seconds cmd...
 }
 STEPS=${STEPS:-smoke,tests,bench}
 if [[ $STEPS == *smoke* ]]; then run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $?; fi
-if [[ $STEPS == *tests* ]]; then run pytest_gpu 1200 python -m pytest tests -m gpu -q -x ${PYTEST_ARGS}; rc=$?; [ $rc -le 1 ] || exit $rc; fi
+if [[ $STEPS == *tests* ]]; then run pytest_gpu 1200 python -m pytest tests -m gpu -v -x --timeout 400 ${PYTEST_ARGS}; rc=$?; [ $rc -le 1 ] || exit $rc; fi
 if [[ $STEPS == *bench* ]]; then run bench 400 python bench.py ${BENCH_ARGS} || exit $?; fi
 exit 0

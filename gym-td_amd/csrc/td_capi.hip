@@ -1,5 +1,9 @@
-// td_capi.hip -- the C-ABI (include/tdstep.h): handle, HBM buffers, launches, and
-// the host side of per-episode layouts (numpy-legacy streams + road generation).
+// td_capi.hip -- the C-ABI (include/tdstep.h): handle, HBM buffers, launches.
+//
+// Everything per board lives on the device: board records, both RNG streams
+// (layouts: numpy-legacy MT19937; built-in opponent: CPython MT19937) and the
+// staged next-episode layout.  Layouts are generated on the device
+// (td_refill_kernel / td_reset_kernel), so the step loop has no host work.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -33,43 +37,31 @@ int fail(const char* fmt, ...) {
   return -1;
 }
 
-#define HIP_OK(expr)                                                                     \
-  do {                                                                                   \
-    hipError_t e_ = (expr);                                                              \
+#define HIP_OK(expr)                                                                                         \
+  do {                                                                                                       \
+    hipError_t e_ = (expr);                                                                                  \
     if (e_ != hipSuccess) return fail("%s: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, __LINE__); \
   } while (0)
 
-constexpr int kMaxAttempts = 20000;  // bound for each of create_road_v2's retry loops
-constexpr int kRefillEvery = 4;      // steps between looks at the consumed-layout counters
-constexpr int kRefillMax = 4096;     // layouts generated per refill at most
+constexpr int kRefillEvery = 8;  // steps between refill launches (episodes last >= ~40 steps)
 
 }  // namespace
 
 struct td_handle {
   int L = 0, NC = 0, B = 0, mode = 0, multi = 0, difficulty = 1, device = 0, autoreset = 1;
   int lw = 0;  // layout record words
+  size_t scratch_stride = 0;
   TdDevCfg dcfg;
-  // device
   TdDevCfg* d_cfg = nullptr;
   TdHdr* d_hdr = nullptr;
   double *d_en_lp = nullptr, *d_en_mg = nullptr, *d_tw_cd = nullptr;
-  uint32_t *d_en_inf = nullptr, *d_tw_inf = nullptr, *d_cells = nullptr, *d_opp = nullptr;
-  uint32_t *d_nxt = nullptr, *d_consumed = nullptr, *d_stage = nullptr;
-  int32_t* d_stage_ids = nullptr;
-  uint8_t* d_mask = nullptr;
-  // host
-  std::vector<uint32_t> np_state;   // [B][625] numpy-legacy stream per board (layouts)
-  std::vector<uint32_t> uploaded;   // layouts staged per board so far
-  uint32_t* h_consumed = nullptr;   // pinned copy of d_consumed
-  uint32_t* h_stage = nullptr;      // pinned staging, kRefillMax records
-  int32_t* h_stage_ids = nullptr;
-  hipEvent_t ev_consumed = nullptr, ev_stage = nullptr;
-  bool consumed_pending = false;
+  uint32_t *d_en_inf = nullptr, *d_tw_inf = nullptr, *d_cells = nullptr, *d_opp = nullptr, *d_np = nullptr;
+  uint32_t *d_nxt = nullptr, *d_qcount = nullptr, *d_stage = nullptr;
+  int32_t *d_queue = nullptr, *d_stage_ids = nullptr;
+  uint8_t *d_scratch = nullptr, *d_mask = nullptr, *d_fail = nullptr;
+  int stage_cap = 0;
   long long steps = 0;
-  long long roadgen_failures = 0;
   std::vector<int32_t> last_reset_failed;
-  int nthreads = 1;
-  std::vector<std::vector<uint8_t>> scratch;  // per worker thread
 };
 
 namespace {
@@ -145,67 +137,49 @@ StepArgs base_args(td_handle* h) {
   a.autoreset = h->autoreset;
   a.hdr = h->d_hdr; a.en_lp = h->d_en_lp; a.en_mg = h->d_en_mg; a.en_inf = h->d_en_inf;
   a.tw_cd = h->d_tw_cd; a.tw_inf = h->d_tw_inf; a.cells = h->d_cells; a.opp_mt = h->d_opp;
-  a.nxt = h->d_nxt; a.consumed = h->d_consumed; a.cfg = h->d_cfg;
+  a.np_mt = h->d_np; a.nxt = h->d_nxt; a.scratch = h->d_scratch; a.scratch_stride = h->scratch_stride;
+  a.queue = h->d_queue; a.qcount = h->d_qcount; a.reset_fail = h->d_fail; a.cfg = h->d_cfg;
   return a;
 }
 
-// Draw the next episode layout of board b from its numpy stream.  A draw whose
-// road generation fails (the reference raises / hangs) is skipped and the stream
-// continues; failures are counted.
-int gen_next(td_handle* h, int b, uint32_t* rec, std::vector<uint8_t>& scratch, bool retry) {
-  for (int tries = 0; tries < 64; ++tries) {
-    int st = episode_layout(&h->np_state[(size_t)b * (MT_N + 1)], h->L, scratch.data(), kMaxAttempts, rec);
-    if (st == ROAD_OK) return 0;
-    __atomic_fetch_add(&h->roadgen_failures, 1, __ATOMIC_RELAXED);
-    if (!retry) return st;
-  }
-  return ROAD_ERR_BOUND;
-}
-
-// fn(i, worker) for i in [0, n) on up to h->nthreads host threads.
+// fn(i) for i in [0, n) on a few host threads (seeding only).
 template <class F>
-void parallel_for(td_handle* h, int n, F fn) {
-  int nt = std::max(1, std::min(h->nthreads, (n + 7) / 8));
-  if (nt == 1) {
-    for (int i = 0; i < n; ++i) fn(i, 0);
-    return;
-  }
+void parallel_for(int n, F fn) {
+  unsigned hw = std::thread::hardware_concurrency();
+  int nt = std::max(1, std::min<int>((int)std::min(8u, hw ? hw : 1u), (n + 1023) / 1024));
   std::vector<std::thread> pool;
   for (int w = 0; w < nt; ++w)
     pool.emplace_back([&, w]() {
-      for (int i = w; i < n; i += nt) fn(i, w);
+      for (int i = w; i < n; i += nt) fn(i);
     });
   for (auto& t : pool) t.join();
 }
 
-// Stage the records of boards ids[0..n) from h_stage into their nxt slots.
-int stage(td_handle* h, int n, hipStream_t s) {
-  if (n <= 0) return 0;
-  HIP_OK(hipMemcpyAsync(h->d_stage, h->h_stage, (size_t)n * h->lw * 4, hipMemcpyHostToDevice, s));
-  HIP_OK(hipMemcpyAsync(h->d_stage_ids, h->h_stage_ids, (size_t)n * 4, hipMemcpyHostToDevice, s));
-  HIP_OK(launch_stage_layouts(h->d_nxt, h->d_stage, h->d_stage_ids, n, h->lw, s));
-  HIP_OK(hipEventRecord(h->ev_stage, s));
+// Drop staged layouts: they were drawn from a stream that has been replaced.
+int drop_staged(td_handle* h, int b) {
+  HIP_OK(hipDeviceSynchronize());
+  HIP_OK(hipMemset(h->d_nxt + (size_t)b * h->lw, 0, 4));
   return 0;
 }
 
-// Top up the next-episode layouts of boards whose staged layout was consumed.
-int refill(td_handle* h, hipStream_t s) {
-  if (!h->consumed_pending) return 0;
-  if (hipEventQuery(h->ev_consumed) != hipSuccess) return 0;  // copy not landed yet: try later
-  h->consumed_pending = false;
-  std::vector<int> need;
-  for (int b = 0; b < h->B; ++b)
-    if (h->h_consumed[b] >= h->uploaded[b]) need.push_back(b);
-  if (need.empty()) return 0;
-  HIP_OK(hipEventSynchronize(h->ev_stage));  // previous staging copy done with h_stage
-  int n = (int)std::min<size_t>(need.size(), kRefillMax);
-  parallel_for(h, n, [&](int i, int w) {
-    int b = need[(size_t)i];
-    gen_next(h, b, h->h_stage + (size_t)i * h->lw, h->scratch[(size_t)w], true);
-    h->h_stage_ids[i] = b;
-  });
-  for (int i = 0; i < n; ++i) h->uploaded[need[i]] += 1;
-  return stage(h, n, s);
+int drop_all_staged(td_handle* h) {
+  HIP_OK(hipDeviceSynchronize());
+  HIP_OK(hipMemset(h->d_nxt, 0, (size_t)h->B * h->lw * 4));
+  HIP_OK(hipMemset(h->d_qcount, 0, 4));
+  return 0;
+}
+
+int run_reset(td_handle* h, const std::vector<uint8_t>& mask, float* obs, hipStream_t s) {
+  HIP_OK(hipMemcpy(h->d_mask, mask.data(), (size_t)h->B, hipMemcpyHostToDevice));
+  HIP_OK(hipMemset(h->d_fail, 0, (size_t)h->B));
+  StepArgs a = base_args(h);
+  a.obs = obs;
+  a.reset_mask = h->d_mask;
+  a.stage_next = h->autoreset;
+  HIP_OK(launch_step(a, s, true));
+  if (h->autoreset) HIP_OK(launch_refill(a, s));
+  HIP_OK(hipStreamSynchronize(s));
+  return 0;
 }
 
 }  // namespace
@@ -273,10 +247,15 @@ td_handle* td_create(const td_config* cfg, int map_size, int n_boards, int mode,
   if (mode == TD_MODE_DEF && (difficulty < 0 || difficulty > 1)) { fail("TD-def difficulty must be 0 or 1 (random_enemy_lv0/lv1)"); return nullptr; }
   if (mode == TD_MODE_ATK && (difficulty < 0 || difficulty > 2)) { fail("TD-atk difficulty must be 0, 1 or 2 (random_tower_lv0/1/2)"); return nullptr; }
   if (mode == TD_MODE_ATK && multi_action) { fail("TD-atk has no multi-action defender"); return nullptr; }
-  if (hipSetDevice(device) != hipSuccess) { fail("hipSetDevice(%d) failed", device); return nullptr; }
+  if (hipSetDevice(device) != hipSuccess) {
+    fail("hipSetDevice(%d) failed: %s", device, hipGetErrorString(hipGetLastError()));
+    return nullptr;
+  }
   td_handle* h = new td_handle();
   h->L = map_size; h->NC = map_size * map_size; h->B = n_boards; h->mode = mode; h->multi = multi_action ? 1 : 0;
   h->difficulty = difficulty; h->device = device; h->lw = layout_words(map_size);
+  h->scratch_stride = (road_scratch_bytes(map_size) + 15) & ~(size_t)15;
+  h->stage_cap = std::min(n_boards, 4096);
   build_dev_cfg(*cfg, h->dcfg);
   const size_t B = (size_t)n_boards;
   int rc = 0;
@@ -289,28 +268,17 @@ td_handle* td_create(const td_config* cfg, int map_size, int n_boards, int mode,
   rc |= dalloc(&h->d_tw_inf, B * TCAP);
   rc |= dalloc(&h->d_cells, B * h->NC);
   rc |= dalloc(&h->d_opp, B * (MT_N + 1));
+  rc |= dalloc(&h->d_np, B * (MT_N + 1));
   rc |= dalloc(&h->d_nxt, B * h->lw);
-  rc |= dalloc(&h->d_consumed, B);
-  rc |= dalloc(&h->d_stage, (size_t)kRefillMax * h->lw);
-  rc |= dalloc(&h->d_stage_ids, (size_t)kRefillMax);
+  rc |= dalloc(&h->d_scratch, B * h->scratch_stride);
+  rc |= dalloc(&h->d_queue, B);
+  rc |= dalloc(&h->d_qcount, 1);
   rc |= dalloc(&h->d_mask, B);
+  rc |= dalloc(&h->d_fail, B);
+  rc |= dalloc(&h->d_stage, (size_t)h->stage_cap * h->lw);
+  rc |= dalloc(&h->d_stage_ids, (size_t)h->stage_cap);
   if (!rc && hipMemcpy(h->d_cfg, &h->dcfg, sizeof(TdDevCfg), hipMemcpyHostToDevice) != hipSuccess) rc = fail("cfg upload");
-  if (!rc && hipHostMalloc((void**)&h->h_consumed, B * 4, hipHostMallocDefault) != hipSuccess) rc = fail("pinned alloc");
-  if (!rc && hipHostMalloc((void**)&h->h_stage, (size_t)kRefillMax * h->lw * 4, hipHostMallocDefault) != hipSuccess) rc = fail("pinned alloc");
-  if (!rc && hipHostMalloc((void**)&h->h_stage_ids, (size_t)kRefillMax * 4, hipHostMallocDefault) != hipSuccess) rc = fail("pinned alloc");
-  if (!rc && hipEventCreateWithFlags(&h->ev_consumed, hipEventDisableTiming) != hipSuccess) rc = fail("event");
-  if (!rc && hipEventCreateWithFlags(&h->ev_stage, hipEventDisableTiming) != hipSuccess) rc = fail("event");
   if (rc) { std::string e = g_err; td_destroy(h); g_err = e; return nullptr; }
-  h->np_state.assign(B * (MT_N + 1), 0u);
-  h->uploaded.assign(B, 0u);
-  {
-    const char* env = getenv("TD_HOST_THREADS");
-    unsigned hw = std::thread::hardware_concurrency();
-    h->nthreads = env ? atoi(env) : (int)std::min(8u, hw ? hw : 1u);
-    if (h->nthreads < 1) h->nthreads = 1;
-  }
-  h->scratch.resize((size_t)h->nthreads);
-  for (auto& s : h->scratch) s.resize(road_scratch_bytes(map_size));
   std::vector<uint32_t> seeds(B);
   for (size_t b = 0; b < B; ++b) seeds[b] = (uint32_t)b;
   if (td_seed(h, seeds.data(), seeds.data()) != 0) { std::string e = g_err; td_destroy(h); g_err = e; return nullptr; }
@@ -321,15 +289,11 @@ void td_destroy(td_handle* h) {
   if (!h) return;
   (void)hipSetDevice(h->device);
   (void)hipDeviceSynchronize();
-  void* dptrs[] = {h->d_cfg, h->d_hdr, h->d_en_lp, h->d_en_mg, h->d_en_inf, h->d_tw_cd, h->d_tw_inf, h->d_cells,
-                   h->d_opp, h->d_nxt, h->d_consumed, h->d_stage, h->d_stage_ids, h->d_mask};
+  void* dptrs[] = {h->d_cfg, h->d_hdr, h->d_en_lp, h->d_en_mg, h->d_en_inf, h->d_tw_cd, h->d_tw_inf,
+                   h->d_cells, h->d_opp, h->d_np, h->d_nxt, h->d_scratch, h->d_queue, h->d_qcount,
+                   h->d_mask, h->d_fail, h->d_stage, h->d_stage_ids};
   for (void* p : dptrs)
     if (p) (void)hipFree(p);
-  if (h->h_consumed) (void)hipHostFree(h->h_consumed);
-  if (h->h_stage) (void)hipHostFree(h->h_stage);
-  if (h->h_stage_ids) (void)hipHostFree(h->h_stage_ids);
-  if (h->ev_consumed) (void)hipEventDestroy(h->ev_consumed);
-  if (h->ev_stage) (void)hipEventDestroy(h->ev_stage);
   delete h;
 }
 
@@ -351,125 +315,51 @@ int td_set_autoreset(td_handle* h, int on) {
 int td_seed(td_handle* h, const uint32_t* np_seeds, const uint32_t* py_seeds) {
   if (!h) return fail("NULL handle");
   const size_t B = (size_t)h->B, W = MT_N + 1;
+  std::vector<uint32_t> st(B * W);
   if (np_seeds) {
-    for (size_t b = 0; b < B; ++b) np_seed(&h->np_state[b * W], np_seeds[b]);
-    // staged next layouts came from the old streams: drop them
-    HIP_OK(hipDeviceSynchronize());
-    HIP_OK(hipMemcpy(h->h_consumed, h->d_consumed, B * 4, hipMemcpyDeviceToHost));
-    for (size_t b = 0; b < B; ++b) h->uploaded[b] = h->h_consumed[b];
-    std::vector<uint32_t> zero(B * (size_t)h->lw, 0u);
-    HIP_OK(hipMemcpy(h->d_nxt, zero.data(), zero.size() * 4, hipMemcpyHostToDevice));
-    h->consumed_pending = false;
+    parallel_for((int)B, [&](int b) { np_seed(&st[(size_t)b * W], np_seeds[b]); });
+    if (drop_all_staged(h)) return -1;
+    HIP_OK(hipMemcpy(h->d_np, st.data(), B * W * 4, hipMemcpyHostToDevice));
   }
   if (py_seeds) {
-    std::vector<uint32_t> opp(B * W);
-    parallel_for(h, (int)B, [&](int b, int) { py_seed(&opp[(size_t)b * W], py_seeds[b]); });
+    parallel_for((int)B, [&](int b) { py_seed(&st[(size_t)b * W], py_seeds[b]); });
     HIP_OK(hipDeviceSynchronize());
-    HIP_OK(hipMemcpy(h->d_opp, opp.data(), B * W * 4, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(h->d_opp, st.data(), B * W * 4, hipMemcpyHostToDevice));
   }
+  return 0;
+}
+
+static int mt_copy(td_handle* h, uint32_t* dev, int b, uint32_t* host, bool to_dev) {
+  if (!h || b < 0 || b >= h->B || !host) return fail("bad board or NULL state");
+  HIP_OK(hipDeviceSynchronize());
+  if (to_dev) HIP_OK(hipMemcpy(dev + (size_t)b * (MT_N + 1), host, (MT_N + 1) * 4, hipMemcpyHostToDevice));
+  else HIP_OK(hipMemcpy(host, dev + (size_t)b * (MT_N + 1), (MT_N + 1) * 4, hipMemcpyDeviceToHost));
   return 0;
 }
 
 int td_set_py_state(td_handle* h, int b, const uint32_t* mt) {
-  if (!h || b < 0 || b >= h->B) return fail("bad board");
-  HIP_OK(hipDeviceSynchronize());
-  HIP_OK(hipMemcpy(h->d_opp + (size_t)b * (MT_N + 1), mt, (MT_N + 1) * 4, hipMemcpyHostToDevice));
-  return 0;
+  return mt_copy(h, h ? h->d_opp : nullptr, b, const_cast<uint32_t*>(mt), true);
 }
-
-int td_get_py_state(td_handle* h, int b, uint32_t* mt) {
-  if (!h || b < 0 || b >= h->B) return fail("bad board");
-  HIP_OK(hipDeviceSynchronize());
-  HIP_OK(hipMemcpy(mt, h->d_opp + (size_t)b * (MT_N + 1), (MT_N + 1) * 4, hipMemcpyDeviceToHost));
-  return 0;
-}
-
+int td_get_py_state(td_handle* h, int b, uint32_t* mt) { return mt_copy(h, h ? h->d_opp : nullptr, b, mt, false); }
+int td_get_np_state(td_handle* h, int b, uint32_t* mt) { return mt_copy(h, h ? h->d_np : nullptr, b, mt, false); }
 int td_set_np_state(td_handle* h, int b, const uint32_t* mt) {
-  if (!h || b < 0 || b >= h->B) return fail("bad board");
-  std::memcpy(&h->np_state[(size_t)b * (MT_N + 1)], mt, (MT_N + 1) * 4);
-  // a staged next layout was drawn from the old stream: drop it
-  HIP_OK(hipDeviceSynchronize());
-  uint32_t c = 0;
-  HIP_OK(hipMemcpy(&c, h->d_consumed + b, 4, hipMemcpyDeviceToHost));
-  h->uploaded[(size_t)b] = c;
-  uint32_t zero = 0;
-  HIP_OK(hipMemcpy(h->d_nxt + (size_t)b * h->lw, &zero, 4, hipMemcpyHostToDevice));
-  return 0;
-}
-
-int td_get_np_state(td_handle* h, int b, uint32_t* mt) {
-  if (!h || b < 0 || b >= h->B) return fail("bad board");
-  std::memcpy(mt, &h->np_state[(size_t)b * (MT_N + 1)], (MT_N + 1) * 4);
-  return 0;
-}
-
-// Stage records h_stage[0..n) (board ids in h_stage_ids) into the next-layout slots.
-static int stage_sync(td_handle* h, int n, hipStream_t s) {
-  if (stage(h, n, s)) return -1;
-  HIP_OK(hipStreamSynchronize(s));
-  return 0;
-}
-
-// Run the reset kernel on the boards with mask[b] != 0 (their staged layout is consumed).
-static int run_reset(td_handle* h, const std::vector<uint8_t>& mask, float* obs, hipStream_t s) {
-  HIP_OK(hipMemcpy(h->d_mask, mask.data(), (size_t)h->B, hipMemcpyHostToDevice));
-  StepArgs a = base_args(h);
-  a.obs = obs;
-  a.reset_mask = h->d_mask;
-  HIP_OK(launch_step(a, s, true));
-  HIP_OK(hipStreamSynchronize(s));
-  return 0;
-}
-
-// Generate (one draw sequence each, from the boards' numpy streams) and stage the
-// next-episode layout of boards ``bs``; returns the boards that failed (no retry)
-// or 0 with ``retry``.
-static int gen_and_stage(td_handle* h, const std::vector<int>& bs, bool retry, std::vector<int>* failed, hipStream_t s) {
-  for (size_t j0 = 0; j0 < bs.size(); j0 += kRefillMax) {
-    int m = (int)std::min<size_t>(kRefillMax, bs.size() - j0);
-    std::vector<int> st((size_t)m);
-    parallel_for(h, m, [&](int j, int w) {
-      st[(size_t)j] = gen_next(h, bs[j0 + j], h->h_stage + (size_t)j * h->lw, h->scratch[(size_t)w], retry);
-    });
-    int k = 0;
-    for (int j = 0; j < m; ++j) {
-      int b = bs[j0 + j];
-      if (st[(size_t)j] != ROAD_OK) { if (failed) failed->push_back(b); continue; }
-      if (k != j) std::memcpy(h->h_stage + (size_t)k * h->lw, h->h_stage + (size_t)j * h->lw, (size_t)h->lw * 4);
-      h->h_stage_ids[k++] = b;
-      h->uploaded[(size_t)b] += 1;
-    }
-    if (stage_sync(h, k, s)) return -1;
-  }
-  return 0;
+  if (mt_copy(h, h ? h->d_np : nullptr, b, const_cast<uint32_t*>(mt), true)) return -1;
+  return drop_staged(h, b);
 }
 
 int td_reset(td_handle* h, const uint8_t* host_mask, float* obs, void* stream) {
   if (!h) return fail("NULL handle");
   hipStream_t s = (hipStream_t)stream;
+  std::vector<uint8_t> mask((size_t)h->B, 1);
+  if (host_mask) std::memcpy(mask.data(), host_mask, (size_t)h->B);
   HIP_OK(hipDeviceSynchronize());
-  HIP_OK(hipMemcpy(h->h_consumed, h->d_consumed, (size_t)h->B * 4, hipMemcpyDeviceToHost));
-  h->consumed_pending = false;
-  std::vector<int> ids, gen;
-  for (int b = 0; b < h->B; ++b) {
-    if (host_mask && !host_mask[b]) continue;
-    ids.push_back(b);
-    // TDGymBasic.reset draws the layout that follows on the board's stream: the
-    // staged one when present, otherwise a fresh draw now.
-    if (h->h_consumed[b] >= h->uploaded[(size_t)b]) gen.push_back(b);
-  }
-  std::vector<int> failed;
-  if (gen_and_stage(h, gen, false, &failed, s)) return -1;
-  h->last_reset_failed.assign(failed.begin(), failed.end());
-  std::vector<uint8_t> mask((size_t)h->B, 0);
-  for (int b : ids) mask[(size_t)b] = 1;
-  for (int b : failed) mask[(size_t)b] = 0;
-  std::vector<int> done;
-  for (int b : ids) if (mask[(size_t)b]) done.push_back(b);
-  if (!done.empty() && run_reset(h, mask, obs, s)) return -1;
-  // the layout for the episode after this one, consumed by the auto-reset
-  if (gen_and_stage(h, done, true, nullptr, s)) return -1;
-  return (int)failed.size();
+  if (run_reset(h, mask, obs, s)) return -1;
+  std::vector<uint8_t> fl((size_t)h->B);
+  HIP_OK(hipMemcpy(fl.data(), h->d_fail, (size_t)h->B, hipMemcpyDeviceToHost));
+  h->last_reset_failed.clear();
+  for (int b = 0; b < h->B; ++b)
+    if (mask[(size_t)b] && fl[(size_t)b]) h->last_reset_failed.push_back(b);
+  return (int)h->last_reset_failed.size();
 }
 
 int td_last_reset_failures(td_handle* h, int32_t* boards, int cap) {
@@ -486,20 +376,16 @@ int td_reset_layouts(td_handle* h, const uint32_t* recs, const int32_t* boards, 
     if (boards[i] < 0 || boards[i] >= h->B || recs[(size_t)i * h->lw] != TD_LAYOUT_MAGIC)
       return fail("td_reset_layouts: bad board id or layout record %d", i);
   HIP_OK(hipDeviceSynchronize());
-  std::vector<uint8_t> mask((size_t)h->B, 0);
-  for (int i0 = 0; i0 < n; i0 += kRefillMax) {
-    int m = std::min(kRefillMax, n - i0);
-    std::memcpy(h->h_stage, recs + (size_t)i0 * h->lw, (size_t)m * h->lw * 4);
-    std::memcpy(h->h_stage_ids, boards + i0, (size_t)m * 4);
-    if (stage_sync(h, m, s)) return -1;
+  for (int i0 = 0; i0 < n; i0 += h->stage_cap) {
+    int m = std::min(h->stage_cap, n - i0);
+    HIP_OK(hipMemcpy(h->d_stage, recs + (size_t)i0 * h->lw, (size_t)m * h->lw * 4, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(h->d_stage_ids, boards + i0, (size_t)m * 4, hipMemcpyHostToDevice));
+    HIP_OK(launch_stage_layouts(h->d_nxt, h->d_stage, h->d_stage_ids, m, h->lw, s));
+    HIP_OK(hipStreamSynchronize(s));
   }
+  std::vector<uint8_t> mask((size_t)h->B, 0);
   for (int i = 0; i < n; ++i) mask[(size_t)boards[i]] = 1;
-  if (n > 0 && run_reset(h, mask, obs, s)) return -1;
-  // explicit layouts leave no staged next layout: the next refill draws from the stream
-  HIP_OK(hipMemcpy(h->h_consumed, h->d_consumed, (size_t)h->B * 4, hipMemcpyDeviceToHost));
-  for (int i = 0; i < n; ++i) h->uploaded[(size_t)boards[i]] = h->h_consumed[boards[i]];
-  h->consumed_pending = false;
-  return 0;
+  return run_reset(h, mask, obs, s);
 }
 
 int td_step(td_handle* h, const td_step_io* io, void* stream) {
@@ -508,18 +394,13 @@ int td_step(td_handle* h, const td_step_io* io, void* stream) {
   if (h->mode != TD_MODE_ATK && !io->def_act) return fail("td_step: def_act required in this mode");
   if (h->mode != TD_MODE_DEF && !io->atk_act) return fail("td_step: atk_act required in this mode");
   hipStream_t s = (hipStream_t)stream;
-  if (h->autoreset && refill(h, s)) return -1;
   StepArgs a = base_args(h);
   a.def_act = io->def_act; a.atk_act = io->atk_act; a.obs = io->obs; a.reward = io->reward; a.done = io->done;
   a.real_def = io->real_def; a.real_atk = io->real_atk; a.fail_def = io->fail_def; a.fail_atk = io->fail_atk;
   a.win = io->win; a.allow_next = io->allow_next; a.ep_return = io->ep_return; a.ep_len = io->ep_len;
   HIP_OK(launch_step(a, s, false));
   h->steps += 1;
-  if (h->autoreset && !h->consumed_pending && (h->steps % kRefillEvery) == 0) {
-    HIP_OK(hipMemcpyAsync(h->h_consumed, h->d_consumed, (size_t)h->B * 4, hipMemcpyDeviceToHost, s));
-    HIP_OK(hipEventRecord(h->ev_consumed, s));
-    h->consumed_pending = true;
-  }
+  if (h->autoreset && (h->steps % kRefillEvery) == 0) HIP_OK(launch_refill(a, s));
   return 0;
 }
 
@@ -533,7 +414,7 @@ int td_layout_from_roads(int map_size, int num_roads, const int32_t* cells, cons
 int td_layout_generate(uint32_t* np_state625, int map_size, int max_attempts, uint32_t* rec) {
   if (map_size < 4 || map_size > MAX_L) return fail("map_size out of range");
   std::vector<uint8_t> scratch(road_scratch_bytes(map_size));
-  return episode_layout(np_state625, map_size, scratch.data(), max_attempts > 0 ? max_attempts : kMaxAttempts, rec);
+  return episode_layout(np_state625, map_size, scratch.data(), max_attempts > 0 ? max_attempts : kRoadAttempts, rec);
 }
 
 size_t td_state_bytes(td_handle* h, int count) {

@@ -16,8 +16,14 @@ struct StepArgs {
   uint32_t* tw_inf;
   uint32_t* cells;
   uint32_t* opp_mt;     // [B][625] CPython-random state of the built-in opponent
+  uint32_t* np_mt;      // [B][625] numpy-legacy state of the layout stream (TDGymBasic.np_random)
   uint32_t* nxt;        // [B][8 + L*L] staged next-episode layout (word 0 = magic while unconsumed)
-  uint32_t* consumed;   // [B] layouts consumed so far (host refills when it catches up)
+  uint8_t* scratch;     // [B][scratch_stride] road-generation scratch
+  size_t scratch_stride;
+  int32_t* queue;       // [B] boards whose staged layout was consumed (refill queue)
+  uint32_t* qcount;     // queue length
+  uint8_t* reset_fail;  // [B] reset kernel: road generation failed (board left unchanged)
+  int stage_next;       // reset kernel: queue reset boards for a staged next layout
   const TdDevCfg* cfg;
   const int64_t* def_act;
   const int64_t* atk_act;
@@ -38,5 +44,10 @@ struct StepArgs {
 hipError_t launch_step(const StepArgs& a, hipStream_t s, bool reset);
 hipError_t launch_stage_layouts(uint32_t* nxt, const uint32_t* recs, const int32_t* boards, int n, int words,
                                 hipStream_t s);
+// Generate staged layouts for the queued boards (one lane per board), then clear the queue.
+hipError_t launch_refill(const StepArgs& a, hipStream_t s);
+
+constexpr int kRoadAttempts = 1000;  // bound of each create_road_v2 retry loop (reference: unbounded)
+constexpr int kLayoutRetries = 64;   // auto-reset: failing draws skipped before giving up
 
 }  // namespace td

@@ -76,6 +76,7 @@ struct MtRef {
   // ---- CPython random ----
   TD_HD uint32_t getrandbits(int k) { return next() >> (32 - k); }
   TD_HD int64_t randbelow(int64_t n) {  // n >= 1, n < 2**32
+    if (n <= 0) return 0;
     int k = 0;
     for (uint64_t v = (uint64_t)n; v; v >>= 1) ++k;
     uint32_t r = getrandbits(k);
@@ -89,6 +90,7 @@ struct MtRef {
   }
   // ---- numpy legacy RandomState ----
   TD_HD int64_t np_randint(int64_t lo, int64_t hi) {  // requires hi > lo
+    if (hi <= lo) return lo;  // numpy raises here; callers check first
     uint64_t rng = (uint64_t)(hi - lo - 1);
     if (rng == 0) return lo;
     uint64_t mask = rng;

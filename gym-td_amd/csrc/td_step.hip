@@ -105,6 +105,7 @@ struct WaveMt {
     return mt_temper(y);
   }
   __device__ int64_t randbelow(int64_t n) {
+    if (n <= 0) return 0;  // never reached on a valid board (guards against an unbounded loop)
     int k = 64 - __builtin_clzll((unsigned long long)n);
     uint32_t r = next() >> (32 - k);
     while ((int64_t)r >= n) r = next() >> (32 - k);
@@ -764,6 +765,20 @@ __device__ void opponent_tower(Smem<NC>& S, U& u, const Ctx& x, WaveMt& R, int d
   build_near_road(S, u, x, R, t, false);
 }
 
+// One lane: the next episode layout of board b from its numpy stream into its
+// staged slot (TDGymBasic.reset :42-51); failing draws are skipped up to ``retries``.
+__device__ __attribute__((noinline)) int draw_layout(const StepArgs& a, int b, int retries) {
+  uint32_t* w = a.np_mt + (size_t)b * (MT_N + 1);
+  uint32_t* rec = a.nxt + (size_t)b * (LAYOUT_HDR + a.L * a.L);
+  void* scr = a.scratch + (size_t)b * a.scratch_stride;
+  int st = ROAD_ERR_BOUND;
+  for (int t = 0; t <= retries; ++t) {
+    st = episode_layout(w, a.L, scr, kRoadAttempts, rec);
+    if (st == ROAD_OK) break;
+  }
+  return st;
+}
+
 // ---------------------------------------------------------------------------
 // kernels
 // ---------------------------------------------------------------------------
@@ -773,6 +788,19 @@ __device__ void step_board(Smem<NC>& S, const StepArgs& a, int b, int L) {
   const TdDevCfg& C = x.C;
   U u;
   load_board(S, u, x, a, b);
+  if (u.num_roads < 1 || u.num_roads > 3) {
+    // never reset (its road generation failed): nothing to step
+    const int nf = NCH * x.NCr;
+    float* o = a.obs + (size_t)b * nf;
+    for (int i = x.lane; i < nf; i += 64) o[i] = 0.0f;
+    if (x.lane == 0) {
+      a.hdr[b].flags = u.flags | FLAG_NO_LAYOUT;
+      a.reward[b] = 0.0;
+      a.done[b] = 1;
+      if (a.win) a.win[b] = -1;
+    }
+    return;
+  }
   WaveMt R{a.opp_mt + (size_t)b * (MT_N + 1), a.opp_mt[(size_t)b * (MT_N + 1) + MT_N], x.lane};
 
   u.atk_cd = u.atk_cd - 1 > 0 ? u.atk_cd - 1 : 0;
@@ -857,12 +885,19 @@ __device__ void step_board(Smem<NC>& S, const StepArgs& a, int b, int L) {
   if (done) u.episodes += 1;
   bool was_reset = false;
   if (done && a.autoreset) {
-    const uint32_t* rec = a.nxt + (size_t)b * (LAYOUT_HDR + x.NCr);
+    uint32_t* rec = a.nxt + (size_t)b * (LAYOUT_HDR + x.NCr);
+    if (rec[0] != TD_LAYOUT_MAGIC) {
+      // nothing staged yet: draw the layout now (skipping failing draws)
+      int st = 0;
+      if (x.lane == 0) st = draw_layout(a, b, kLayoutRetries);
+      __threadfence_block();
+      st = __shfl(st, 0);
+      __syncthreads();
+      if (st != ROAD_OK) u.flags |= FLAG_NO_LAYOUT;
+    }
     if (rec[0] == TD_LAYOUT_MAGIC) {
       reset_board(S, u, x, rec);
       was_reset = true;
-    } else {
-      u.flags |= FLAG_NO_LAYOUT;
     }
   }
   if (!was_reset) enemy_stats(S, u, x);
@@ -876,8 +911,8 @@ __device__ void step_board(Smem<NC>& S, const StepArgs& a, int b, int L) {
 
   if (x.lane == 0) {
     if (was_reset) {
-      a.nxt[(size_t)b * (LAYOUT_HDR + x.NCr)] = 0u;  // staged layout consumed
-      a.consumed[b] += 1u;
+      a.nxt[(size_t)b * (LAYOUT_HDR + x.NCr)] = 0u;  // staged layout consumed: queue a refill
+      a.queue[atomicAdd(a.qcount, 1u)] = b;
     }
     a.opp_mt[(size_t)b * (MT_N + 1) + MT_N] = R.pos;
     a.reward[b] = reward;
@@ -908,7 +943,9 @@ __global__ __launch_bounds__(64) void td_step_kernel(StepArgs a) {
   step_board<NC>(S, a, b, LT ? LT : a.L);
 }
 
-// Reset selected boards from their staged layout and write the initial obs.
+// TDGymBasic.reset for the boards in reset_mask: the staged layout when there is
+// one, else a draw from the board's numpy stream now (no retry: a failing draw is
+// reported in reset_fail and the board is left unchanged, as the reference raises).
 template <int LT>
 __global__ __launch_bounds__(64) void td_reset_kernel(StepArgs a) {
   constexpr int NC = LT ? LT * LT : MAX_L * MAX_L / 4;
@@ -921,10 +958,17 @@ __global__ __launch_bounds__(64) void td_reset_kernel(StepArgs a) {
   U u;
   u.episodes = a.hdr[b].episodes;
   u.flags = 0;
-  const uint32_t* rec = a.nxt + (size_t)b * (LAYOUT_HDR + x.NCr);
+  uint32_t* rec = a.nxt + (size_t)b * (LAYOUT_HDR + x.NCr);
   if (rec[0] != TD_LAYOUT_MAGIC) {
-    if (x.lane == 0) a.hdr[b].flags |= FLAG_NO_LAYOUT;
-    return;
+    int st = 0;
+    if (x.lane == 0) st = draw_layout(a, b, 0);
+    __threadfence_block();
+    st = __shfl(st, 0);
+    __syncthreads();
+    if (st != ROAD_OK) {
+      if (x.lane == 0) a.reset_fail[b] = (uint8_t)st;
+      return;
+    }
   }
   reset_board(S, u, x, rec);
   for (int i = x.lane; i < 4 * NC; i += 64) (&S.grp[0][0])[i] = 0xFF;
@@ -933,8 +977,19 @@ __global__ __launch_bounds__(64) void td_reset_kernel(StepArgs a) {
   if (a.obs) write_obs(S, x, a.obs + (size_t)b * NCH * x.NCr);
   store_board(S, u, x, a, b);
   if (x.lane == 0) {
-    a.nxt[(size_t)b * (LAYOUT_HDR + x.NCr)] = 0u;
-    a.consumed[b] += 1u;
+    a.reset_fail[b] = 0;
+    rec[0] = 0u;
+    if (a.stage_next) a.queue[atomicAdd(a.qcount, 1u)] = b;
+  }
+}
+
+// Stage the next-episode layout of every queued board: one lane per board runs
+// create_road_v2 on the board's numpy stream (serial, latency-bound, rare).
+__global__ __launch_bounds__(64) void td_refill_kernel(StepArgs a) {
+  const uint32_t n = *a.qcount;
+  for (uint32_t i = blockIdx.x * 64u + threadIdx.x; i < n; i += gridDim.x * 64u) {
+    const int b = a.queue[i];
+    draw_layout(a, b, kLayoutRetries);
   }
 }
 
@@ -962,6 +1017,13 @@ hipError_t launch_step(const StepArgs& a, hipStream_t s, bool reset) {
     case 30: return launch2<30>(a, s, reset);
     default: return launch2<0>(a, s, reset);
   }
+}
+
+hipError_t launch_refill(const StepArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(td_refill_kernel, dim3(64), dim3(64), 0, s, a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  return hipMemsetAsync(a.qcount, 0, sizeof(uint32_t), s);
 }
 
 hipError_t launch_stage_layouts(uint32_t* nxt, const uint32_t* recs, const int32_t* boards, int n, int words,

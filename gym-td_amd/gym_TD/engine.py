@@ -160,6 +160,22 @@ class TDEngine(object):
             failed = ids.tolist()
         return self.obs, failed
 
+    def reset_all(self, max_retries=64):
+        """reset() every board, redrawing (from the same streams) the layouts whose
+        road generation failed -- the reference would raise or hang on those draws
+        (TDRoadGen.py:177-189).  Returns (obs, number of failed draws skipped)."""
+        obs, failed = self.reset()
+        skipped = 0
+        while failed and max_retries > 0:
+            skipped += len(failed)
+            m = np.zeros(self.B, dtype=np.uint8)
+            m[failed] = 1
+            obs, failed = self.reset(m)
+            max_retries -= 1
+        if failed:
+            raise RuntimeError("road generation kept failing for boards %r" % failed[:8])
+        return obs, skipped
+
     def reset_layouts(self, recs, boards):
         recs = _u32(recs).reshape(-1, self.lw)
         ids = np.ascontiguousarray(boards, dtype=np.int32)

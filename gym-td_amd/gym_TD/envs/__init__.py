@@ -292,16 +292,8 @@ class TDVecEnv(object):
         self.roadgen_failures = 0
 
     def reset(self, max_retries=64):
-        obs, failed = self.engine.reset()
-        tries = 0
-        while failed and tries < max_retries:  # the reference would raise / hang; redraw from the same stream
-            self.roadgen_failures += len(failed)
-            mask = np.zeros(self.num_envs, dtype=np.uint8)
-            mask[failed] = 1
-            obs, failed = self.engine.reset(mask)
-            tries += 1
-        if failed:
-            raise RuntimeError("road generation kept failing for boards %r" % failed[:8])
+        obs, skipped = self.engine.reset_all(max_retries)  # failing draws: the reference raises / hangs
+        self.roadgen_failures += skipped
         return obs
 
     def step(self, actions):

@@ -193,6 +193,8 @@ def test_full_size_properties(L, B, mode, multi):
         good[failed] = False
         picks = [b for b in np.random.RandomState(1).choice(B, 24, replace=False) if good[b]][:12]
         orc = _oracle_envs(L, [int(seeds[b]) for b in picks], mode, multi)
+        # boards whose first draw failed (the reference raises) stay unstepped: flagged, zero obs
+        assert len(failed) < B // 10
         g = torch.Generator(device="cuda").manual_seed(5)
         for k in range(40):
             if multi:
@@ -204,6 +206,8 @@ def test_full_size_properties(L, B, mode, multi):
             ob = eng.obs
             assert float(ob.min()) >= 0.0 and float(ob.max()) <= 1.0
             assert torch.equal(ob[:, 0], (ob[:, 1:4].sum(1) > 0).float())
+            if failed:
+                assert float(ob[failed].abs().max()) == 0.0
             dh = d[picks].cpu().numpy()
             ah = a[picks].cpu().numpy() if a is not None else [None] * len(picks)
             obh = ob[picks].cpu().numpy()
@@ -214,5 +218,6 @@ def test_full_size_properties(L, B, mode, multi):
                 assert np.array_equal(obh[j], wo)
         fl = eng.flags()
         assert (fl[good] == 0).all()
+        assert (fl[~good] == 8).all()  # TD_FLAG_NO_LAYOUT
     finally:
         eng.close()
