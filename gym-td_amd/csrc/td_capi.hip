@@ -60,6 +60,7 @@ struct td_handle {
   int32_t *d_queue = nullptr, *d_stage_ids = nullptr;
   uint8_t *d_scratch = nullptr, *d_mask = nullptr, *d_fail = nullptr;
   int stage_cap = 0;
+  uint64_t* d_stamps = nullptr;  // TD_STAMPS diagnostic builds only (not owned)
   long long steps = 0;
   std::vector<int32_t> last_reset_failed;
 };
@@ -398,6 +399,7 @@ int td_step(td_handle* h, const td_step_io* io, void* stream) {
   a.def_act = io->def_act; a.atk_act = io->atk_act; a.obs = io->obs; a.reward = io->reward; a.done = io->done;
   a.real_def = io->real_def; a.real_atk = io->real_atk; a.fail_def = io->fail_def; a.fail_atk = io->fail_atk;
   a.win = io->win; a.allow_next = io->allow_next; a.ep_return = io->ep_return; a.ep_len = io->ep_len;
+  a.stamps = h->d_stamps;
   HIP_OK(launch_step(a, s, false));
   h->steps += 1;
   if (h->autoreset && (h->steps % kRefillEvery) == 0) HIP_OK(launch_refill(a, s));
@@ -455,6 +457,15 @@ int td_get_flags(td_handle* h, int32_t* host_flags) {
   for (int b = 0; b < h->B; ++b) host_flags[b] = hdr[(size_t)b].flags;
   return 0;
 }
+
+#ifdef TD_STAMPS
+// Diagnostic builds: per-board phase timestamps ([B][16] uint64, device memory).
+int td_debug_stamps(td_handle* h, uint64_t* dev) {
+  if (!h) return fail("NULL handle");
+  h->d_stamps = dev;
+  return 0;
+}
+#endif
 
 void td_py_seed(uint32_t* mt, uint32_t seed) { py_seed(mt, seed); }
 void td_np_seed(uint32_t* mt, uint32_t seed) { np_seed(mt, seed); }

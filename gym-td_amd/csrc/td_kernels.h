@@ -24,6 +24,7 @@ struct StepArgs {
   uint32_t* qcount;     // queue length
   uint8_t* reset_fail;  // [B] reset kernel: road generation failed (board left unchanged)
   int stage_next;       // reset kernel: queue reset boards for a staged next layout
+  uint64_t* stamps;     // TD_STAMPS diagnostic builds only: [B][16] s_memtime per phase
   const TdDevCfg* cfg;
   const int64_t* def_act;
   const int64_t* atk_act;

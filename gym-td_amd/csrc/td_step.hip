@@ -24,6 +24,12 @@
 
 namespace td {
 
+#ifdef TD_STAMPS
+#define STAMP(i) do { if (a.stamps && x.lane == 0) a.stamps[(size_t)b * 16 + (i)] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define STAMP(i) do { } while (0)
+#endif
+
 enum : int { FC_OK = 0, FC_COST = 1, FC_POS = 2, FC_LVMAX = 3, FC_TARGET = 4, FC_CAP = 6 };  // utils/fail_code.py
 
 // ---------------------------------------------------------------------------
@@ -61,13 +67,17 @@ struct Smem {
   uint32_t tInf[TCAP];
   float chv[48];          // broadcast channel values
   float d9[256];          // channel 9 by distance
+  int32_t atk[24];        // attacker clusters of this step (TD-atk / TD-2p)
+  int32_t real_atk[24];   // info['RealAction'] of the attacker
+  int32_t fail_atk[4];    // info['FailCode'] of the attacker (-1 = no entry)
 };
 
 // Wave-uniform scalar board state (identical in every lane).
 struct U {
   double cost_def, cost_atk, ep_ret, progress;
   int steps, base_LP, atk_cd, def_cd, n, nt, num_roads, end_cell, maxdist, flags, episodes;
-  int start[3];
+  int start0, start1, start2;
+  __device__ __forceinline__ int start(int road) const { return road == 0 ? start0 : (road == 1 ? start1 : start2); }
 };
 
 struct Ctx {
@@ -78,41 +88,43 @@ struct Ctx {
 // ---------------------------------------------------------------------------
 // CPython MT19937 for the built-in opponent, state in HBM, wave-parallel twist
 // ---------------------------------------------------------------------------
+// Rewrites the 624 words in chunks of 64 in index order: w[i+1] and w[i+397]
+// (i < 227) are still old, w[i-227] (i >= 227) was rewritten by an earlier
+// chunk -- the sequential result.  Once every 624 draws.
+__device__ __attribute__((noinline)) void wave_mt_twist(uint32_t* w, int lane) {
+  for (int base = 0; base < MT_N; base += 64) {
+    int i = base + lane;
+    uint32_t nv = 0;
+    if (i < MT_N) {
+      uint32_t y = (w[i] & 0x80000000u) | (w[(i + 1) % MT_N] & 0x7fffffffu);
+      nv = w[(i + MT_M) % MT_N] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+    }
+    __syncthreads();
+    if (i < MT_N) w[i] = nv;
+    __threadfence_block();
+    __syncthreads();
+  }
+}
+
 struct WaveMt {
   uint32_t* w;
   uint32_t pos;
   int lane;
-  __device__ void twist() {
-    // chunks of 64 in index order: w[i+1] and w[i+397] (i < 227) are still old,
-    // w[i-227] (i >= 227) was rewritten by an earlier chunk -- the sequential result.
-    for (int base = 0; base < MT_N; base += 64) {
-      int i = base + lane;
-      uint32_t nv = 0;
-      if (i < MT_N) {
-        uint32_t y = (w[i] & 0x80000000u) | (w[(i + 1) % MT_N] & 0x7fffffffu);
-        nv = w[(i + MT_M) % MT_N] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
-      }
-      __syncthreads();
-      if (i < MT_N) w[i] = nv;
-      __threadfence_block();
-      __syncthreads();
-    }
-  }
-  __device__ uint32_t next() {
-    if (pos >= (uint32_t)MT_N) { twist(); pos = 0; }
+  __device__ __forceinline__ uint32_t next() {
+    if (pos >= (uint32_t)MT_N) { wave_mt_twist(w, lane); pos = 0; }
     uint32_t y = w[pos];
     ++pos;
     return mt_temper(y);
   }
-  __device__ int64_t randbelow(int64_t n) {
+  __device__ __forceinline__ int64_t randbelow(int64_t n) {
     if (n <= 0) return 0;  // never reached on a valid board (guards against an unbounded loop)
     int k = 64 - __builtin_clzll((unsigned long long)n);
     uint32_t r = next() >> (32 - k);
     while ((int64_t)r >= n) r = next() >> (32 - k);
     return r;
   }
-  __device__ int64_t randint(int64_t a, int64_t b) { return a + randbelow(b - a + 1); }
-  __device__ double random() {
+  __device__ __forceinline__ int64_t randint(int64_t a, int64_t b) { return a + randbelow(b - a + 1); }
+  __device__ __forceinline__ double random() {
     uint32_t x = next() >> 5, y = next() >> 6;
     return (x * 67108864.0 + y) * (1.0 / 9007199254740992.0);
   }
@@ -279,29 +291,40 @@ __device__ void defender_scan(Smem<NC>& S, U& u, const Ctx& x, const int64_t* A,
 // ---------------------------------------------------------------------------
 // attacker: summon_cluster (TDBoard.py:199-224)
 // ---------------------------------------------------------------------------
+// Cluster types / real actions are packed 4 bits per slot (slot k at bits 4k..4k+3).
 template <int NC>
-__device__ int summon_cluster(Smem<NC>& S, U& u, const Ctx& x, const int* types, int road, int* real) {
+__device__ int summon_cluster(Smem<NC>& S, U& u, const Ctx& x, uint32_t types, int road, uint32_t* real) {
   const TdDevCfg& C = x.C;
   const int lv = u.progress >= C.enemy_upgrade_at ? 1 : 0;  // :201
-  const int st = u.start[road];
+  const int st = u.start(road);
   bool tried = false, summoned = false;
+  uint32_t rp = 0;
+#pragma unroll
   for (int k = 0; k < 8; ++k) {
-    int t = types[k];
-    if (t == 4) { real[k] = 4; continue; }                  // :207-209
-    tried = true;
-    double cost = C.e_cost[t][lv];
-    if (u.cost_atk < cost) { real[k] = 4; continue; }       // :212-213
-    if (u.n >= ECAP) { u.flags |= FLAG_EN_OVERFLOW; real[k] = 4; continue; }
-    u.cost_atk = dsub(u.cost_atk, cost);                    // :215
-    if (x.lane == 0) {
-      S.eLP[u.n] = C.e_lp[t][lv];
-      S.eMg[u.n] = 0.0;
-      S.eInf[u.n] = en_pack(st, t, lv, 0);
+    const int t = (int)((types >> (4 * k)) & 0xfu);
+    int r = t;
+    if (t != 4) {                                           // :207-209
+      tried = true;
+      const double cost = C.e_cost[t][lv];
+      if (u.cost_atk < cost) {                              // :212-213
+        r = 4;
+      } else if (u.n >= ECAP) {
+        u.flags |= FLAG_EN_OVERFLOW;
+        r = 4;
+      } else {
+        u.cost_atk = dsub(u.cost_atk, cost);                // :215
+        if (x.lane == 0) {
+          S.eLP[u.n] = C.e_lp[t][lv];
+          S.eMg[u.n] = 0.0;
+          S.eInf[u.n] = en_pack(st, t, lv, 0);
+        }
+        u.n += 1;
+        summoned = true;
+      }
     }
-    u.n += 1;
-    summoned = true;
-    real[k] = t;
+    rp |= (uint32_t)r << (4 * k);
   }
+  if (real) *real = rp;
   return (tried && !summoned) ? FC_COST : FC_OK;            // :219-224
 }
 
@@ -326,7 +349,7 @@ __device__ __forceinline__ double damage(double LP, double atk, double def, bool
 }
 
 template <int NC>
-__device__ double board_step(Smem<NC>& S, U& u, const Ctx& x) {
+__device__ double board_step(Smem<NC>& S, U& u, const Ctx& x, const StepArgs& a, int b) {
   const TdDevCfg& C = x.C;
   const int L = x.L, lane = x.lane;
   double reward = dadd(0.0, C.reward_time);                 // :298-299
@@ -372,6 +395,7 @@ __device__ double board_step(Smem<NC>& S, U& u, const Ctx& x) {
     inf[s] = val[s] ? S.eInf[i] : 0u;
   }
 
+  STAMP(3);
   // --- towers fire in list order (:306-313); dead enemies stay targetable
   for (int k = 0; k < u.nt; ++k) {
     double cd = dsub(S.tCd[k], 1.0);                        // :307
@@ -388,9 +412,8 @@ __device__ double board_step(Smem<NC>& S, U& u, const Ctx& x) {
         const double atk = C.t_atk[tt][tl];
         if (tt <= 1) {  // TowerArrow / TowerMagic (TDElements.py:71-93)
           if (lane == (tgt & 63)) {
-            const int s = tgt >> 6;
-            const uint32_t e = inf[s];
-            lp[s] = damage(lp[s], atk, C.e_def[en_type(e)][en_lv(e)], tt == 1);
+            if (tgt < 64) lp[0] = damage(lp[0], atk, C.e_def[en_type(inf[0])][en_lv(inf[0])], tt == 1);
+            else lp[1] = damage(lp[1], atk, C.e_def[en_type(inf[1])][en_lv(inf[1])], tt == 1);
           }
         } else {
           const uint32_t tinf = (tgt >> 6) ? __shfl(inf[1], tgt & 63) : __shfl(inf[0], tgt & 63);
@@ -408,9 +431,9 @@ __device__ double board_step(Smem<NC>& S, U& u, const Ctx& x) {
             if (q0 | q1) {
               const int f = q0 ? ctz64(q0) : 64 + ctz64(q1);
               if (lane == (f & 63)) {
-                const int s = f >> 6;
-                lp[s] = damage(lp[s], atk, 0.0, true);
-                inf[s] = (inf[s] & 0xffffu) | ((uint32_t)C.frozen_time << 16);
+                const uint32_t slow = (uint32_t)C.frozen_time << 16;
+                if (f < 64) { lp[0] = damage(lp[0], atk, 0.0, true); inf[0] = (inf[0] & 0xffffu) | slow; }
+                else { lp[1] = damage(lp[1], atk, 0.0, true); inf[1] = (inf[1] & 0xffffu) | slow; }
               }
             }
           }
@@ -421,6 +444,7 @@ __device__ double board_step(Smem<NC>& S, U& u, const Ctx& x) {
     if (lane == 0) S.tCd[k] = cd;
   }
 
+  STAMP(4);
   // --- kills (:313-317): every enemy at LP 0 was hit this step
   bool dead0 = val[0] && lp[0] == 0.0, dead1 = val[1] && lp[1] == 0.0;
   const int nk = popc64(ballot(dead0)) + popc64(ballot(dead1));
@@ -429,7 +453,6 @@ __device__ double board_step(Smem<NC>& S, U& u, const Ctx& x) {
   // --- march (:319-344)
   bool alive[2] = {val[0] && !dead0, val[1] && !dead1};
   bool leak[2] = {false, false};
-  const int DR[4] = {0, 0, 1, -1}, DC[4] = {1, -1, 0, 0};
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
     if (!alive[s]) continue;
@@ -442,7 +465,8 @@ __device__ double board_step(Smem<NC>& S, U& u, const Ctx& x) {
     while (mg[s] >= 1.0) {
       mg[s] = dsub(mg[s], 1.0);
       const int d = cw_dir(S.cell[cell]);
-      int r = cell / L + DR[d], c = cell % L + DC[d];
+      // map[5] codes (TDBoard.py:319): 0:+c 1:-c 2:+r 3:-r
+      int r = cell / L + (d == 2) - (d == 3), c = cell % L + (d == 0) - (d == 1);
       if (r < 0 || r >= L || c < 0 || c >= L) { u.flags |= FLAG_BAD_MOVE; break; }
       cell = r * L + c;
       if (cell == u.end_cell) { leak[s] = true; break; }
@@ -607,7 +631,7 @@ __device__ void load_board(Smem<NC>& S, U& u, const Ctx& x, const StepArgs& a, i
   u.cost_def = h.cost_def; u.cost_atk = h.cost_atk; u.ep_ret = h.ep_return;
   u.steps = h.steps; u.base_LP = h.base_LP; u.atk_cd = h.atk_cd; u.def_cd = h.def_cd;
   u.n = h.n_en; u.nt = h.n_tw; u.num_roads = h.num_roads; u.end_cell = h.end_cell;
-  u.start[0] = h.start_cell[0]; u.start[1] = h.start_cell[1]; u.start[2] = h.start_cell[2];
+  u.start0 = h.start_cell[0]; u.start1 = h.start_cell[1]; u.start2 = h.start_cell[2];
   u.maxdist = h.maxdist; u.flags = h.flags; u.episodes = h.episodes;
   u.progress = ddiv((double)u.steps, (double)x.C.max_episode_steps);
   const size_t eb = (size_t)b * ECAP, tb = (size_t)b * TCAP, cb = (size_t)b * x.NCr;
@@ -628,7 +652,7 @@ __device__ void reset_board(Smem<NC>& S, U& u, const Ctx& x, const uint32_t* rec
   const TdDevCfg& C = x.C;
   for (int i = x.lane; i < x.NCr; i += 64) { S.cell[i] = rec[LAYOUT_HDR + i]; S.twr[i] = 0; }
   u.num_roads = (int)rec[1]; u.end_cell = (int)rec[2]; u.maxdist = (int)rec[3];
-  u.start[0] = (int)rec[4]; u.start[1] = (int)rec[5]; u.start[2] = (int)rec[6];
+  u.start0 = (int)rec[4]; u.start1 = (int)rec[5]; u.start2 = (int)rec[6];
   u.cost_def = C.def_init_cost; u.cost_atk = C.atk_init_cost;
   u.base_LP = C.base_LP; u.steps = 0; u.progress = 0.0;
   u.atk_cd = 0; u.def_cd = 0; u.n = 0; u.nt = 0; u.ep_ret = 0.0;
@@ -642,7 +666,7 @@ __device__ void store_board(const Smem<NC>& S, const U& u, const Ctx& x, const S
     h.cost_def = u.cost_def; h.cost_atk = u.cost_atk; h.ep_return = u.ep_ret;
     h.steps = u.steps; h.base_LP = u.base_LP; h.atk_cd = u.atk_cd; h.def_cd = u.def_cd;
     h.n_en = u.n; h.n_tw = u.nt; h.num_roads = u.num_roads; h.end_cell = u.end_cell;
-    h.start_cell[0] = u.start[0]; h.start_cell[1] = u.start[1]; h.start_cell[2] = u.start[2];
+    h.start_cell[0] = u.start0; h.start_cell[1] = u.start1; h.start_cell[2] = u.start2;
     h.maxdist = u.maxdist; h.flags = u.flags; h.episodes = u.episodes;
     h.pad[0] = h.pad[1] = h.pad[2] = h.pad[3] = 0;
     a.hdr[b] = h;
@@ -660,17 +684,17 @@ template <int NC>
 __device__ void opponent_enemy(Smem<NC>& S, U& u, const Ctx& x, WaveMt& R, int difficulty) {
   // random_enemy_lv0 / lv1 with random_agent=True (TDGymBasic.py:81-108)
   if (u.atk_cd != 0) return;
-  int types[8], real[8];
+  uint32_t types = 0;
   int road;
   if (difficulty == 0) {
-    for (int k = 0; k < 8; ++k) types[k] = (int)R.randint(0, 4);
+    for (int k = 0; k < 8; ++k) types |= (uint32_t)R.randint(0, 4) << (4 * k);
     road = (int)R.randint(0, u.num_roads - 1);
   } else {
-    int t = (int)R.randint(0, 3);
+    const uint32_t t = (uint32_t)R.randint(0, 3);
     road = (int)R.randint(0, u.num_roads - 1);
-    for (int k = 0; k < 8; ++k) types[k] = t;
+    types = t * 0x11111111u;
   }
-  summon_cluster(S, u, x, types, road, real);
+  summon_cluster(S, u, x, types, road, nullptr);
   __syncthreads();
   u.atk_cd = x.C.atk_interval;  // the (ok, real) tuple is always truthy
 }
@@ -782,12 +806,58 @@ __device__ __attribute__((noinline)) int draw_layout(const StepArgs& a, int b, i
 // ---------------------------------------------------------------------------
 // kernels
 // ---------------------------------------------------------------------------
-template <int NC>
+// Attacker clusters of TD-atk (TDAttack.py:36-46) and TD-2p (TDMulti.py:199-206, 229-241).
+template <int NC, int MODE>
+__device__ void attacker_actions(Smem<NC>& S, U& u, const Ctx& x, const StepArgs& a, int b) {
+  const TdDevCfg& C = x.C;
+  if (x.lane < 24) {
+    int64_t v = a.atk_act[(size_t)b * 24 + x.lane];
+    const bool bad = v < 0 || v > 4;
+    S.atk[x.lane] = bad ? 4 : (int)v;
+    S.real_atk[x.lane] = bad ? 4 : (int)v;
+  }
+  if (x.lane < 4) S.fail_atk[x.lane] = -1;
+  {
+    bool bad = false;
+    if (x.lane < 24) { int64_t v = a.atk_act[(size_t)b * 24 + x.lane]; bad = v < 0 || v > 4; }
+    if (ballot(bad)) u.flags |= FLAG_BAD_ACTION;
+  }
+  __syncthreads();
+  if (u.atk_cd != 0) return;
+  for (int i = 0; i < u.num_roads; ++i) {
+    uint32_t cl = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) cl |= (uint32_t)S.atk[8 * i + k] << (4 * k);
+    const bool all4 = cl == 0x44444444u;
+    uint32_t real = cl;
+    if (MODE == MODE_2P && a.multi) {  // TDMulti multi: every road, always truthy (:201-206)
+      summon_cluster(S, u, x, cl, i, &real);
+      u.atk_cd = C.atk_interval;
+    } else if (all4) {
+      if (x.lane == 0) S.fail_atk[i] = 0;               // TDAttack.py:40-42, TDMulti.py:234-236
+    } else {
+      const int fc = summon_cluster(S, u, x, cl, i, &real);
+      if (MODE == MODE_ATK) {
+        if (fc == FC_OK) u.atk_cd = C.atk_interval;     // res is a real bool here (TDAttack.py:43-44)
+        if (x.lane < 8) S.real_atk[8 * i + x.lane] = (int)((real >> (4 * x.lane)) & 0xfu);
+      } else {
+        u.atk_cd = C.atk_interval;                      // tuple truthiness (TDMulti.py:237-238)
+      }
+      if (x.lane == 0) S.fail_atk[i] = fc;
+    }
+    __syncthreads();
+  }
+}
+
+
+template <int NC, int MODE>
 __device__ void step_board(Smem<NC>& S, const StepArgs& a, int b, int L) {
   const Ctx x{*a.cfg, L, L * L, (int)threadIdx.x};
   const TdDevCfg& C = x.C;
   U u;
+  STAMP(0);
   load_board(S, u, x, a, b);
+  STAMP(1);
   if (u.num_roads < 1 || u.num_roads > 3) {
     // never reset (its road generation failed): nothing to step
     const int nf = NCH * x.NCr;
@@ -808,11 +878,9 @@ __device__ void step_board(Smem<NC>& S, const StepArgs& a, int b, int L) {
   const int64_t empty_def = (int64_t)6 * x.NCr;
   int fail_def = 0;
   int64_t real_def = empty_def;
-  int fail_atk[3] = {-1, -1, -1};
-  int real_atk[24];
 
   // ---- defender
-  if (a.mode != MODE_ATK) {
+  if (MODE != MODE_ATK) {
     if (a.multi) {
       defender_scan(S, u, x, a.def_act + (size_t)b * 6 * x.NCr,
                     a.real_def ? a.real_def + (size_t)b * 6 * x.NCr : nullptr, u.def_cd == 0);
@@ -827,56 +895,24 @@ __device__ void step_board(Smem<NC>& S, const StepArgs& a, int b, int L) {
     }
   }
   // ---- attacker
-  if (a.mode == MODE_DEF) {
+  if (MODE == MODE_DEF) {
     opponent_enemy(S, u, x, R, a.difficulty);
   } else {
-    const int64_t* A = a.atk_act + (size_t)b * 24;
-    int acts[24];
-    bool bad = false;
-    for (int k = 0; k < 24; ++k) {
-      int64_t v = A[k];
-      if (v < 0 || v > 4) { bad = true; v = 4; }
-      acts[k] = (int)v;
-      real_atk[k] = (int)v;
-    }
-    if (bad) u.flags |= FLAG_BAD_ACTION;
-    if (u.atk_cd == 0) {
-      for (int i = 0; i < u.num_roads; ++i) {
-        const int* cl = acts + 8 * i;
-        bool all4 = true;
-        for (int k = 0; k < 8; ++k) all4 = all4 && cl[k] == 4;
-        if (a.mode == MODE_2P && a.multi) {  // TDMulti multi: every road, always truthy (:201-206)
-          summon_cluster(S, u, x, cl, i, real_atk + 8 * i);
-          for (int k = 0; k < 8; ++k) real_atk[8 * i + k] = cl[k];
-          u.atk_cd = C.atk_interval;
-        } else if (all4) {
-          fail_atk[i] = 0;                                  // TDAttack.py:40-42, TDMulti.py:234-236
-        } else {
-          int fc = summon_cluster(S, u, x, cl, i, real_atk + 8 * i);
-          if (a.mode == MODE_ATK) {
-            if (fc == FC_OK) u.atk_cd = C.atk_interval;     // res is a real bool here (TDAttack.py:43-44)
-          } else {
-            u.atk_cd = C.atk_interval;                      // tuple truthiness (TDMulti.py:237-238)
-            for (int k = 0; k < 8; ++k) real_atk[8 * i + k] = cl[k];
-          }
-          fail_atk[i] = fc;
-        }
-        __syncthreads();
-      }
-    }
-    if (a.mode == MODE_ATK) opponent_tower(S, u, x, R, a.difficulty);
+    attacker_actions<NC, MODE>(S, u, x, a, b);
+    if (MODE == MODE_ATK) opponent_tower(S, u, x, R, a.difficulty);
   }
   __syncthreads();
+  STAMP(2);
 
   // ---- TDBoard.step
-  double reward = board_step(S, u, x);
-  if (a.mode == MODE_ATK) reward = -reward;                 // TDAttack.py:50
+  double reward = board_step(S, u, x, a, b);
+  if (MODE == MODE_ATK) reward = -reward;                   // TDAttack.py:50
   const bool done = (u.base_LP <= 0) || (u.steps >= C.max_episode_steps);  // :384-385
   u.ep_ret = dadd(u.ep_ret, reward);
   const int ep_steps = u.steps;
   int8_t win = -1;
   if (done) {
-    if (a.mode == MODE_ATK) win = u.base_LP <= 0 ? 1 : 0;
+    if (MODE == MODE_ATK) win = u.base_LP <= 0 ? 1 : 0;
     else win = u.base_LP > 0 ? 1 : 0;
   }
   const uint8_t allow = (uint8_t)((u.atk_cd <= 1 ? 1 : 0) | (u.def_cd <= 1 ? 2 : 0));
@@ -885,28 +921,24 @@ __device__ void step_board(Smem<NC>& S, const StepArgs& a, int b, int L) {
   if (done) u.episodes += 1;
   bool was_reset = false;
   if (done && a.autoreset) {
-    uint32_t* rec = a.nxt + (size_t)b * (LAYOUT_HDR + x.NCr);
-    if (rec[0] != TD_LAYOUT_MAGIC) {
-      // nothing staged yet: draw the layout now (skipping failing draws)
-      int st = 0;
-      if (x.lane == 0) st = draw_layout(a, b, kLayoutRetries);
-      __threadfence_block();
-      st = __shfl(st, 0);
-      __syncthreads();
-      if (st != ROAD_OK) u.flags |= FLAG_NO_LAYOUT;
-    }
+    const uint32_t* rec = a.nxt + (size_t)b * (LAYOUT_HDR + x.NCr);
     if (rec[0] == TD_LAYOUT_MAGIC) {
       reset_board(S, u, x, rec);
       was_reset = true;
+    } else {
+      u.flags |= FLAG_NO_LAYOUT;  // refill fell behind: the board keeps stepping its finished episode
     }
   }
+  STAMP(5);
   if (!was_reset) enemy_stats(S, u, x);
   else {
     for (int i = x.lane; i < 4 * NC; i += 64) (&S.grp[0][0])[i] = 0xFF;
     __syncthreads();
   }
   channel_scalars(S, u, x);
+  STAMP(6);
   write_obs(S, x, a.obs + (size_t)b * NCH * x.NCr);
+  STAMP(7);
   store_board(S, u, x, a, b);
 
   if (x.lane == 0) {
@@ -924,23 +956,20 @@ __device__ void step_board(Smem<NC>& S, const StepArgs& a, int b, int L) {
     if (a.ep_return) a.ep_return[b] = ep_ret;
     if (a.ep_len) a.ep_len[b] = ep_steps;
   }
-  if (a.mode != MODE_DEF) {
-    if (a.fail_atk && x.lane < 3) a.fail_atk[(size_t)b * 3 + x.lane] = fail_atk[x.lane];
-    if (a.real_atk && x.lane < 24) {
-      int v = 0;
-      for (int k = 0; k < 24; ++k) if (k == x.lane) v = real_atk[k];
-      a.real_atk[(size_t)b * 24 + x.lane] = v;
-    }
+  if (MODE != MODE_DEF) {
+    if (a.fail_atk && x.lane < 3) a.fail_atk[(size_t)b * 3 + x.lane] = S.fail_atk[x.lane];
+    if (a.real_atk && x.lane < 24) a.real_atk[(size_t)b * 24 + x.lane] = S.real_atk[x.lane];
   }
+  STAMP(8);
 }
 
-template <int LT>
+template <int LT, int MODE>
 __global__ __launch_bounds__(64) void td_step_kernel(StepArgs a) {
   constexpr int NC = LT ? LT * LT : MAX_L * MAX_L / 4;
   __shared__ Smem<NC> S;
   const int b = blockIdx.x;
   if (b >= a.B) return;
-  step_board<NC>(S, a, b, LT ? LT : a.L);
+  step_board<NC, MODE>(S, a, b, LT ? LT : a.L);
 }
 
 // TDGymBasic.reset for the boards in reset_mask: the staged layout when there is
@@ -1006,7 +1035,9 @@ __global__ __launch_bounds__(64) void td_stage_layouts_kernel(uint32_t* nxt, con
 template <int LT>
 static hipError_t launch2(const StepArgs& a, hipStream_t s, bool reset) {
   if (reset) hipLaunchKernelGGL(td_reset_kernel<LT>, dim3(a.B), dim3(64), 0, s, a);
-  else hipLaunchKernelGGL(td_step_kernel<LT>, dim3(a.B), dim3(64), 0, s, a);
+  else if (a.mode == MODE_DEF) hipLaunchKernelGGL((td_step_kernel<LT, MODE_DEF>), dim3(a.B), dim3(64), 0, s, a);
+  else if (a.mode == MODE_ATK) hipLaunchKernelGGL((td_step_kernel<LT, MODE_ATK>), dim3(a.B), dim3(64), 0, s, a);
+  else hipLaunchKernelGGL((td_step_kernel<LT, MODE_2P>), dim3(a.B), dim3(64), 0, s, a);
   return hipGetLastError();
 }
 

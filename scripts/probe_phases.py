@@ -1,0 +1,47 @@
+"""Diagnostic: per-phase wave cycles of the step kernel (TD_STAMPS build) and
+timings, at a chosen batch.  Usage: TDSTEP_LIB=.../libtdstep_stamps.so python probe_phases.py B L burnin"""
+import os, sys, time
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "gym-td_amd"))
+import numpy as np, torch
+from gym_TD import _lib
+from gym_TD.engine import TDEngine
+
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
+L = int(sys.argv[2]) if len(sys.argv) > 2 else 10
+burn = int(sys.argv[3]) if len(sys.argv) > 3 else 600
+seeds = np.arange(B) + 11
+eng = TDEngine(L, B, "def", False, 1, np_seeds=seeds, py_seeds=seeds, autoreset=True)
+eng.reset_all()
+g = torch.Generator(device="cuda").manual_seed(0)
+acts = torch.randint(0, 6 * L * L + 1, (burn + 20, B), device="cuda", generator=g)
+for k in range(burn):
+    eng.step(def_act=acts[k])
+torch.cuda.synchronize()
+stamps = torch.zeros((B, 16), dtype=torch.int64, device="cuda")
+fn = getattr(_lib.lib, "td_debug_stamps", None)
+if fn is not None:
+    fn.restype = _lib.ctypes.c_int
+    fn.argtypes = [_lib.c_vp, _lib.c_vp]
+    fn(eng._h, stamps.data_ptr())
+names = ["load", "actions", "sort", "towers", "march+costs", "stats+scalars", "obs", "store+out"]
+acc = np.zeros(len(names))
+t0 = time.time()
+for k in range(burn, burn + 20):
+    eng.step(def_act=acts[k])
+    torch.cuda.synchronize()
+    if fn is not None:
+        s = stamps.cpu().numpy().astype(np.float64)
+        idx = [0, 1, 2, 3, 4, 5, 6, 7, 8]
+        d = np.diff(s[:, idx], axis=1)
+        acc += d.mean(axis=0)
+dt = (time.time() - t0) / 20
+print("B=%d L=%d step %.1f us" % (B, L, dt * 1e6))
+if fn is not None:
+    tot = acc.sum()
+    for n, v in zip(names, acc / 20):
+        print("  %-14s %10.0f cycles/wave  %5.1f%%" % (n, v, 100 * v / (tot / 20)))
+    s = stamps.cpu().numpy()
+    span = (s[:, 8].max() - s[:, 0].min())
+    print("  kernel span (first start -> last end) %.0f cycles; mean wave life %.0f cycles" % (span, (s[:, 8] - s[:, 0]).mean()))
+    st = eng.export_state(0, min(B, 4096))
+    print("  mean enemies %.2f towers %.2f steps %.0f" % (st["hdr"]["n_en"].mean(), st["hdr"]["n_tw"].mean(), st["hdr"]["steps"].mean()))
