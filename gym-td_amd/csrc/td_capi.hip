@@ -56,11 +56,18 @@ struct td_handle {
   TdHdr* d_hdr = nullptr;
   double *d_en_lp = nullptr, *d_en_mg = nullptr, *d_tw_cd = nullptr;
   uint32_t *d_en_inf = nullptr, *d_tw_inf = nullptr, *d_cells = nullptr, *d_opp = nullptr, *d_np = nullptr;
-  uint32_t *d_nxt = nullptr, *d_qcount = nullptr, *d_stage = nullptr;
+  uint32_t* d_hot = nullptr;  // opponent hot record [B][HOT_WORDS]
+  uint32_t *d_nxt = nullptr, *d_qcount = nullptr, *d_stage = nullptr;  // d_queue / d_qcount: 2 buffers
   int32_t *d_queue = nullptr, *d_stage_ids = nullptr;
   uint8_t *d_scratch = nullptr, *d_mask = nullptr, *d_fail = nullptr;
   int stage_cap = 0;
   uint64_t* d_stamps = nullptr;  // TD_STAMPS diagnostic builds only (not owned)
+  // Layout refill runs on a side stream: step kernels append to queue[cur]; a
+  // refill takes the current buffer and steps switch to the other one.
+  hipStream_t side = nullptr;
+  hipEvent_t ev_main = nullptr, ev_refill[2] = {nullptr, nullptr};
+  bool refill_pending[2] = {false, false};
+  int cur = 0;
   long long steps = 0;
   std::vector<int32_t> last_reset_failed;
 };
@@ -137,9 +144,10 @@ StepArgs base_args(td_handle* h) {
   a.B = h->B; a.L = h->L; a.mode = h->mode; a.multi = h->multi; a.difficulty = h->difficulty;
   a.autoreset = h->autoreset;
   a.hdr = h->d_hdr; a.en_lp = h->d_en_lp; a.en_mg = h->d_en_mg; a.en_inf = h->d_en_inf;
-  a.tw_cd = h->d_tw_cd; a.tw_inf = h->d_tw_inf; a.cells = h->d_cells; a.opp_mt = h->d_opp;
+  a.tw_cd = h->d_tw_cd; a.tw_inf = h->d_tw_inf; a.cells = h->d_cells; a.opp_mt = h->d_opp; a.opp_hot = h->d_hot;
   a.np_mt = h->d_np; a.nxt = h->d_nxt; a.scratch = h->d_scratch; a.scratch_stride = h->scratch_stride;
-  a.queue = h->d_queue; a.qcount = h->d_qcount; a.reset_fail = h->d_fail; a.cfg = h->d_cfg;
+  a.queue = h->d_queue + (size_t)h->cur * h->B; a.qcount = h->d_qcount + h->cur;
+  a.reset_fail = h->d_fail; a.cfg = h->d_cfg;
   return a;
 }
 
@@ -166,7 +174,27 @@ int drop_staged(td_handle* h, int b) {
 int drop_all_staged(td_handle* h) {
   HIP_OK(hipDeviceSynchronize());
   HIP_OK(hipMemset(h->d_nxt, 0, (size_t)h->B * h->lw * 4));
-  HIP_OK(hipMemset(h->d_qcount, 0, 4));
+  HIP_OK(hipMemset(h->d_qcount, 0, 8));
+  return 0;
+}
+
+// Hand the current refill queue to the side stream (after the work on `s` that
+// filled it) and switch the step kernels to the other buffer.
+int start_refill(td_handle* h, hipStream_t s) {
+  const int q = h->cur;
+  StepArgs a = base_args(h);
+  HIP_OK(hipEventRecord(h->ev_main, s));
+  HIP_OK(hipStreamWaitEvent(h->side, h->ev_main, 0));
+  HIP_OK(launch_refill(a, h->side));
+  HIP_OK(hipEventRecord(h->ev_refill[q], h->side));
+  h->refill_pending[q] = true;
+  h->cur ^= 1;
+  // the buffer steps now append to was handed out two refills ago: its refill
+  // (and the queue reset behind it) must be done before the next step reads it
+  if (h->refill_pending[h->cur]) {
+    HIP_OK(hipStreamWaitEvent(s, h->ev_refill[h->cur], 0));
+    h->refill_pending[h->cur] = false;
+  }
   return 0;
 }
 
@@ -178,8 +206,9 @@ int run_reset(td_handle* h, const std::vector<uint8_t>& mask, float* obs, hipStr
   a.reset_mask = h->d_mask;
   a.stage_next = h->autoreset;
   HIP_OK(launch_step(a, s, true));
-  if (h->autoreset) HIP_OK(launch_refill(a, s));
+  if (h->autoreset && start_refill(h, s)) return -1;
   HIP_OK(hipStreamSynchronize(s));
+  HIP_OK(hipStreamSynchronize(h->side));
   return 0;
 }
 
@@ -268,17 +297,22 @@ td_handle* td_create(const td_config* cfg, int map_size, int n_boards, int mode,
   rc |= dalloc(&h->d_tw_cd, B * TCAP);
   rc |= dalloc(&h->d_tw_inf, B * TCAP);
   rc |= dalloc(&h->d_cells, B * h->NC);
-  rc |= dalloc(&h->d_opp, B * (MT_N + 1));
-  rc |= dalloc(&h->d_np, B * (MT_N + 1));
+  rc |= dalloc(&h->d_opp, B * OPP_WORDS);
+  rc |= dalloc(&h->d_hot, B * HOT_WORDS);
+  rc |= dalloc(&h->d_np, B * OPP_WORDS);
   rc |= dalloc(&h->d_nxt, B * h->lw);
   rc |= dalloc(&h->d_scratch, B * h->scratch_stride);
-  rc |= dalloc(&h->d_queue, B);
-  rc |= dalloc(&h->d_qcount, 1);
+  rc |= dalloc(&h->d_queue, 2 * B);
+  rc |= dalloc(&h->d_qcount, 2);
   rc |= dalloc(&h->d_mask, B);
   rc |= dalloc(&h->d_fail, B);
   rc |= dalloc(&h->d_stage, (size_t)h->stage_cap * h->lw);
   rc |= dalloc(&h->d_stage_ids, (size_t)h->stage_cap);
   if (!rc && hipMemcpy(h->d_cfg, &h->dcfg, sizeof(TdDevCfg), hipMemcpyHostToDevice) != hipSuccess) rc = fail("cfg upload");
+  if (!rc && hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking) != hipSuccess) rc = fail("side stream");
+  if (!rc && hipEventCreateWithFlags(&h->ev_main, hipEventDisableTiming) != hipSuccess) rc = fail("event");
+  for (int q = 0; q < 2 && !rc; ++q)
+    if (hipEventCreateWithFlags(&h->ev_refill[q], hipEventDisableTiming) != hipSuccess) rc = fail("event");
   if (rc) { std::string e = g_err; td_destroy(h); g_err = e; return nullptr; }
   std::vector<uint32_t> seeds(B);
   for (size_t b = 0; b < B; ++b) seeds[b] = (uint32_t)b;
@@ -291,10 +325,14 @@ void td_destroy(td_handle* h) {
   (void)hipSetDevice(h->device);
   (void)hipDeviceSynchronize();
   void* dptrs[] = {h->d_cfg, h->d_hdr, h->d_en_lp, h->d_en_mg, h->d_en_inf, h->d_tw_cd, h->d_tw_inf,
-                   h->d_cells, h->d_opp, h->d_np, h->d_nxt, h->d_scratch, h->d_queue, h->d_qcount,
+                   h->d_cells, h->d_opp, h->d_hot, h->d_np, h->d_nxt, h->d_scratch, h->d_queue, h->d_qcount,
                    h->d_mask, h->d_fail, h->d_stage, h->d_stage_ids};
   for (void* p : dptrs)
     if (p) (void)hipFree(p);
+  if (h->ev_main) (void)hipEventDestroy(h->ev_main);
+  for (int q = 0; q < 2; ++q)
+    if (h->ev_refill[q]) (void)hipEventDestroy(h->ev_refill[q]);
+  if (h->side) (void)hipStreamDestroy(h->side);
   delete h;
 }
 
@@ -317,34 +355,76 @@ int td_seed(td_handle* h, const uint32_t* np_seeds, const uint32_t* py_seeds) {
   if (!h) return fail("NULL handle");
   const size_t B = (size_t)h->B, W = MT_N + 1;
   std::vector<uint32_t> st(B * W);
+  (void)st;
+  (void)W;
   if (np_seeds) {
-    parallel_for((int)B, [&](int b) { np_seed(&st[(size_t)b * W], np_seeds[b]); });
+    std::vector<uint32_t> nw(B * OPP_WORDS);
+    parallel_for((int)B, [&](int b) {
+      uint32_t* w = &nw[(size_t)b * OPP_WORDS];
+      np_seed(w, np_seeds[b]);
+      w[MT_N + 1] = MT_N;  // no lazy words
+    });
     if (drop_all_staged(h)) return -1;
-    HIP_OK(hipMemcpy(h->d_np, st.data(), B * W * 4, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(h->d_np, nw.data(), B * OPP_WORDS * 4, hipMemcpyHostToDevice));
   }
   if (py_seeds) {
-    parallel_for((int)B, [&](int b) { py_seed(&st[(size_t)b * W], py_seeds[b]); });
+    std::vector<uint32_t> op(B * OPP_WORDS);
+    parallel_for((int)B, [&](int b) {
+      uint32_t* w = &op[(size_t)b * OPP_WORDS];
+      py_seed(w, py_seeds[b]);
+      w[MT_N + 1] = MT_N;  // no lazy words
+    });
+    std::vector<uint32_t> hot(B * HOT_WORDS, 0u);
+    for (size_t b = 0; b < B; ++b) { hot[b * HOT_WORDS] = MT_N; hot[b * HOT_WORDS + 1] = MT_N; }
     HIP_OK(hipDeviceSynchronize());
-    HIP_OK(hipMemcpy(h->d_opp, st.data(), B * W * 4, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(h->d_opp, op.data(), B * OPP_WORDS * 4, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(h->d_hot, hot.data(), B * HOT_WORDS * 4, hipMemcpyHostToDevice));
   }
-  return 0;
-}
-
-static int mt_copy(td_handle* h, uint32_t* dev, int b, uint32_t* host, bool to_dev) {
-  if (!h || b < 0 || b >= h->B || !host) return fail("bad board or NULL state");
-  HIP_OK(hipDeviceSynchronize());
-  if (to_dev) HIP_OK(hipMemcpy(dev + (size_t)b * (MT_N + 1), host, (MT_N + 1) * 4, hipMemcpyHostToDevice));
-  else HIP_OK(hipMemcpy(host, dev + (size_t)b * (MT_N + 1), (MT_N + 1) * 4, hipMemcpyDeviceToHost));
   return 0;
 }
 
 int td_set_py_state(td_handle* h, int b, const uint32_t* mt) {
-  return mt_copy(h, h ? h->d_opp : nullptr, b, const_cast<uint32_t*>(mt), true);
+  if (!h || b < 0 || b >= h->B || !mt) return fail("bad board or NULL state");
+  uint32_t w[OPP_WORDS];
+  std::memcpy(w, mt, (MT_N + 1) * 4);
+  w[MT_N + 1] = MT_N;
+  uint32_t hot[HOT_WORDS] = {w[MT_N], MT_N, 0u};
+  HIP_OK(hipDeviceSynchronize());
+  HIP_OK(hipMemcpy(h->d_opp + (size_t)b * OPP_WORDS, w, sizeof w, hipMemcpyHostToDevice));
+  HIP_OK(hipMemcpy(h->d_hot + (size_t)b * HOT_WORDS, hot, sizeof hot, hipMemcpyHostToDevice));
+  return 0;
 }
-int td_get_py_state(td_handle* h, int b, uint32_t* mt) { return mt_copy(h, h ? h->d_opp : nullptr, b, mt, false); }
-int td_get_np_state(td_handle* h, int b, uint32_t* mt) { return mt_copy(h, h ? h->d_np : nullptr, b, mt, false); }
+// The device keeps the opponent's position in the hot record and may have
+// pre-drawn (and lazily twisted) ahead of it; the exported state is CPython's
+// getstate() form of the same stream (equal future draws).
+int td_get_py_state(td_handle* h, int b, uint32_t* mt) {
+  if (!h || b < 0 || b >= h->B || !mt) return fail("bad board or NULL state");
+  uint32_t w[OPP_WORDS], hot[HOT_WORDS];
+  HIP_OK(hipDeviceSynchronize());
+  HIP_OK(hipMemcpy(w, h->d_opp + (size_t)b * OPP_WORDS, sizeof w, hipMemcpyDeviceToHost));
+  HIP_OK(hipMemcpy(hot, h->d_hot + (size_t)b * HOT_WORDS, sizeof hot, hipMemcpyDeviceToHost));
+  w[MT_N] = hot[0];
+  w[MT_N + 1] = hot[1];
+  mt_finish_lazy(w);
+  std::memcpy(mt, w, (MT_N + 1) * 4);
+  return 0;
+}
+int td_get_np_state(td_handle* h, int b, uint32_t* mt) {
+  if (!h || b < 0 || b >= h->B || !mt) return fail("bad board or NULL state");
+  uint32_t w[OPP_WORDS];
+  HIP_OK(hipDeviceSynchronize());
+  HIP_OK(hipMemcpy(w, h->d_np + (size_t)b * OPP_WORDS, sizeof w, hipMemcpyDeviceToHost));
+  mt_finish_lazy(w);
+  std::memcpy(mt, w, (MT_N + 1) * 4);
+  return 0;
+}
 int td_set_np_state(td_handle* h, int b, const uint32_t* mt) {
-  if (mt_copy(h, h ? h->d_np : nullptr, b, const_cast<uint32_t*>(mt), true)) return -1;
+  if (!h || b < 0 || b >= h->B || !mt) return fail("bad board or NULL state");
+  uint32_t w[OPP_WORDS];
+  std::memcpy(w, mt, (MT_N + 1) * 4);
+  w[MT_N + 1] = MT_N;
+  HIP_OK(hipDeviceSynchronize());
+  HIP_OK(hipMemcpy(h->d_np + (size_t)b * OPP_WORDS, w, sizeof w, hipMemcpyHostToDevice));
   return drop_staged(h, b);
 }
 
@@ -402,7 +482,7 @@ int td_step(td_handle* h, const td_step_io* io, void* stream) {
   a.stamps = h->d_stamps;
   HIP_OK(launch_step(a, s, false));
   h->steps += 1;
-  if (h->autoreset && (h->steps % kRefillEvery) == 0) HIP_OK(launch_refill(a, s));
+  if (h->autoreset && (h->steps % kRefillEvery) == 0 && start_refill(h, s)) return -1;
   return 0;
 }
 
@@ -421,7 +501,7 @@ int td_layout_generate(uint32_t* np_state625, int map_size, int max_attempts, ui
 
 size_t td_state_bytes(td_handle* h, int count) {
   if (!h || count < 0) return 0;
-  return (size_t)count * (sizeof(TdHdr) + ECAP * (8 + 8 + 4) + TCAP * (8 + 4) + (size_t)h->NC * 4 + (MT_N + 1) * 4);
+  return (size_t)count * (sizeof(TdHdr) + ECAP * (8 + 8 + 4) + TCAP * (8 + 4) + (size_t)h->NC * 4 + OPP_WORDS * 4);
 }
 
 static int state_copy(td_handle* h, int b0, int count, void* host, bool to_host) {
@@ -436,10 +516,26 @@ static int state_copy(td_handle* h, int b0, int count, void* host, bool to_host)
     p += bytes;
     return 0;
   };
+  uint32_t* opp = (uint32_t*)(p + (size_t)count * (sizeof(TdHdr) + ECAP * 20 + TCAP * 12 + (size_t)h->NC * 4));
+  std::vector<uint32_t> hot((size_t)count * HOT_WORDS);
+  if (!to_host) {  // the hot record follows the imported words (no pre-drawn outputs)
+    for (int i = 0; i < count; ++i) {
+      hot[(size_t)i * HOT_WORDS] = opp[(size_t)i * OPP_WORDS + MT_N];
+      hot[(size_t)i * HOT_WORDS + 1] = opp[(size_t)i * OPP_WORDS + MT_N + 1];
+    }
+    HIP_OK(hipMemcpy(h->d_hot + (size_t)b0 * HOT_WORDS, hot.data(), hot.size() * 4, hipMemcpyHostToDevice));
+  }
   if (cp(h->d_hdr, sizeof(TdHdr)) || cp(h->d_en_lp, ECAP * 8) || cp(h->d_en_mg, ECAP * 8) ||
       cp(h->d_en_inf, ECAP * 4) || cp(h->d_tw_cd, TCAP * 8) || cp(h->d_tw_inf, TCAP * 4) ||
-      cp(h->d_cells, (size_t)h->NC * 4) || cp(h->d_opp, (MT_N + 1) * 4))
+      cp(h->d_cells, (size_t)h->NC * 4) || cp(h->d_opp, OPP_WORDS * 4))
     return -1;
+  if (to_host) {  // position and lazy boundary live in the hot record
+    HIP_OK(hipMemcpy(hot.data(), h->d_hot + (size_t)b0 * HOT_WORDS, hot.size() * 4, hipMemcpyDeviceToHost));
+    for (int i = 0; i < count; ++i) {
+      opp[(size_t)i * OPP_WORDS + MT_N] = hot[(size_t)i * HOT_WORDS];
+      opp[(size_t)i * OPP_WORDS + MT_N + 1] = hot[(size_t)i * HOT_WORDS + 1];
+    }
+  }
   return 0;
 }
 

@@ -9,7 +9,7 @@
 //   tw_cd   f64              [B][TCAP]   tower cool-down     (Tower.cd, :54)
 //   tw_inf  u32              [B][TCAP]   cell | type<<12 | lv<<14
 //   cells   u32              [B][L*L]    cell words (td_layout.h bit layout)
-//   opp_mt  u32              [B][625]    CPython-random MT19937 of the built-in opponent
+//   opp_mt  u32              [B][626]    CPython-random MT19937 of the built-in opponent (lazy twist)
 //   nxt     u32              [B][8+L*L]  staged layout for the board's next episode
 // Enemy / tower lists keep the reference's list order (index order).
 #pragma once
@@ -20,6 +20,9 @@ namespace td {
 constexpr int ECAP = 128;  // enemies alive per board (<=121 reachable with default config)
 constexpr int TCAP = 32;   // towers per board (<=25 reachable with default config)
 constexpr int NCH = 45;    // observation channels (TDBoard.py:146-154, default type/level counts)
+// Opponent stream words per board: MT19937 state [0..623], position [624], and the
+// lazy-twist boundary [625] (words [tw, 624) still hold the previous block).
+constexpr int OPP_WORDS = 626;
 
 enum Mode : int { MODE_DEF = 0, MODE_ATK = 1, MODE_2P = 2 };
 

@@ -6,6 +6,10 @@
 
 namespace td {
 
+// opponent hot record: [0] position, [1] lazy-twist boundary, [2] pre-drawn count,
+// [3] unused, [4..11] pre-drawn tempered outputs for positions pos .. pos+count-1
+constexpr int HOT_WORDS = 12;
+
 struct StepArgs {
   int B, L, mode, multi, difficulty, autoreset;
   TdHdr* hdr;
@@ -15,7 +19,8 @@ struct StepArgs {
   double* tw_cd;
   uint32_t* tw_inf;
   uint32_t* cells;
-  uint32_t* opp_mt;     // [B][625] CPython-random state of the built-in opponent
+  uint32_t* opp_mt;     // [B][626] CPython-random MT words of the built-in opponent ([624..625] unused)
+  uint32_t* opp_hot;    // [B][HOT_WORDS] its position, lazy-twist boundary, count and next 8 draws
   uint32_t* np_mt;      // [B][625] numpy-legacy state of the layout stream (TDGymBasic.np_random)
   uint32_t* nxt;        // [B][8 + L*L] staged next-episode layout (word 0 = magic while unconsumed)
   uint8_t* scratch;     // [B][scratch_stride] road-generation scratch

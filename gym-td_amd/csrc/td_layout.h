@@ -65,8 +65,9 @@ TD_HD inline RoadScratch road_scratch_carve(void* base, int L) {
   return s;
 }
 
+template <class RNG>
 struct RoadGen {
-  MtRef rng;
+  RNG& rng;
   int L;
   RoadScratch s;
   int max_attempts;
@@ -269,16 +270,19 @@ TD_HD inline int layout_from_roads(int L, int num_roads, const int32_t* cells, c
 }
 
 // TDGymBasic.reset (:42-51): num_roads = randint(1, 4) then create_road_v2, on one stream.
-TD_HD inline int episode_layout(uint32_t* np_state, int L, void* scratch, int max_attempts, uint32_t* rec) {
-  RoadGen g;
-  g.rng.w = np_state;
-  g.L = L;
-  g.s = road_scratch_carve(scratch, L);
-  g.max_attempts = max_attempts;
-  int nr = (int)g.rng.np_randint(1, 4);
+template <class RNG>
+TD_HD inline int episode_layout_rng(RNG& rng, int L, void* scratch, int max_attempts, uint32_t* rec) {
+  RoadGen<RNG> g{rng, L, road_scratch_carve(scratch, L), max_attempts};
+  int nr = (int)rng.np_randint(1, 4);
   int st = g.generate(nr, rec);
   if (st != ROAD_OK) { rec[0] = 0; rec[1] = (uint32_t)nr; rec[7] = (uint32_t)st; }
   return st;
+}
+
+// Host form on a 625-word numpy state (RandomState.get_state() words + position).
+TD_HD inline int episode_layout(uint32_t* np_state, int L, void* scratch, int max_attempts, uint32_t* rec) {
+  MtRef rng{np_state};
+  return episode_layout_rng(rng, L, scratch, max_attempts, rec);
 }
 
 }  // namespace td

@@ -101,6 +101,55 @@ struct MtRef {
   }
 };
 
+// Lazy-twist form used on the device (td_step.hip WaveMt): w[625] = tw, words
+// [tw, 624) of the current block are not yet twisted.  Complete them in place,
+// giving CPython's ``getstate()`` form (624 words + position).
+TD_HD inline void mt_finish_lazy(uint32_t* w) {
+  for (uint32_t p = w[625]; p < (uint32_t)MT_N; ++p) {
+    uint32_t y = (w[p] & 0x80000000u) | (w[(p + 1) % MT_N] & 0x7fffffffu);
+    w[p] = w[(p + MT_M) % MT_N] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+  }
+  w[625] = MT_N;
+}
+
+// MT19937 over 626 words with a lazy twist (see mt_finish_lazy): the next block's
+// word p is computed when drawn.  Draws are bit-identical to MtRef; the 624-word
+// twist loop never runs on the critical path.  pos / tw live in registers while
+// drawing; load() / store() move them from / to w[624], w[625].
+struct LazyMt {
+  uint32_t* w;
+  uint32_t pos, tw;
+  TD_HD void load() { pos = w[MT_N]; tw = w[MT_N + 1]; }
+  TD_HD void store() { w[MT_N] = pos; w[MT_N + 1] = tw; }
+  TD_HD uint32_t next() {
+    if (pos >= (uint32_t)MT_N) { pos = 0; tw = 0; }
+    uint32_t y;
+    if (pos >= tw) {
+      const uint32_t a = w[pos];
+      const uint32_t nb = w[pos == MT_N - 1 ? 0u : pos + 1u];
+      const uint32_t far = w[pos < (uint32_t)(MT_N - MT_M) ? pos + MT_M : pos - (MT_N - MT_M)];
+      const uint32_t yy = (a & 0x80000000u) | (nb & 0x7fffffffu);
+      y = far ^ (yy >> 1) ^ ((yy & 1u) ? 0x9908b0dfu : 0u);
+      w[pos] = y;
+      tw = pos + 1;
+    } else {
+      y = w[pos];
+    }
+    ++pos;
+    return mt_temper(y);
+  }
+  TD_HD int64_t np_randint(int64_t lo, int64_t hi) {  // numpy legacy masked rejection
+    if (hi <= lo) return lo;
+    uint64_t rng = (uint64_t)(hi - lo - 1);
+    if (rng == 0) return lo;
+    uint64_t mask = rng;
+    mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4; mask |= mask >> 8; mask |= mask >> 16;
+    uint32_t v;
+    while ((v = (next() & (uint32_t)mask)) > rng) {}
+    return lo + (int64_t)v;
+  }
+};
+
 TD_HD inline void py_seed(uint32_t* w, uint32_t seed) {
   uint32_t key[1] = {seed};
   mt_init_by_array(w, key, 1);

@@ -30,6 +30,8 @@ namespace td {
 #define STAMP(i) do { } while (0)
 #endif
 
+constexpr int MAX_KERNEL_L = 32;  // generic-L kernels: L <= 32
+
 enum : int { FC_OK = 0, FC_COST = 1, FC_POS = 2, FC_LVMAX = 3, FC_TARGET = 4, FC_CAP = 6 };  // utils/fail_code.py
 
 // ---------------------------------------------------------------------------
@@ -50,34 +52,51 @@ __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
 // per-board LDS image
 // ---------------------------------------------------------------------------
 template <int NC>
-struct Smem {
+struct alignas(16) Smem {
   uint32_t cell[NC];      // cell words (td_layout.h)
   uint8_t twr[NC];        // tower at cell: 0 none, else 0x80 | lv << 2 | type
   uint8_t grp[4][NC];     // enemy group (head enemy index) per (type, cell), 0xFF none
-  double eLP[ECAP];
-  double eMg[ECAP];
+  union {
+    struct {              // load .. march: the enemy list (written back right after the march)
+      double eLP[ECAP];
+      double eMg[ECAP];
+    };
+    float gst[ECAP][4];   // stats .. obs: group stats min, max, avg, count/8 by head enemy
+  };
   uint32_t eInf[ECAP];
-  float eR[ECAP];         // f32(LP / maxLP)
   union {
     double key[ECAP];     // sort keys
-    float gst[ECAP][4];   // group stats: min, max, avg, count/8
-    uint32_t scratch[4 * ECAP];
+    float eR[ECAP];       // f32(LP / maxLP)
   };
   double tCd[TCAP];
   uint32_t tInf[TCAP];
   float chv[48];          // broadcast channel values
-  float d9[256];          // channel 9 by distance
+  float d9[64];           // channel 9 by distance (road length < 2L <= 64)
   int32_t atk[24];        // attacker clusters of this step (TD-atk / TD-2p)
   int32_t real_atk[24];   // info['RealAction'] of the attacker
   int32_t fail_atk[4];    // info['FailCode'] of the attacker (-1 = no entry)
+  TdDevCfg cfg;           // constant block, staged once per board: per-lane table lookups hit LDS
 };
+
+// Stage the constant block into LDS (16 bytes per lane).
+template <int NC>
+__device__ __forceinline__ void stage_cfg(Smem<NC>& S, const TdDevCfg* g) {
+  static_assert(sizeof(TdDevCfg) % 16 == 0 && sizeof(TdDevCfg) <= 64 * 16, "cfg staging");
+  const int l = (int)threadIdx.x;
+  if (l < (int)(sizeof(TdDevCfg) / 16))
+    reinterpret_cast<uint4*>(&S.cfg)[l] = reinterpret_cast<const uint4*>(g)[l];
+}
 
 // Wave-uniform scalar board state (identical in every lane).
 struct U {
   double cost_def, cost_atk, ep_ret, progress;
   int steps, base_LP, atk_cd, def_cd, n, nt, num_roads, end_cell, maxdist, flags, episodes;
-  int start0, start1, start2;
-  __device__ __forceinline__ int start(int road) const { return road == 0 ? start0 : (road == 1 ? start1 : start2); }
+  bool cells_dirty;  // map[6] changed (tower built / destroyed) or a new layout: write the cells back
+  uint64_t starts;  // start cells of roads 0-2, 16 bits each (a shift, not an indexed field: keeps U in registers)
+  __device__ __forceinline__ int start(int road) const { return (int)((starts >> (16 * road)) & 0xffffu); }
+  __device__ __forceinline__ void set_starts(uint32_t s0, uint32_t s1, uint32_t s2) {
+    starts = (uint64_t)s0 | ((uint64_t)s1 << 16) | ((uint64_t)s2 << 32);
+  }
 };
 
 struct Ctx {
@@ -88,31 +107,73 @@ struct Ctx {
 // ---------------------------------------------------------------------------
 // CPython MT19937 for the built-in opponent, state in HBM, wave-parallel twist
 // ---------------------------------------------------------------------------
-// Rewrites the 624 words in chunks of 64 in index order: w[i+1] and w[i+397]
-// (i < 227) are still old, w[i-227] (i >= 227) was rewritten by an earlier
-// chunk -- the sequential result.  Once every 624 draws.
-__device__ __attribute__((noinline)) void wave_mt_twist(uint32_t* w, int lane) {
-  for (int base = 0; base < MT_N; base += 64) {
-    int i = base + lane;
-    uint32_t nv = 0;
-    if (i < MT_N) {
-      uint32_t y = (w[i] & 0x80000000u) | (w[(i + 1) % MT_N] & 0x7fffffffu);
-      nv = w[(i + MT_M) % MT_N] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
-    }
-    __syncthreads();
-    if (i < MT_N) w[i] = nv;
-    __threadfence_block();
-    __syncthreads();
-  }
-}
-
+// CPython MT19937 with a lazy twist: word p of a new block is twisted when it is
+// drawn.  In sequential order word p of the new block depends on old[p], old[p+1]
+// (new[0] for p = 623) and old[p+397] (p < 227) or new[p-227] (p >= 227), all of
+// which are available when p is drawn in order, so draws are bit-identical to
+// CPython's block twist without ever running the 624-word loop in the step.
+// State: w[0..623], pos = w[624], tw = w[625] (words [tw, 624) not yet twisted).
 struct WaveMt {
   uint32_t* w;
-  uint32_t pos;
-  int lane;
+  uint32_t pos, tw;
+  uint32_t cache = 0, cbase = 0, cn = 0;  // lane j: tempered output for position cbase + j (j < cn)
+
+  // Pre-draw the next up-to-8 words in parallel, one per lane, for the next
+  // step: issue() starts the loads, finish() (at the end of the step) lazily
+  // twists, stores and tempers them -- the memory latency overlaps the step.
+  uint32_t pa = 0, pnb = 0, pfar = 0;
+  bool plazy = false, pmine = false;
+  __device__ __forceinline__ void prefetch_issue(int lane) {
+    if (pos >= (uint32_t)MT_N) { pos = 0; tw = 0; }
+    cbase = pos;
+    cn = (uint32_t)MT_N - pos < 8u ? (uint32_t)MT_N - pos : 8u;
+    const uint32_t q = pos + (uint32_t)lane;
+    pmine = (uint32_t)lane < cn;
+    plazy = pmine && q >= tw;
+    if (pmine) {
+      pa = w[q];
+      if (plazy) {
+        // word q (< pos + 8 <= tw + 8) needs new[q - 227], twisted in an earlier step
+        pnb = w[q == MT_N - 1 ? 0u : q + 1u];
+        pfar = w[q < (uint32_t)(MT_N - MT_M) ? q + MT_M : q - (MT_N - MT_M)];
+      }
+    }
+  }
+  __device__ __forceinline__ void prefetch_finish(int lane) {
+    const uint32_t q = cbase + (uint32_t)lane;
+    uint32_t y = pa;
+    if (plazy) {
+      const uint32_t yy = (pa & 0x80000000u) | (pnb & 0x7fffffffu);
+      y = pfar ^ (yy >> 1) ^ ((yy & 1u) ? 0x9908b0dfu : 0u);
+      w[q] = y;  // after every lane's loads (data dependency)
+    }
+    if (cbase + cn > tw) tw = cbase + cn;
+    cache = pmine ? mt_temper(y) : 0u;
+  }
+  __device__ __forceinline__ void prefetch(int lane) {
+    prefetch_issue(lane);
+    prefetch_finish(lane);
+  }
+
   __device__ __forceinline__ uint32_t next() {
-    if (pos >= (uint32_t)MT_N) { wave_mt_twist(w, lane); pos = 0; }
-    uint32_t y = w[pos];
+    const uint32_t d = pos - cbase;
+    if (d < cn) {
+      ++pos;
+      return (uint32_t)__shfl((int)cache, (int)d);
+    }
+    if (pos >= (uint32_t)MT_N) { pos = 0; tw = 0; cn = 0; }
+    uint32_t y;
+    if (pos >= tw) {
+      const uint32_t a = w[pos];
+      const uint32_t nb = w[pos == MT_N - 1 ? 0u : pos + 1u];
+      const uint32_t far = w[pos < (uint32_t)(MT_N - MT_M) ? pos + MT_M : pos - (MT_N - MT_M)];
+      const uint32_t yy = (a & 0x80000000u) | (nb & 0x7fffffffu);
+      y = far ^ (yy >> 1) ^ ((yy & 1u) ? 0x9908b0dfu : 0u);
+      w[pos] = y;  // every lane stores the same word
+      tw = pos + 1;
+    } else {
+      y = w[pos];
+    }
     ++pos;
     return mt_temper(y);
   }
@@ -163,6 +224,7 @@ __device__ int tower_build(Smem<NC>& S, U& u, const Ctx& x, int t, int cell) {
   }
   u.nt += 1;
   u.cost_def = dsub(u.cost_def, price);                   // :238
+  u.cells_dirty = true;
   __syncthreads();
   diamond(S, x, cell, +1);                                // :239-245
   return FC_OK;
@@ -202,6 +264,7 @@ __device__ int tower_destruct(Smem<NC>& S, U& u, const Ctx& x, int cell) {
   int t = (ti >> 12) & 3, lv = (ti >> 14) & 1;
   u.cost_def = dadd(u.cost_def, dmul(x.C.t_value[t][lv], x.C.destruct_return));  // :276
   u.cost_def = pymin(u.cost_def, x.C.max_cost);                                  // :277
+  u.cells_dirty = true;
   // towers.remove(t): keep the order of the rest (:278)
   uint32_t vi = 0;
   double vc = 0.0;
@@ -396,53 +459,63 @@ __device__ double board_step(Smem<NC>& S, U& u, const Ctx& x, const StepArgs& a,
   }
 
   STAMP(3);
-  // --- towers fire in list order (:306-313); dead enemies stay targetable
-  for (int k = 0; k < u.nt; ++k) {
-    double cd = dsub(S.tCd[k], 1.0);                        // :307
-    if (!(cd > 0.0)) {
-      const uint32_t ti = S.tInf[k];
-      const int tt = (ti >> 12) & 3, tl = (ti >> 14) & 1, tc = ti & 0xfff;
-      const double rge = C.t_rge[tt][tl];
-      bool in0 = val[0] && (double)cheb(en_cell(inf[0]), tc, L) <= rge;
-      bool in1 = val[1] && (double)cheb(en_cell(inf[1]), tc, L) <= rge;
-      uint64_t m0 = ballot(in0), m1 = ballot(in1);
-      if (m0 | m1) {
-        const int tgt = m0 ? ctz64(m0) : 64 + ctz64(m1);
-        cd = dadd(cd, C.t_intv[tt][tl]);                    // cd += intv
-        const double atk = C.t_atk[tt][tl];
-        if (tt <= 1) {  // TowerArrow / TowerMagic (TDElements.py:71-93)
-          if (lane == (tgt & 63)) {
-            if (tgt < 64) lp[0] = damage(lp[0], atk, C.e_def[en_type(inf[0])][en_lv(inf[0])], tt == 1);
-            else lp[1] = damage(lp[1], atk, C.e_def[en_type(inf[1])][en_lv(inf[1])], tt == 1);
-          }
-        } else {
-          const uint32_t tinf = (tgt >> 6) ? __shfl(inf[1], tgt & 63) : __shfl(inf[0], tgt & 63);
-          const int tgc = en_cell(tinf);
-          const double dr = C.t_dmg[tt][tl];
-          if (tt == 2) {  // TowerBomb splash (:95-110)
+  // --- towers fire in list order (:306-313); dead enemies stay targetable.
+  // Tower k lives in lane k (cool-down in a register); a fired tower is read
+  // with a wave-uniform lane index (v_readlane).
+  double tcd = lane < u.nt ? S.tCd[lane] : 0.0;
+  const uint32_t tinf_l = lane < u.nt ? S.tInf[lane] : 0u;
+  if (n == 0) {
+    // no enemy anywhere: every tower just cools down (cd -= 1; no target; clamp at 0)
+    if (lane < u.nt) { const double cd = dsub(tcd, 1.0); tcd = cd > 0.0 ? cd : 0.0; }
+  } else {
+    for (int k = 0; k < u.nt; ++k) {
+      double cd = dsub(__shfl(tcd, k), 1.0);                 // :307
+      if (!(cd > 0.0)) {
+        const uint32_t ti = __shfl(tinf_l, k);
+        const int tt = (ti >> 12) & 3, tl = (ti >> 14) & 1, tc = ti & 0xfff;
+        const double rge = C.t_rge[tt][tl];
+        bool in0 = val[0] && (double)cheb(en_cell(inf[0]), tc, L) <= rge;
+        bool in1 = val[1] && (double)cheb(en_cell(inf[1]), tc, L) <= rge;
+        uint64_t m0 = ballot(in0), m1 = ballot(in1);
+        if (m0 | m1) {
+          const int tgt = m0 ? ctz64(m0) : 64 + ctz64(m1);
+          cd = dadd(cd, C.t_intv[tt][tl]);                   // cd += intv
+          const double atk = C.t_atk[tt][tl];
+          if (tt <= 1) {  // TowerArrow / TowerMagic (TDElements.py:71-93)
+            if (lane == (tgt & 63)) {
+              if (tgt < 64) lp[0] = damage(lp[0], atk, C.e_def[en_type(inf[0])][en_lv(inf[0])], tt == 1);
+              else lp[1] = damage(lp[1], atk, C.e_def[en_type(inf[1])][en_lv(inf[1])], tt == 1);
+            }
+          } else {
+            const uint32_t tinf = (tgt >> 6) ? __shfl(inf[1], tgt & 63) : __shfl(inf[0], tgt & 63);
+            const int tgc = en_cell(tinf);
+            const double dr = C.t_dmg[tt][tl];
+            if (tt == 2) {  // TowerBomb splash (:95-110)
 #pragma unroll
-            for (int s = 0; s < 2; ++s)
-              if (val[s] && (double)cheb(tgc, en_cell(inf[s]), L) <= dr)
-                lp[s] = damage(lp[s], atk, C.e_def[en_type(inf[s])][en_lv(inf[s])], false);
-          } else {  // TowerFrozen: first enemy within splash of the target (:112-132)
-            bool h0 = val[0] && (double)cheb(tgc, en_cell(inf[0]), L) <= dr;
-            bool h1 = val[1] && (double)cheb(tgc, en_cell(inf[1]), L) <= dr;
-            uint64_t q0 = ballot(h0), q1 = ballot(h1);
-            if (q0 | q1) {
-              const int f = q0 ? ctz64(q0) : 64 + ctz64(q1);
-              if (lane == (f & 63)) {
-                const uint32_t slow = (uint32_t)C.frozen_time << 16;
-                if (f < 64) { lp[0] = damage(lp[0], atk, 0.0, true); inf[0] = (inf[0] & 0xffffu) | slow; }
-                else { lp[1] = damage(lp[1], atk, 0.0, true); inf[1] = (inf[1] & 0xffffu) | slow; }
+              for (int s = 0; s < 2; ++s)
+                if (val[s] && (double)cheb(tgc, en_cell(inf[s]), L) <= dr)
+                  lp[s] = damage(lp[s], atk, C.e_def[en_type(inf[s])][en_lv(inf[s])], false);
+            } else {  // TowerFrozen: first enemy within splash of the target (:112-132)
+              bool h0 = val[0] && (double)cheb(tgc, en_cell(inf[0]), L) <= dr;
+              bool h1 = val[1] && (double)cheb(tgc, en_cell(inf[1]), L) <= dr;
+              uint64_t q0 = ballot(h0), q1 = ballot(h1);
+              if (q0 | q1) {
+                const int f = q0 ? ctz64(q0) : 64 + ctz64(q1);
+                if (lane == (f & 63)) {
+                  const uint32_t slow = (uint32_t)C.frozen_time << 16;
+                  if (f < 64) { lp[0] = damage(lp[0], atk, 0.0, true); inf[0] = (inf[0] & 0xffffu) | slow; }
+                  else { lp[1] = damage(lp[1], atk, 0.0, true); inf[1] = (inf[1] & 0xffffu) | slow; }
+                }
               }
             }
           }
         }
+        if (cd < 0.0) cd = 0.0;                              // :311-312
       }
-      if (cd < 0.0) cd = 0.0;                               // :311-312
+      if (lane == k) tcd = cd;
     }
-    if (lane == 0) S.tCd[k] = cd;
   }
+  if (lane < u.nt) S.tCd[lane] = tcd;
 
   STAMP(4);
   // --- kills (:313-317): every enemy at LP 0 was hit this step
@@ -497,6 +570,9 @@ __device__ double board_step(Smem<NC>& S, U& u, const Ctx& x, const StepArgs& a,
   u.cost_atk = pymin(dadd(u.cost_atk, rate), C.max_cost);
   u.cost_def = pymin(dadd(u.cost_def, C.def_rate), C.max_cost);
   __syncthreads();
+  // the enemy list is final for this step: write it back now (its LDS is reused by the stats)
+  const size_t eb = (size_t)b * ECAP;
+  for (int i = lane; i < n2; i += 64) { a.en_lp[eb + i] = S.eLP[i]; a.en_mg[eb + i] = S.eMg[i]; a.en_inf[eb + i] = S.eInf[i]; }
   return reward;
 }
 
@@ -507,6 +583,7 @@ template <int NC>
 __device__ void enemy_stats(Smem<NC>& S, const U& u, const Ctx& x) {
   const TdDevCfg& C = x.C;
   const int n = u.n;
+  if (n == 0) return;  // write_obs emits zero planes without reading grp
   for (int i = x.lane; i < 4 * NC; i += 64) (&S.grp[0][0])[i] = 0xFF;
   uint32_t key[2];
   bool val[2];
@@ -573,51 +650,99 @@ __device__ void channel_scalars(Smem<NC>& S, const U& u, const Ctx& x) {
     S.chv[l] = v;
   }
   // s[9] = map[4] / (max(map[4]) + 1): int32 scalar divisor promotes to f64, rounded once to f32
-  for (int d = l; d <= u.maxdist && d < 256; d += 64) S.d9[d] = f32(ddiv((double)d, (double)(u.maxdist + 1)));
+  for (int d = l; d <= u.maxdist && d < 64; d += 64) S.d9[d] = f32(ddiv((double)d, (double)(u.maxdist + 1)));
   __syncthreads();
 }
 
+// Binary observation channels as bits of one word per cell (bit c = channel c):
+// 0-3 roads, 4 end, 6-8 starts, 14 buildable (map[6] == 0), 15-16 tower level,
+// 17-20 tower type (TDBoard.py:113-133).
+constexpr uint32_t kBinaryChannels = 0x1FC1DFu;
+
+__device__ __forceinline__ uint32_t cell_bits(uint32_t w, uint32_t tw) {
+  uint32_t m = (w & 0x1Fu) | (((w >> 5) & 7u) << 6) | ((w >> 24) == 0u ? (1u << 14) : 0u);
+  if (tw & 0x80u) m |= (1u << (15u + ((tw >> 2) & 1u))) | (1u << (17u + (tw & 3u)));
+  return m;
+}
+
+__device__ __forceinline__ float bitf(uint32_t m, int ch) { return (float)((m >> ch) & 1u); }
+
+// Channel ch of cells 4q .. 4q+3 (TDBoard.get_states, :112-143).
 template <int NC>
-__device__ __forceinline__ float obs_value(const Smem<NC>& S, int ch, int cell) {
-  const uint32_t w = S.cell[cell];
-  if (ch < 5) return (float)((w >> ch) & 1u);                      // 0-3 roads, 4 end
-  if (ch >= 6 && ch < 9) return (float)((w >> (ch - 1)) & 1u);     // 6-8 starts (bits 5-7)
-  if (ch == 9) return S.d9[cw_dist(w)];
-  if (ch == 14) return cw_block(w) == 0 ? 1.0f : 0.0f;
-  if (ch >= 15 && ch < 21) {
-    const uint32_t tw = S.twr[cell];
-    if (!(tw & 0x80u)) return 0.0f;
-    if (ch < 17) return ((int)((tw >> 2) & 1u) == ch - 15) ? 1.0f : 0.0f;
-    return ((int)(tw & 3u) == ch - 17) ? 1.0f : 0.0f;
+__device__ __forceinline__ float4 obs_quad(const Smem<NC>& S, int ch, int q, bool any_enemy) {
+  float4 v;
+  if (ch < 32 && ((kBinaryChannels >> ch) & 1u)) {
+    const uint4 w = *reinterpret_cast<const uint4*>(&S.cell[4 * q]);
+    const uint32_t tw = *reinterpret_cast<const uint32_t*>(&S.twr[4 * q]);
+    v.x = bitf(cell_bits(w.x, tw & 0xffu), ch);
+    v.y = bitf(cell_bits(w.y, (tw >> 8) & 0xffu), ch);
+    v.z = bitf(cell_bits(w.z, (tw >> 16) & 0xffu), ch);
+    v.w = bitf(cell_bits(w.w, tw >> 24), ch);
+  } else if (ch == 9) {
+    const uint4 w = *reinterpret_cast<const uint4*>(&S.cell[4 * q]);
+    v.x = S.d9[cw_dist(w.x)];
+    v.y = S.d9[cw_dist(w.y)];
+    v.z = S.d9[cw_dist(w.z)];
+    v.w = S.d9[cw_dist(w.w)];
+  } else if (ch >= 25 && ch < 41) {
+    const int e = ch - 25, st = e >> 2, t = e & 3;
+    v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    const uint32_t g4 = any_enemy ? *reinterpret_cast<const uint32_t*>(&S.grp[t][4 * q]) : 0xFFFFFFFFu;
+    if (g4 != 0xFFFFFFFFu) {
+      const uint32_t g0 = g4 & 0xffu, g1 = (g4 >> 8) & 0xffu, g2 = (g4 >> 16) & 0xffu, g3 = g4 >> 24;
+      if (g0 != 0xffu) v.x = S.gst[g0][st];
+      if (g1 != 0xffu) v.y = S.gst[g1][st];
+      if (g2 != 0xffu) v.z = S.gst[g2][st];
+      if (g3 != 0xffu) v.w = S.gst[g3][st];
+    }
+  } else {  // 5, 10-13, 21-24, 41-44: one value for the whole plane
+    const float c = S.chv[ch];
+    v = make_float4(c, c, c, c);
   }
-  if (ch >= 25 && ch < 41) {
-    const int q = ch - 25, st = q >> 2, t = q & 3;
-    const uint32_t g = S.grp[t][cell];
-    return g == 0xFFu ? 0.0f : S.gst[g][st];
-  }
-  return S.chv[ch];  // 5, 10-13, 21-24, 41-44
+  return v;
 }
 
 template <int NC>
-__device__ void write_obs(const Smem<NC>& S, const Ctx& x, float* out) {
-  const int ncr = x.NCr;
+__device__ __forceinline__ float obs_value(const Smem<NC>& S, int ch, int cell, bool any_enemy) {
+  const uint32_t w = S.cell[cell];
+  if (ch < 32 && ((kBinaryChannels >> ch) & 1u)) return bitf(cell_bits(w, S.twr[cell]), ch);
+  if (ch == 9) return S.d9[cw_dist(w)];
+  if (ch >= 25 && ch < 41) {
+    if (!any_enemy) return 0.0f;
+    const int e = ch - 25;
+    const uint32_t g = S.grp[e & 3][cell];
+    return g == 0xFFu ? 0.0f : S.gst[g][e >> 2];
+  }
+  return S.chv[ch];
+}
+
+// The (45, L, L) float32 observation, 16-byte stores.  When a plane has at most
+// 64 quads (L = 10: 25), each lane keeps one quad and the wave writes
+// floor(64 / quads) adjacent planes per store instruction; otherwise the
+// board's quads are swept in order.
+template <int NC, int LT>
+__device__ void write_obs(const Smem<NC>& S, const Ctx& x, float* out, bool any_enemy) {
+  const int ncr = LT ? LT * LT : x.NCr;
   if ((ncr & 3) == 0) {
+    const int Q = ncr / 4;
     float4* o4 = reinterpret_cast<float4*>(out);
-    const int nq = NCH * ncr / 4;
-    for (int q = x.lane; q < nq; q += 64) {
-      const int f = q * 4, ch = f / ncr, cell = f - ch * ncr;
-      float4 v;
-      v.x = obs_value(S, ch, cell);
-      v.y = obs_value(S, ch, cell + 1);
-      v.z = obs_value(S, ch, cell + 2);
-      v.w = obs_value(S, ch, cell + 3);
-      o4[q] = v;
+    if (Q <= 64) {
+      const int G = 64 / Q, q = x.lane % Q, g = x.lane / Q;
+      if (g < G) {
+        for (int ch = g; ch < NCH; ch += G) o4[ch * Q + q] = obs_quad(S, ch, q, any_enemy);
+      }
+    } else {
+      const int nq = NCH * Q;
+      for (int i = x.lane; i < nq; i += 64) {
+        const int ch = i / Q;
+        o4[i] = obs_quad(S, ch, i - ch * Q, any_enemy);
+      }
     }
   } else {
     const int nf = NCH * ncr;
     for (int f = x.lane; f < nf; f += 64) {
       const int ch = f / ncr;
-      out[f] = obs_value(S, ch, f - ch * ncr);
+      out[f] = obs_value(S, ch, f - ch * ncr, any_enemy);
     }
   }
 }
@@ -627,22 +752,32 @@ __device__ void write_obs(const Smem<NC>& S, const Ctx& x, float* out) {
 // ---------------------------------------------------------------------------
 template <int NC>
 __device__ void load_board(Smem<NC>& S, U& u, const Ctx& x, const StepArgs& a, int b) {
+  // Issue every load of the board before waiting on any: the first 64 enemy
+  // slots and all tower slots are fetched speculatively alongside the header
+  // (one memory round trip instead of header -> lists).
+  const size_t eb = (size_t)b * ECAP, tb = (size_t)b * TCAP, cb = (size_t)b * x.NCr;
+  const double lp0 = a.en_lp[eb + x.lane], mg0 = a.en_mg[eb + x.lane];
+  const uint32_t in0 = a.en_inf[eb + x.lane];
+  const double tcd0 = a.tw_cd[tb + (x.lane & (TCAP - 1))];
+  const uint32_t tin0 = a.tw_inf[tb + (x.lane & (TCAP - 1))];
+  for (int i = x.lane; i < x.NCr; i += 64) { S.cell[i] = a.cells[cb + i]; S.twr[i] = 0; }
   const TdHdr& h = a.hdr[b];
   u.cost_def = h.cost_def; u.cost_atk = h.cost_atk; u.ep_ret = h.ep_return;
   u.steps = h.steps; u.base_LP = h.base_LP; u.atk_cd = h.atk_cd; u.def_cd = h.def_cd;
   u.n = h.n_en; u.nt = h.n_tw; u.num_roads = h.num_roads; u.end_cell = h.end_cell;
-  u.start0 = h.start_cell[0]; u.start1 = h.start_cell[1]; u.start2 = h.start_cell[2];
+  u.set_starts(h.start_cell[0], h.start_cell[1], h.start_cell[2]);
   u.maxdist = h.maxdist; u.flags = h.flags; u.episodes = h.episodes;
   u.progress = ddiv((double)u.steps, (double)x.C.max_episode_steps);
-  const size_t eb = (size_t)b * ECAP, tb = (size_t)b * TCAP, cb = (size_t)b * x.NCr;
-  for (int i = x.lane; i < x.NCr; i += 64) { S.cell[i] = a.cells[cb + i]; S.twr[i] = 0; }
-  for (int i = x.lane; i < u.n; i += 64) { S.eLP[i] = a.en_lp[eb + i]; S.eMg[i] = a.en_mg[eb + i]; S.eInf[i] = a.en_inf[eb + i]; }
-  if (x.lane < u.nt) { S.tCd[x.lane] = a.tw_cd[tb + x.lane]; S.tInf[x.lane] = a.tw_inf[tb + x.lane]; }
-  __syncthreads();
+  u.cells_dirty = false;
+  if (x.lane < u.n) { S.eLP[x.lane] = lp0; S.eMg[x.lane] = mg0; S.eInf[x.lane] = in0; }
+  for (int i = 64 + x.lane; i < u.n; i += 64) { S.eLP[i] = a.en_lp[eb + i]; S.eMg[i] = a.en_mg[eb + i]; S.eInf[i] = a.en_inf[eb + i]; }
   if (x.lane < u.nt) {
-    uint32_t ti = S.tInf[x.lane];
-    S.twr[ti & 0xfffu] = (uint8_t)(0x80u | (((ti >> 14) & 1u) << 2) | ((ti >> 12) & 3u));
+    S.tCd[x.lane] = tcd0;
+    S.tInf[x.lane] = tin0;
   }
+  __syncthreads();
+  if (x.lane < u.nt)
+    S.twr[tin0 & 0xfffu] = (uint8_t)(0x80u | (((tin0 >> 14) & 1u) << 2) | ((tin0 >> 12) & 3u));
   __syncthreads();
 }
 
@@ -652,10 +787,11 @@ __device__ void reset_board(Smem<NC>& S, U& u, const Ctx& x, const uint32_t* rec
   const TdDevCfg& C = x.C;
   for (int i = x.lane; i < x.NCr; i += 64) { S.cell[i] = rec[LAYOUT_HDR + i]; S.twr[i] = 0; }
   u.num_roads = (int)rec[1]; u.end_cell = (int)rec[2]; u.maxdist = (int)rec[3];
-  u.start0 = (int)rec[4]; u.start1 = (int)rec[5]; u.start2 = (int)rec[6];
+  u.set_starts(rec[4], rec[5], rec[6]);
   u.cost_def = C.def_init_cost; u.cost_atk = C.atk_init_cost;
   u.base_LP = C.base_LP; u.steps = 0; u.progress = 0.0;
   u.atk_cd = 0; u.def_cd = 0; u.n = 0; u.nt = 0; u.ep_ret = 0.0;
+  u.cells_dirty = true;
   __syncthreads();
 }
 
@@ -666,14 +802,15 @@ __device__ void store_board(const Smem<NC>& S, const U& u, const Ctx& x, const S
     h.cost_def = u.cost_def; h.cost_atk = u.cost_atk; h.ep_return = u.ep_ret;
     h.steps = u.steps; h.base_LP = u.base_LP; h.atk_cd = u.atk_cd; h.def_cd = u.def_cd;
     h.n_en = u.n; h.n_tw = u.nt; h.num_roads = u.num_roads; h.end_cell = u.end_cell;
-    h.start_cell[0] = u.start0; h.start_cell[1] = u.start1; h.start_cell[2] = u.start2;
+    h.start_cell[0] = u.start(0); h.start_cell[1] = u.start(1); h.start_cell[2] = u.start(2);
     h.maxdist = u.maxdist; h.flags = u.flags; h.episodes = u.episodes;
     h.pad[0] = h.pad[1] = h.pad[2] = h.pad[3] = 0;
     a.hdr[b] = h;
   }
-  const size_t eb = (size_t)b * ECAP, tb = (size_t)b * TCAP, cb = (size_t)b * x.NCr;
-  for (int i = x.lane; i < x.NCr; i += 64) a.cells[cb + i] = S.cell[i];
-  for (int i = x.lane; i < u.n; i += 64) { a.en_lp[eb + i] = S.eLP[i]; a.en_mg[eb + i] = S.eMg[i]; a.en_inf[eb + i] = S.eInf[i]; }
+  const size_t tb = (size_t)b * TCAP, cb = (size_t)b * x.NCr;
+  if (u.cells_dirty)
+    for (int i = x.lane; i < x.NCr; i += 64) a.cells[cb + i] = S.cell[i];
+  // enemies were written back at the end of board_step
   if (x.lane < u.nt) { a.tw_cd[tb + x.lane] = S.tCd[x.lane]; a.tw_inf[tb + x.lane] = S.tInf[x.lane]; }
 }
 
@@ -789,23 +926,6 @@ __device__ void opponent_tower(Smem<NC>& S, U& u, const Ctx& x, WaveMt& R, int d
   build_near_road(S, u, x, R, t, false);
 }
 
-// One lane: the next episode layout of board b from its numpy stream into its
-// staged slot (TDGymBasic.reset :42-51); failing draws are skipped up to ``retries``.
-__device__ __attribute__((noinline)) int draw_layout(const StepArgs& a, int b, int retries) {
-  uint32_t* w = a.np_mt + (size_t)b * (MT_N + 1);
-  uint32_t* rec = a.nxt + (size_t)b * (LAYOUT_HDR + a.L * a.L);
-  void* scr = a.scratch + (size_t)b * a.scratch_stride;
-  int st = ROAD_ERR_BOUND;
-  for (int t = 0; t <= retries; ++t) {
-    st = episode_layout(w, a.L, scr, kRoadAttempts, rec);
-    if (st == ROAD_OK) break;
-  }
-  return st;
-}
-
-// ---------------------------------------------------------------------------
-// kernels
-// ---------------------------------------------------------------------------
 // Attacker clusters of TD-atk (TDAttack.py:36-46) and TD-2p (TDMulti.py:199-206, 229-241).
 template <int NC, int MODE>
 __device__ void attacker_actions(Smem<NC>& S, U& u, const Ctx& x, const StepArgs& a, int b) {
@@ -850,9 +970,10 @@ __device__ void attacker_actions(Smem<NC>& S, U& u, const Ctx& x, const StepArgs
 }
 
 
-template <int NC, int MODE>
+template <int NC, int LT, int MODE>
 __device__ void step_board(Smem<NC>& S, const StepArgs& a, int b, int L) {
-  const Ctx x{*a.cfg, L, L * L, (int)threadIdx.x};
+  stage_cfg(S, a.cfg);
+  const Ctx x{S.cfg, L, L * L, (int)threadIdx.x};
   const TdDevCfg& C = x.C;
   U u;
   STAMP(0);
@@ -871,7 +992,14 @@ __device__ void step_board(Smem<NC>& S, const StepArgs& a, int b, int L) {
     }
     return;
   }
-  WaveMt R{a.opp_mt + (size_t)b * (MT_N + 1), a.opp_mt[(size_t)b * (MT_N + 1) + MT_N], x.lane};
+  // built-in opponent stream: position, lazy-twist boundary and the next draws
+  // (pre-computed by the previous step) come from the board's hot record
+  uint32_t* const opp = a.opp_mt + (size_t)b * OPP_WORDS;
+  uint32_t* const hot = a.opp_hot + (size_t)b * HOT_WORDS;
+  WaveMt R{opp, hot[0], hot[1]};
+  R.cn = hot[2];
+  R.cbase = R.pos;
+  R.cache = x.lane < 8 ? hot[4 + x.lane] : 0u;
 
   u.atk_cd = u.atk_cd - 1 > 0 ? u.atk_cd - 1 : 0;
   u.def_cd = u.def_cd - 1 > 0 ? u.def_cd - 1 : 0;
@@ -901,6 +1029,8 @@ __device__ void step_board(Smem<NC>& S, const StepArgs& a, int b, int L) {
     attacker_actions<NC, MODE>(S, u, x, a, b);
     if (MODE == MODE_ATK) opponent_tower(S, u, x, R, a.difficulty);
   }
+  // pre-draw the next step's words: loads issued now, consumed at the end of the step
+  if (MODE != MODE_2P) R.prefetch_issue(x.lane);
   __syncthreads();
   STAMP(2);
 
@@ -930,23 +1060,22 @@ __device__ void step_board(Smem<NC>& S, const StepArgs& a, int b, int L) {
     }
   }
   STAMP(5);
-  if (!was_reset) enemy_stats(S, u, x);
-  else {
-    for (int i = x.lane; i < 4 * NC; i += 64) (&S.grp[0][0])[i] = 0xFF;
-    __syncthreads();
-  }
+  enemy_stats(S, u, x);  // no-op for a board without enemies (e.g. just reset)
   channel_scalars(S, u, x);
   STAMP(6);
-  write_obs(S, x, a.obs + (size_t)b * NCH * x.NCr);
+  write_obs<NC, LT>(S, x, a.obs + (size_t)b * NCH * x.NCr, u.n > 0);
   STAMP(7);
   store_board(S, u, x, a, b);
 
+  if (MODE != MODE_2P) R.prefetch_finish(x.lane);
   if (x.lane == 0) {
     if (was_reset) {
       a.nxt[(size_t)b * (LAYOUT_HDR + x.NCr)] = 0u;  // staged layout consumed: queue a refill
       a.queue[atomicAdd(a.qcount, 1u)] = b;
     }
-    a.opp_mt[(size_t)b * (MT_N + 1) + MT_N] = R.pos;
+    hot[0] = R.pos;
+    hot[1] = R.tw;
+    hot[2] = R.cn;
     a.reward[b] = reward;
     a.done[b] = done ? 1 : 0;
     if (a.win) a.win[b] = win;
@@ -956,6 +1085,7 @@ __device__ void step_board(Smem<NC>& S, const StepArgs& a, int b, int L) {
     if (a.ep_return) a.ep_return[b] = ep_ret;
     if (a.ep_len) a.ep_len[b] = ep_steps;
   }
+  if (MODE != MODE_2P && x.lane < 8) hot[4 + x.lane] = R.cache;
   if (MODE != MODE_DEF) {
     if (a.fail_atk && x.lane < 3) a.fail_atk[(size_t)b * 3 + x.lane] = S.fail_atk[x.lane];
     if (a.real_atk && x.lane < 24) a.real_atk[(size_t)b * 24 + x.lane] = S.real_atk[x.lane];
@@ -965,11 +1095,56 @@ __device__ void step_board(Smem<NC>& S, const StepArgs& a, int b, int L) {
 
 template <int LT, int MODE>
 __global__ __launch_bounds__(64) void td_step_kernel(StepArgs a) {
-  constexpr int NC = LT ? LT * LT : MAX_L * MAX_L / 4;
+  constexpr int NC = LT ? LT * LT : MAX_KERNEL_L * MAX_KERNEL_L;
   __shared__ Smem<NC> S;
   const int b = blockIdx.x;
   if (b >= a.B) return;
-  step_board<NC, MODE>(S, a, b, LT ? LT : a.L);
+  step_board<NC, LT, MODE>(S, a, b, LT ? LT : a.L);
+}
+
+// ---------------------------------------------------------------------------
+// episode layouts on the device
+// ---------------------------------------------------------------------------
+// LDS image of one layout draw: the board's numpy stream, the output record and
+// create_road_v2's scratch.  Lane 0 runs the (serial) generator entirely out of
+// LDS; the other lanes stage the stream and the record in and out.
+template <int NC>
+struct LayoutSmem {
+  uint32_t mt[OPP_WORDS];
+  uint32_t rec[LAYOUT_HDR + NC];
+  uint8_t scratch[14 * NC + 64];
+};
+
+// TDGymBasic.reset's draws (:42-51) for board b: the layout goes to its staged
+// slot nxt[b] (word 0 = magic written last), failing draws are skipped up to
+// ``retries`` times.  Returns the road status of the last draw (wave-uniform).
+template <int NC>
+__device__ int wave_layout(LayoutSmem<NC>& G, const StepArgs& a, int b, int retries) {
+  const int lane = (int)threadIdx.x, L = a.L, lw = LAYOUT_HDR + L * L;
+  uint32_t* gmt = a.np_mt + (size_t)b * OPP_WORDS;
+  uint32_t* grec = a.nxt + (size_t)b * lw;
+  for (int i = lane; i < OPP_WORDS; i += 64) G.mt[i] = gmt[i];
+  __syncthreads();
+  int st = ROAD_ERR_BOUND;
+  if (lane == 0) {
+    LazyMt rng{G.mt, 0, 0};
+    rng.load();
+    for (int t = 0; t <= retries; ++t) {
+      st = episode_layout_rng(rng, L, G.scratch, kRoadAttempts, G.rec);
+      if (st == ROAD_OK) break;
+    }
+    rng.store();
+  }
+  st = __shfl(st, 0);
+  __syncthreads();
+  for (int i = lane; i < OPP_WORDS; i += 64) gmt[i] = G.mt[i];
+  if (st == ROAD_OK) {
+    for (int i = 1 + lane; i < lw; i += 64) grec[i] = G.rec[i];
+    __threadfence();
+    __syncthreads();
+    if (lane == 0) grec[0] = TD_LAYOUT_MAGIC;
+  }
+  return st;
 }
 
 // TDGymBasic.reset for the boards in reset_mask: the staged layout when there is
@@ -977,33 +1152,34 @@ __global__ __launch_bounds__(64) void td_step_kernel(StepArgs a) {
 // reported in reset_fail and the board is left unchanged, as the reference raises).
 template <int LT>
 __global__ __launch_bounds__(64) void td_reset_kernel(StepArgs a) {
-  constexpr int NC = LT ? LT * LT : MAX_L * MAX_L / 4;
-  __shared__ Smem<NC> S;
+  constexpr int NC = LT ? LT * LT : MAX_KERNEL_L * MAX_KERNEL_L;
+  __shared__ union U_ {
+    Smem<NC> board;
+    LayoutSmem<NC> gen;
+  } sh;
   const int b = blockIdx.x;
   if (b >= a.B) return;
   if (a.reset_mask && !a.reset_mask[b]) return;
   const int L = LT ? LT : a.L;
-  const Ctx x{*a.cfg, L, L * L, (int)threadIdx.x};
-  U u;
-  u.episodes = a.hdr[b].episodes;
-  u.flags = 0;
-  uint32_t* rec = a.nxt + (size_t)b * (LAYOUT_HDR + x.NCr);
+  uint32_t* rec = a.nxt + (size_t)b * (LAYOUT_HDR + L * L);
   if (rec[0] != TD_LAYOUT_MAGIC) {
-    int st = 0;
-    if (x.lane == 0) st = draw_layout(a, b, 0);
-    __threadfence_block();
-    st = __shfl(st, 0);
+    const int st = wave_layout(sh.gen, a, b, 0);
     __syncthreads();
     if (st != ROAD_OK) {
-      if (x.lane == 0) a.reset_fail[b] = (uint8_t)st;
+      if (threadIdx.x == 0) a.reset_fail[b] = (uint8_t)st;
       return;
     }
   }
-  reset_board(S, u, x, rec);
-  for (int i = x.lane; i < 4 * NC; i += 64) (&S.grp[0][0])[i] = 0xFF;
+  Smem<NC>& S = sh.board;
+  stage_cfg(S, a.cfg);
   __syncthreads();
+  const Ctx x{S.cfg, L, L * L, (int)threadIdx.x};
+  U u;
+  u.episodes = a.hdr[b].episodes;
+  u.flags = 0;
+  reset_board(S, u, x, rec);
   channel_scalars(S, u, x);
-  if (a.obs) write_obs(S, x, a.obs + (size_t)b * NCH * x.NCr);
+  if (a.obs) write_obs<NC, LT>(S, x, a.obs + (size_t)b * NCH * x.NCr, false);
   store_board(S, u, x, a, b);
   if (x.lane == 0) {
     a.reset_fail[b] = 0;
@@ -1012,13 +1188,17 @@ __global__ __launch_bounds__(64) void td_reset_kernel(StepArgs a) {
   }
 }
 
-// Stage the next-episode layout of every queued board: one lane per board runs
-// create_road_v2 on the board's numpy stream (serial, latency-bound, rare).
+// Stage the next-episode layout of every queued board: one wave per board
+// (grid-stride over the queue), then clear the queue.  Runs on a side stream,
+// concurrently with later steps (td_capi.hip double-buffers the queue).
+template <int LT>
 __global__ __launch_bounds__(64) void td_refill_kernel(StepArgs a) {
+  constexpr int NC = LT ? LT * LT : MAX_KERNEL_L * MAX_KERNEL_L;
+  __shared__ LayoutSmem<NC> G;
   const uint32_t n = *a.qcount;
-  for (uint32_t i = blockIdx.x * 64u + threadIdx.x; i < n; i += gridDim.x * 64u) {
-    const int b = a.queue[i];
-    draw_layout(a, b, kLayoutRetries);
+  for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+    wave_layout(G, a, a.queue[i], kLayoutRetries);
+    __syncthreads();
   }
 }
 
@@ -1050,8 +1230,18 @@ hipError_t launch_step(const StepArgs& a, hipStream_t s, bool reset) {
   }
 }
 
+template <int LT>
+static void launch_refill2(const StepArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(td_refill_kernel<LT>, dim3(1024), dim3(64), 0, s, a);
+}
+
 hipError_t launch_refill(const StepArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(td_refill_kernel, dim3(64), dim3(64), 0, s, a);
+  switch (a.L) {
+    case 10: launch_refill2<10>(a, s); break;
+    case 20: launch_refill2<20>(a, s); break;
+    case 30: launch_refill2<30>(a, s); break;
+    default: launch_refill2<0>(a, s); break;
+  }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   return hipMemsetAsync(a.qcount, 0, sizeof(uint32_t), s);

@@ -15,6 +15,7 @@ LIB_PATH = os.environ.get("TDSTEP_LIB", os.path.join(os.path.dirname(_HERE), "li
 
 ECAP, TCAP, NCH = 128, 32, 45
 MT_WORDS = 625
+OPP_WORDS = 626
 HDR_BYTES = 96
 
 c_u32p = ctypes.POINTER(ctypes.c_uint32)

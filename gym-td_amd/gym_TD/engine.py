@@ -296,7 +296,7 @@ def _layout(count, L):
     return [("hdr", HDR_DTYPE, ()), ("en_lp", np.float64, (_lib.ECAP,)), ("en_mg", np.float64, (_lib.ECAP,)),
             ("en_inf", np.uint32, (_lib.ECAP,)), ("tw_cd", np.float64, (_lib.TCAP,)),
             ("tw_inf", np.uint32, (_lib.TCAP,)), ("cells", np.uint32, (L * L,)),
-            ("opp_mt", np.uint32, (_lib.MT_WORDS,))]
+            ("opp_mt", np.uint32, (_lib.OPP_WORDS,))]
 
 
 def _decode_state(buf, count, L):

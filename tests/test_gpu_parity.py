@@ -134,6 +134,16 @@ def test_batched_vs_oracle(L, B, steps):
                 assert np.array_equal(ob[b], wo), (L, k, b, np.argwhere(ob[b] != wo)[:5].tolist())
                 assert bool(dn[b]) == wd
         assert (eng.flags() == 0).all()
+        # both RNG streams end where the reference's would (lazy twist completed on export)
+        import random
+        for b in range(0, B, max(1, B // 8)):
+            # the device may have pre-drawn past CPython's block boundary: compare the streams
+            mine, ref = random.Random(), random.Random()
+            mine.setstate((3, tuple(int(v) for v in eng.get_py_state(b)), None))
+            ref.setstate(orc[b].rnd.getstate())
+            assert [mine.getrandbits(32) for _ in range(700)] == [ref.getrandbits(32) for _ in range(700)], (L, b)
+            ns = orc[b].np_random.get_state()
+            assert eng.get_np_state(b).tolist() == list(ns[1]) + [int(ns[2])], (L, b)
     finally:
         eng.close()
 
