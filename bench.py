@@ -103,6 +103,7 @@ def main():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--autoreset", type=int, default=1, help="diagnostic: 0 keeps finished boards stepping (not the metric)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -118,7 +119,7 @@ def main():
 
     B, L, K, W = args.boards, args.map_size, args.steps, args.warmup
     seeds = np.arange(B, dtype=np.int64) + args.seed + rank * B
-    eng = TDEngine(L, B, "def", False, 1, device=dev, np_seeds=seeds, py_seeds=seeds, autoreset=True, info=True)
+    eng = TDEngine(L, B, "def", False, 1, device=dev, np_seeds=seeds, py_seeds=seeds, autoreset=bool(args.autoreset), info=True)
     obs, _ = eng.reset_all()  # failing road draws (the reference raises/hangs) are redrawn
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     n_act = 6 * L * L + 1
@@ -184,7 +185,7 @@ def main():
             "metric": "env-steps/sec (whole node), 10x10 board, batch=65k, at 1/2/4/8 MI355X",
             "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": K, "warmup": W,
             "ms_per_step": elapsed / K * 1e3, "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "f64+f32 (f64 game state, f32 obs)",
+            "vs_baseline": None, "dtype": "f64",
             "data": "synthetic: uniform random defender actions, built-in lv1 opponent, seeded boards",
             "config": {"workload": "TD-def-small-v0 (10x10), %d boards per GPU, auto-reset, burn-in %d steps"
                                    % (B, args.burnin), "global_batch": world * B, "boards_per_gpu": B,

@@ -22,6 +22,8 @@
 #include "td_layout.h"
 #include "td_rng.h"
 
+#include <utility>
+
 namespace td {
 
 #ifdef TD_STAMPS
@@ -47,6 +49,12 @@ __device__ __forceinline__ float f32(double x) { return __double2float_rn(x); }
 __device__ __forceinline__ int ctz64(uint64_t m) { return __builtin_ctzll(m); }
 __device__ __forceinline__ int popc64(uint64_t m) { return __popcll(m); }
 __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+// Lane l's value (l wave-uniform): a scalar broadcast, no LDS traffic.
+__device__ __forceinline__ uint32_t rdl(uint32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ float rdl(float v, int l) { return __int_as_float((int)rdl((uint32_t)__float_as_int(v), l)); }
+__device__ __forceinline__ double rdl(double v, int l) {
+  return __hiloint2double((int)rdl((uint32_t)__double2hiint(v), l), (int)rdl((uint32_t)__double2loint(v), l));
+}
 
 // ---------------------------------------------------------------------------
 // per-board LDS image
@@ -64,17 +72,19 @@ struct alignas(16) Smem {
     float gst[ECAP][4];   // stats .. obs: group stats min, max, avg, count/8 by head enemy
   };
   uint32_t eInf[ECAP];
-  union {
-    double key[ECAP];     // sort keys
-    float eR[ECAP];       // f32(LP / maxLP)
-  };
   double tCd[TCAP];
   uint32_t tInf[TCAP];
-  float chv[48];          // broadcast channel values
-  float d9[64];           // channel 9 by distance (road length < 2L <= 64)
-  int32_t atk[24];        // attacker clusters of this step (TD-atk / TD-2p)
-  int32_t real_atk[24];   // info['RealAction'] of the attacker
-  int32_t fail_atk[4];    // info['FailCode'] of the attacker (-1 = no entry)
+  union {
+    struct {              // actions: the attacker's clusters (TD-atk / TD-2p), written out right after
+      int32_t atk[24];
+      int32_t real_atk[24];  // info['RealAction'] of the attacker
+      int32_t fail_atk[4];   // info['FailCode'] of the attacker (-1 = no entry)
+    };
+    struct {              // observation
+      float chv[48];      // broadcast channel values
+      float d9[64];       // channel 9 by distance (road length < 2L <= 64)
+    };
+  };
   TdDevCfg cfg;           // constant block, staged once per board: per-lane table lookups hit LDS
 };
 
@@ -432,12 +442,10 @@ __device__ double board_step(Smem<NC>& S, U& u, const Ctx& x, const StepArgs& a,
     mg[s] = val[s] ? S.eMg[i] : 0.0;
     inf[s] = val[s] ? S.eInf[i] : 0u;
     key[s] = val[s] ? dsub((double)cw_dist(S.cell[en_cell(inf[s])]), mg[s]) : 0.0;
-    if (val[s]) S.key[i] = key[s];
   }
-  __syncthreads();
   int rank[2] = {0, 0};
-  for (int j = 0; j < n; ++j) {
-    double kj = S.key[j];
+  for (int j = 0; j < n; ++j) {  // enemy j's key from the lane that holds it
+    const double kj = j < 64 ? rdl(key[0], j) : rdl(key[1], j - 64);
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       int i = lane + 64 * s;
@@ -572,7 +580,11 @@ __device__ double board_step(Smem<NC>& S, U& u, const Ctx& x, const StepArgs& a,
   __syncthreads();
   // the enemy list is final for this step: write it back now (its LDS is reused by the stats)
   const size_t eb = (size_t)b * ECAP;
-  for (int i = lane; i < n2; i += 64) { a.en_lp[eb + i] = S.eLP[i]; a.en_mg[eb + i] = S.eMg[i]; a.en_inf[eb + i] = S.eInf[i]; }
+  for (int i = lane; i < n2; i += 64) {
+    a.en_lp[eb + i] = S.eLP[i];
+    a.en_mg[eb + i] = S.eMg[i];
+    a.en_inf[eb + i] = S.eInf[i];
+  }
   return reward;
 }
 
@@ -586,6 +598,7 @@ __device__ void enemy_stats(Smem<NC>& S, const U& u, const Ctx& x) {
   if (n == 0) return;  // write_obs emits zero planes without reading grp
   for (int i = x.lane; i < 4 * NC; i += 64) (&S.grp[0][0])[i] = 0xFF;
   uint32_t key[2];
+  float r[2] = {0.0f, 0.0f};
   bool val[2];
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
@@ -595,16 +608,15 @@ __device__ void enemy_stats(Smem<NC>& S, const U& u, const Ctx& x) {
     if (val[s]) {
       uint32_t e = S.eInf[i];
       key[s] = e & 0x3fffu;  // cell | type << 12
-      S.eR[i] = f32(ddiv(S.eLP[i], C.e_lp[en_type(e)][en_lv(e)]));  // r = LP / maxLP (:358)
+      r[s] = f32(ddiv(S.eLP[i], C.e_lp[en_type(e)][en_lv(e)]));  // r = LP / maxLP (:358)
     }
   }
-  __syncthreads();
   float mn[2] = {1.0f, 1.0f}, mx[2] = {0.0f, 0.0f}, sm[2] = {0.0f, 0.0f};
   int cnt[2] = {0, 0};
   bool head[2] = {val[0], val[1]};
-  for (int j = 0; j < n; ++j) {
-    uint32_t kj = S.eInf[j] & 0x3fffu;
-    float rj = S.eR[j];
+  for (int j = 0; j < n; ++j) {  // enemy j's group key and ratio from the lane that holds it
+    const uint32_t kj = j < 64 ? rdl(key[0], j) : rdl(key[1], j - 64);
+    const float rj = j < 64 ? rdl(r[0], j) : rdl(r[1], j - 64);
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       int i = x.lane + 64 * s;
@@ -634,6 +646,13 @@ __device__ void enemy_stats(Smem<NC>& S, const U& u, const Ctx& x) {
   __syncthreads();
 }
 
+// Channel 9 by distance (per episode): s[9] = map[4] / (max(map[4]) + 1), an
+// int32 scalar divisor promotes to f64, rounded once to f32 (TDBoard.py:121).
+template <int NC>
+__device__ __forceinline__ void d9_table(Smem<NC>& S, int maxdist, int lane) {
+  if (lane <= maxdist) S.d9[lane] = f32(ddiv((double)lane, (double)(maxdist + 1)));
+}
+
 // Broadcast channels and the channel-9 table (TDBoard.py:115-142).
 template <int NC>
 __device__ void channel_scalars(Smem<NC>& S, const U& u, const Ctx& x) {
@@ -649,10 +668,10 @@ __device__ void channel_scalars(Smem<NC>& S, const U& u, const Ctx& x) {
     else if (l >= 41 && l < 45) v = f32(ddiv(ddiv(u.cost_def, C.e_cost[l - 41][0]), (double)C.max_cluster_length));
     S.chv[l] = v;
   }
-  // s[9] = map[4] / (max(map[4]) + 1): int32 scalar divisor promotes to f64, rounded once to f32
-  for (int d = l; d <= u.maxdist && d < 64; d += 64) S.d9[d] = f32(ddiv((double)d, (double)(u.maxdist + 1)));
+  d9_table(S, u.maxdist, l);
   __syncthreads();
 }
+
 
 // Binary observation channels as bits of one word per cell (bit c = channel c):
 // 0-3 roads, 4 end, 6-8 starts, 14 buildable (map[6] == 0), 15-16 tower level,
@@ -667,39 +686,72 @@ __device__ __forceinline__ uint32_t cell_bits(uint32_t w, uint32_t tw) {
 
 __device__ __forceinline__ float bitf(uint32_t m, int ch) { return (float)((m >> ch) & 1u); }
 
-// Channel ch of cells 4q .. 4q+3 (TDBoard.get_states, :112-143).
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// Channel-independent data of cells 4q .. 4q+3, kept in registers while a lane
+// sweeps the channels: the binary-channel bits and the channel-9 values.
+struct QuadData {
+  u32x4 bits;
+  f32x4 d9;
+};
+
 template <int NC>
-__device__ __forceinline__ float4 obs_quad(const Smem<NC>& S, int ch, int q, bool any_enemy) {
-  float4 v;
-  if (ch < 32 && ((kBinaryChannels >> ch) & 1u)) {
-    const uint4 w = *reinterpret_cast<const uint4*>(&S.cell[4 * q]);
-    const uint32_t tw = *reinterpret_cast<const uint32_t*>(&S.twr[4 * q]);
-    v.x = bitf(cell_bits(w.x, tw & 0xffu), ch);
-    v.y = bitf(cell_bits(w.y, (tw >> 8) & 0xffu), ch);
-    v.z = bitf(cell_bits(w.z, (tw >> 16) & 0xffu), ch);
-    v.w = bitf(cell_bits(w.w, tw >> 24), ch);
-  } else if (ch == 9) {
-    const uint4 w = *reinterpret_cast<const uint4*>(&S.cell[4 * q]);
-    v.x = S.d9[cw_dist(w.x)];
-    v.y = S.d9[cw_dist(w.y)];
-    v.z = S.d9[cw_dist(w.z)];
-    v.w = S.d9[cw_dist(w.w)];
-  } else if (ch >= 25 && ch < 41) {
-    const int e = ch - 25, st = e >> 2, t = e & 3;
-    v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    const uint32_t g4 = any_enemy ? *reinterpret_cast<const uint32_t*>(&S.grp[t][4 * q]) : 0xFFFFFFFFu;
-    if (g4 != 0xFFFFFFFFu) {
-      const uint32_t g0 = g4 & 0xffu, g1 = (g4 >> 8) & 0xffu, g2 = (g4 >> 16) & 0xffu, g3 = g4 >> 24;
-      if (g0 != 0xffu) v.x = S.gst[g0][st];
-      if (g1 != 0xffu) v.y = S.gst[g1][st];
-      if (g2 != 0xffu) v.z = S.gst[g2][st];
-      if (g3 != 0xffu) v.w = S.gst[g3][st];
-    }
-  } else {  // 5, 10-13, 21-24, 41-44: one value for the whole plane
+__device__ __forceinline__ QuadData quad_data(const Smem<NC>& S, int q) {
+  QuadData d;
+  const uint4 w = *reinterpret_cast<const uint4*>(&S.cell[4 * q]);
+  const uint32_t tw = *reinterpret_cast<const uint32_t*>(&S.twr[4 * q]);
+  d.bits = u32x4{cell_bits(w.x, tw & 0xffu), cell_bits(w.y, (tw >> 8) & 0xffu),
+                 cell_bits(w.z, (tw >> 16) & 0xffu), cell_bits(w.w, tw >> 24)};
+  d.d9 = f32x4{S.d9[cw_dist(w.x)], S.d9[cw_dist(w.y)], S.d9[cw_dist(w.z)], S.d9[cw_dist(w.w)]};
+  return d;
+}
+
+// Channel kinds of the observation (TDBoard.get_states, :112-143).
+enum ObsKind : int { OK_BIN, OK_CONST, OK_D9, OK_ENEMY, OK_NONE };
+__host__ __device__ constexpr int obs_kind(int ch) {
+  return ch < 0 ? OK_NONE
+       : ch == 9 ? OK_D9
+       : (ch < 32 && ((kBinaryChannels >> ch) & 1u)) ? OK_BIN
+       : (ch >= 25 && ch < 41) ? OK_ENEMY
+       : OK_CONST;
+}
+
+// Channel ch of a lane's quad, for a channel kind K known at compile time (ch may
+// differ between lanes but is always of kind K).
+template <int K, int NC>
+__device__ __forceinline__ f32x4 obs_chan(const Smem<NC>& S, const QuadData& d, int ch, int q, bool any_enemy) {
+  if constexpr (K == OK_BIN) {
+    return __builtin_convertvector((d.bits >> (uint32_t)ch) & 1u, f32x4);
+  } else if constexpr (K == OK_D9) {
+    return d.d9;
+  } else if constexpr (K == OK_CONST) {  // 5, 10-13, 21-24, 41-44: one value for the whole plane
     const float c = S.chv[ch];
-    v = make_float4(c, c, c, c);
+    return f32x4{c, c, c, c};
+  } else {
+    f32x4 v = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    if (any_enemy) {  // wave-uniform
+      const int e = ch - 25, st = e >> 2, t = e & 3;
+      const uint32_t g4 = *reinterpret_cast<const uint32_t*>(&S.grp[t][4 * q]);
+      const uint32_t g0 = g4 & 0xffu, g1 = (g4 >> 8) & 0xffu, g2 = (g4 >> 16) & 0xffu, g3 = g4 >> 24;
+      // branch-free: read a clamped slot, keep it only where the cell has a group
+      const float f0 = S.gst[g0 & (ECAP - 1)][st], f1 = S.gst[g1 & (ECAP - 1)][st];
+      const float f2 = S.gst[g2 & (ECAP - 1)][st], f3 = S.gst[g3 & (ECAP - 1)][st];
+      v = f32x4{g0 != 0xffu ? f0 : 0.0f, g1 != 0xffu ? f1 : 0.0f, g2 != 0xffu ? f2 : 0.0f, g3 != 0xffu ? f3 : 0.0f};
+    }
+    return v;
   }
-  return v;
+}
+
+// Channel ch (runtime) of a lane's quad.
+template <int NC>
+__device__ __forceinline__ f32x4 obs_quad(const Smem<NC>& S, const QuadData& d, int ch, int q, bool any_enemy) {
+  switch (obs_kind(ch)) {
+    case OK_BIN: return obs_chan<OK_BIN>(S, d, ch, q, any_enemy);
+    case OK_D9: return obs_chan<OK_D9>(S, d, ch, q, any_enemy);
+    case OK_ENEMY: return obs_chan<OK_ENEMY>(S, d, ch, q, any_enemy);
+    default: return obs_chan<OK_CONST>(S, d, ch, q, any_enemy);
+  }
 }
 
 template <int NC>
@@ -716,26 +768,57 @@ __device__ __forceinline__ float obs_value(const Smem<NC>& S, int ch, int cell, 
   return S.chv[ch];
 }
 
-// The (45, L, L) float32 observation, 16-byte stores.  When a plane has at most
-// 64 quads (L = 10: 25), each lane keeps one quad and the wave writes
-// floor(64 / quads) adjacent planes per store instruction; otherwise the
-// board's quads are swept in order.
+// Two channels written by one store instruction when a plane has <= 32 quads:
+// lanes of group 0 write channel A, lanes of group 1 channel B.  Pairs are of one
+// kind wherever possible so the wave executes one code path per store.
+template <int CA, int CB, int Q, int NC>
+__device__ __forceinline__ void obs_pair(const Smem<NC>& S, const QuadData& d, f32x4* o4, int q, int g,
+                                         bool any_enemy) {
+  constexpr int KA = obs_kind(CA), KB = obs_kind(CB);
+  f32x4 v;
+  int ch;
+  if constexpr (KB == OK_NONE) {
+    if (g) return;
+    ch = CA;
+    v = obs_chan<KA>(S, d, CA, q, any_enemy);
+  } else if constexpr (KA == KB) {
+    ch = g ? CB : CA;
+    v = obs_chan<KA>(S, d, ch, q, any_enemy);
+  } else {
+    ch = g ? CB : CA;
+    const f32x4 va = obs_chan<KA>(S, d, CA, q, any_enemy), vb = obs_chan<KB>(S, d, CB, q, any_enemy);
+    v = g ? vb : va;
+  }
+  o4[ch * Q + q] = v;
+  __builtin_amdgcn_sched_barrier(0);  // one channel in flight: keeps the VGPR count at the kernel's level
+}
+
+// Observation stores are non-temporal: 1.2 GB per launch written once and never
+// read back by the kernel; as plain stores the dirty lines fill the XCD L2s and
+// every state load behind them waits on a write-back (measured: 16 % slower).
+__device__ __forceinline__ void obs_store(f32x4* p, f32x4 v) { __builtin_nontemporal_store(v, p); }
+
+// The (45, L, L) float32 observation, 16-byte stores.  Lanes own quads (four
+// cells) and keep the channel-independent data in registers.  With at most 32
+// quads per plane (L = 10: 25) floor(64 / quads) lane groups write that many
+// adjacent planes per store instruction, in plane order; otherwise lane l owns
+// quads l, l + 64, ... and each store covers up to 64 quads of one plane.
 template <int NC, int LT>
-__device__ void write_obs(const Smem<NC>& S, const Ctx& x, float* out, bool any_enemy) {
+__device__ __forceinline__ void write_obs(const Smem<NC>& S, const Ctx& x, float* out, bool any_enemy) {
+  f32x4* o4 = reinterpret_cast<f32x4*>(out);
   const int ncr = LT ? LT * LT : x.NCr;
   if ((ncr & 3) == 0) {
     const int Q = ncr / 4;
-    float4* o4 = reinterpret_cast<float4*>(out);
-    if (Q <= 64) {
+    if (Q <= 32) {
       const int G = 64 / Q, q = x.lane % Q, g = x.lane / Q;
       if (g < G) {
-        for (int ch = g; ch < NCH; ch += G) o4[ch * Q + q] = obs_quad(S, ch, q, any_enemy);
+        const QuadData d = quad_data(S, q);
+        for (int ch = g; ch < NCH; ch += G) obs_store(o4 + ch * Q + q, obs_quad(S, d, ch, q, any_enemy));
       }
     } else {
-      const int nq = NCH * Q;
-      for (int i = x.lane; i < nq; i += 64) {
-        const int ch = i / Q;
-        o4[i] = obs_quad(S, ch, i - ch * Q, any_enemy);
+      for (int q = x.lane; q < Q; q += 64) {
+        const QuadData d = quad_data(S, q);
+        for (int ch = 0; ch < NCH; ++ch) obs_store(o4 + ch * Q + q, obs_quad(S, d, ch, q, any_enemy));
       }
     }
   } else {
@@ -750,34 +833,73 @@ __device__ void write_obs(const Smem<NC>& S, const Ctx& x, float* out, bool any_
 // ---------------------------------------------------------------------------
 // board load / reset / store
 // ---------------------------------------------------------------------------
+// The inputs of one board step, all loads issued before any is waited on.
+// Lane l holds enemy slot l (l < PF_EN), tower slot l & 31, cells l and l + 64, and one word
+// of `w`: lanes 0-23 the header, 24-25 the discrete defender action, 26-37 the
+// opponent stream's hot record.
+struct Prefetch {
+  double lp, mg, tcd;
+  uint32_t inf, tinf, c0, c1, w;
+};
+constexpr int PF_ACT = 24, PF_HOT = 26, PF_EN = 16;
+static_assert(offsetof(TdHdr, steps) == 24 && offsetof(TdHdr, start_cell) == 56 && offsetof(TdHdr, episodes) == 76,
+              "Prefetch header word map");
+
+__device__ __forceinline__ void prefetch_issue(Prefetch& P, const StepArgs& a, int b, int lane, int ncr,
+                                               bool want_act) {
+  const size_t eb = (size_t)b * ECAP, tb = (size_t)b * TCAP, cb = (size_t)b * ncr;
+  if (lane < PF_EN) {  // enemy slots beyond PF_EN (rare) load after the header
+    P.lp = a.en_lp[eb + lane];
+    P.mg = a.en_mg[eb + lane];
+    P.inf = a.en_inf[eb + lane];
+  }
+  P.tcd = a.tw_cd[tb + (lane & (TCAP - 1))];
+  P.tinf = a.tw_inf[tb + (lane & (TCAP - 1))];
+  P.c0 = lane < ncr ? a.cells[cb + lane] : 0u;
+  P.c1 = lane + 64 < ncr ? a.cells[cb + lane + 64] : 0u;
+  const uint32_t* src;
+  if (lane < PF_ACT) src = reinterpret_cast<const uint32_t*>(a.hdr + b) + lane;
+  else if (lane < PF_HOT) src = want_act ? reinterpret_cast<const uint32_t*>(a.def_act + b) + (lane - PF_ACT) : nullptr;
+  else if (lane < PF_HOT + HOT_WORDS) src = a.opp_hot + (size_t)b * HOT_WORDS + (lane - PF_HOT);
+  else src = nullptr;
+  P.w = src ? *src : 0u;
+}
+
+__device__ __forceinline__ uint32_t lane_word(uint32_t v, int l) { return rdl(v, l); }
+// The f64 whose low / high words are held by lanes l / l + 1.
+__device__ __forceinline__ double lane_f64(uint32_t v, int l) {
+  return __hiloint2double((int)lane_word(v, l + 1), (int)lane_word(v, l));
+}
+
+// Commit the prefetched inputs of board b into the LDS image and the scalar state.
 template <int NC>
-__device__ void load_board(Smem<NC>& S, U& u, const Ctx& x, const StepArgs& a, int b) {
-  // Issue every load of the board before waiting on any: the first 64 enemy
-  // slots and all tower slots are fetched speculatively alongside the header
-  // (one memory round trip instead of header -> lists).
-  const size_t eb = (size_t)b * ECAP, tb = (size_t)b * TCAP, cb = (size_t)b * x.NCr;
-  const double lp0 = a.en_lp[eb + x.lane], mg0 = a.en_mg[eb + x.lane];
-  const uint32_t in0 = a.en_inf[eb + x.lane];
-  const double tcd0 = a.tw_cd[tb + (x.lane & (TCAP - 1))];
-  const uint32_t tin0 = a.tw_inf[tb + (x.lane & (TCAP - 1))];
-  for (int i = x.lane; i < x.NCr; i += 64) { S.cell[i] = a.cells[cb + i]; S.twr[i] = 0; }
-  const TdHdr& h = a.hdr[b];
-  u.cost_def = h.cost_def; u.cost_atk = h.cost_atk; u.ep_ret = h.ep_return;
-  u.steps = h.steps; u.base_LP = h.base_LP; u.atk_cd = h.atk_cd; u.def_cd = h.def_cd;
-  u.n = h.n_en; u.nt = h.n_tw; u.num_roads = h.num_roads; u.end_cell = h.end_cell;
-  u.set_starts(h.start_cell[0], h.start_cell[1], h.start_cell[2]);
-  u.maxdist = h.maxdist; u.flags = h.flags; u.episodes = h.episodes;
+__device__ void load_board(Smem<NC>& S, U& u, const Ctx& x, const StepArgs& a, int b, const Prefetch& P) {
+  const size_t eb = (size_t)b * ECAP, cb = (size_t)b * x.NCr;
+  if (x.lane < x.NCr) S.cell[x.lane] = P.c0;
+  if (x.lane + 64 < x.NCr) S.cell[x.lane + 64] = P.c1;
+  for (int i = 128 + x.lane; i < x.NCr; i += 64) S.cell[i] = a.cells[cb + i];
+  for (int i = x.lane; i < x.NCr; i += 64) S.twr[i] = 0;
+  // TdHdr words (td_common.h): 0-5 cost_def, cost_atk, ep_return; 6 steps, 7 base_LP,
+  // 8 atk_cd, 9 def_cd, 10 n_en, 11 n_tw, 12 num_roads, 13 end_cell, 14-16 start_cell,
+  // 17 maxdist, 18 flags, 19 episodes
+  u.cost_def = lane_f64(P.w, 0); u.cost_atk = lane_f64(P.w, 2); u.ep_ret = lane_f64(P.w, 4);
+  u.steps = (int)lane_word(P.w, 6); u.base_LP = (int)lane_word(P.w, 7);
+  u.atk_cd = (int)lane_word(P.w, 8); u.def_cd = (int)lane_word(P.w, 9);
+  u.n = (int)lane_word(P.w, 10); u.nt = (int)lane_word(P.w, 11);
+  u.num_roads = (int)lane_word(P.w, 12); u.end_cell = (int)lane_word(P.w, 13);
+  u.set_starts((int)lane_word(P.w, 14), (int)lane_word(P.w, 15), (int)lane_word(P.w, 16));
+  u.maxdist = (int)lane_word(P.w, 17); u.flags = (int)lane_word(P.w, 18); u.episodes = (int)lane_word(P.w, 19);
   u.progress = ddiv((double)u.steps, (double)x.C.max_episode_steps);
   u.cells_dirty = false;
-  if (x.lane < u.n) { S.eLP[x.lane] = lp0; S.eMg[x.lane] = mg0; S.eInf[x.lane] = in0; }
-  for (int i = 64 + x.lane; i < u.n; i += 64) { S.eLP[i] = a.en_lp[eb + i]; S.eMg[i] = a.en_mg[eb + i]; S.eInf[i] = a.en_inf[eb + i]; }
+  if (x.lane < u.n && x.lane < PF_EN) { S.eLP[x.lane] = P.lp; S.eMg[x.lane] = P.mg; S.eInf[x.lane] = P.inf; }
+  for (int i = PF_EN + x.lane; i < u.n; i += 64) { S.eLP[i] = a.en_lp[eb + i]; S.eMg[i] = a.en_mg[eb + i]; S.eInf[i] = a.en_inf[eb + i]; }
   if (x.lane < u.nt) {
-    S.tCd[x.lane] = tcd0;
-    S.tInf[x.lane] = tin0;
+    S.tCd[x.lane] = P.tcd;
+    S.tInf[x.lane] = P.tinf;
   }
   __syncthreads();
   if (x.lane < u.nt)
-    S.twr[tin0 & 0xfffu] = (uint8_t)(0x80u | (((tin0 >> 14) & 1u) << 2) | ((tin0 >> 12) & 3u));
+    S.twr[P.tinf & 0xfffu] = (uint8_t)(0x80u | (((P.tinf >> 14) & 1u) << 2) | ((P.tinf >> 12) & 3u));
   __syncthreads();
 }
 
@@ -971,13 +1093,20 @@ __device__ void attacker_actions(Smem<NC>& S, U& u, const Ctx& x, const StepArgs
 
 
 template <int NC, int LT, int MODE>
-__device__ void step_board(Smem<NC>& S, const StepArgs& a, int b, int L) {
-  stage_cfg(S, a.cfg);
-  const Ctx x{S.cfg, L, L * L, (int)threadIdx.x};
+__device__ void step_board(Smem<NC>& S, const Ctx& x, const StepArgs& a, int b, const Prefetch& P) {
   const TdDevCfg& C = x.C;
+  uint32_t* const opp = a.opp_mt + (size_t)b * OPP_WORDS;
+  uint32_t* const hot = a.opp_hot + (size_t)b * HOT_WORDS;
   U u;
   STAMP(0);
-  load_board(S, u, x, a, b);
+  load_board(S, u, x, a, b, P);
+  const int64_t act_in = (int64_t)(((uint64_t)lane_word(P.w, PF_ACT + 1) << 32) | lane_word(P.w, PF_ACT));
+  // built-in opponent stream: position, lazy-twist boundary and the next draws
+  // (pre-computed by the previous step) come from the board's hot record
+  WaveMt R{opp, lane_word(P.w, PF_HOT + 0), lane_word(P.w, PF_HOT + 1)};
+  R.cn = lane_word(P.w, PF_HOT + 2);
+  R.cbase = R.pos;
+  R.cache = __shfl(P.w, PF_HOT + 4 + (x.lane & 7));
   STAMP(1);
   if (u.num_roads < 1 || u.num_roads > 3) {
     // never reset (its road generation failed): nothing to step
@@ -992,14 +1121,7 @@ __device__ void step_board(Smem<NC>& S, const StepArgs& a, int b, int L) {
     }
     return;
   }
-  // built-in opponent stream: position, lazy-twist boundary and the next draws
-  // (pre-computed by the previous step) come from the board's hot record
-  uint32_t* const opp = a.opp_mt + (size_t)b * OPP_WORDS;
-  uint32_t* const hot = a.opp_hot + (size_t)b * HOT_WORDS;
-  WaveMt R{opp, hot[0], hot[1]};
-  R.cn = hot[2];
-  R.cbase = R.pos;
-  R.cache = x.lane < 8 ? hot[4 + x.lane] : 0u;
+  float* const obs = a.obs + (size_t)b * NCH * x.NCr;
 
   u.atk_cd = u.atk_cd - 1 > 0 ? u.atk_cd - 1 : 0;
   u.def_cd = u.def_cd - 1 > 0 ? u.def_cd - 1 : 0;
@@ -1013,11 +1135,13 @@ __device__ void step_board(Smem<NC>& S, const StepArgs& a, int b, int L) {
       defender_scan(S, u, x, a.def_act + (size_t)b * 6 * x.NCr,
                     a.real_def ? a.real_def + (size_t)b * 6 * x.NCr : nullptr, u.def_cd == 0);
     } else {
-      int64_t act = a.def_act[b];
+      int64_t act = act_in;
       if (act < 0 || act > empty_def) { u.flags |= FLAG_BAD_ACTION; act = empty_def; }
       if (u.def_cd == 0 && act != empty_def) {
-        const int op = (int)(act / x.NCr), r = (int)((act / L) % L), c = (int)(act % L);
-        fail_def = defender_op(S, u, x, op, r * L + c);
+        // op = act // L^2, row = (act // L) % L, column = act % L (TDDefense.py:65-67)
+        const int a32 = (int)act, ncr = LT ? LT * LT : x.NCr;
+        const int op = a32 / ncr;
+        fail_def = defender_op(S, u, x, op, a32 - op * ncr);
         if (fail_def == FC_OK) { u.def_cd = C.def_interval; real_def = act; }
       }
     }
@@ -1027,6 +1151,9 @@ __device__ void step_board(Smem<NC>& S, const StepArgs& a, int b, int L) {
     opponent_enemy(S, u, x, R, a.difficulty);
   } else {
     attacker_actions<NC, MODE>(S, u, x, a, b);
+    // info of the attacker now: its LDS arrays share space with the observation tables
+    if (a.fail_atk && x.lane < 3) a.fail_atk[(size_t)b * 3 + x.lane] = S.fail_atk[x.lane];
+    if (a.real_atk && x.lane < 24) a.real_atk[(size_t)b * 24 + x.lane] = S.real_atk[x.lane];
     if (MODE == MODE_ATK) opponent_tower(S, u, x, R, a.difficulty);
   }
   // pre-draw the next step's words: loads issued now, consumed at the end of the step
@@ -1055,6 +1182,8 @@ __device__ void step_board(Smem<NC>& S, const StepArgs& a, int b, int L) {
     if (rec[0] == TD_LAYOUT_MAGIC) {
       reset_board(S, u, x, rec);
       was_reset = true;
+      // the new episode's static / tower planes replace the ones written above:
+      // drain those stores first so the rewrite lands after them
     } else {
       u.flags |= FLAG_NO_LAYOUT;  // refill fell behind: the board keeps stepping its finished episode
     }
@@ -1063,7 +1192,7 @@ __device__ void step_board(Smem<NC>& S, const StepArgs& a, int b, int L) {
   enemy_stats(S, u, x);  // no-op for a board without enemies (e.g. just reset)
   channel_scalars(S, u, x);
   STAMP(6);
-  write_obs<NC, LT>(S, x, a.obs + (size_t)b * NCH * x.NCr, u.n > 0);
+  write_obs<NC, LT>(S, x, obs, u.n > 0);
   STAMP(7);
   store_board(S, u, x, a, b);
 
@@ -1086,20 +1215,24 @@ __device__ void step_board(Smem<NC>& S, const StepArgs& a, int b, int L) {
     if (a.ep_len) a.ep_len[b] = ep_steps;
   }
   if (MODE != MODE_2P && x.lane < 8) hot[4 + x.lane] = R.cache;
-  if (MODE != MODE_DEF) {
-    if (a.fail_atk && x.lane < 3) a.fail_atk[(size_t)b * 3 + x.lane] = S.fail_atk[x.lane];
-    if (a.real_atk && x.lane < 24) a.real_atk[(size_t)b * 24 + x.lane] = S.real_atk[x.lane];
-  }
   STAMP(8);
 }
 
+// One workgroup (one wave) per board.  (A persistent variant that prefetched the
+// next board while stepping the current one measured slower: its static board
+// assignment leaves a one-board tail, and the step is bound by HBM writes.)
 template <int LT, int MODE>
 __global__ __launch_bounds__(64) void td_step_kernel(StepArgs a) {
   constexpr int NC = LT ? LT * LT : MAX_KERNEL_L * MAX_KERNEL_L;
   __shared__ Smem<NC> S;
   const int b = blockIdx.x;
   if (b >= a.B) return;
-  step_board<NC, LT, MODE>(S, a, b, LT ? LT : a.L);
+  stage_cfg(S, a.cfg);
+  const int L = LT ? LT : a.L;
+  const Ctx x{S.cfg, L, L * L, (int)threadIdx.x};
+  Prefetch P;
+  prefetch_issue(P, a, b, x.lane, x.NCr, MODE != MODE_ATK && !a.multi);
+  step_board<NC, LT, MODE>(S, x, a, b, P);
 }
 
 // ---------------------------------------------------------------------------

@@ -120,8 +120,9 @@ int td_set_np_state(td_handle* h, int board, const uint32_t* mt625);
 int td_get_np_state(td_handle* h, int board, uint32_t* mt625);
 
 /* Start a new episode on every board with host_mask[b] != 0 (NULL = all): draws
- * the layout from the board's numpy stream (host), resets the board on the device
- * and writes its initial observation into obs (device, may be NULL).  Synchronous.
+ * the layout from the board's numpy stream (on the device; with auto-reset on, a
+ * layout staged ahead of time by the refill kernel is used), resets the board and
+ * writes its initial observation into obs (device, may be NULL).  Synchronous.
  * Returns the number of boards whose road generation failed (the reference raises
  * or hangs there, TDRoadGen.py:177-189); those boards keep their previous state. */
 int td_reset(td_handle* h, const uint8_t* host_mask, float* obs, void* stream);
@@ -145,7 +146,8 @@ int td_layout_generate(uint32_t* np_state625, int map_size, int max_attempts, ui
 /* Board state, array-major for boards [b0, b0+count):
  *   hdr[count] (96 B each: see td_common.h TdHdr), en_lp f64[count][128], en_mg f64[count][128],
  *   en_inf u32[count][128], tw_cd f64[count][32], tw_inf u32[count][32], cells u32[count][L*L],
- *   opp_mt u32[count][625].  Synchronous. */
+ *   opp_mt u32[count][626] (the opponent's CPython stream: 624 words, position, and the
+ *   lazy-twist boundary -- words [w[625], 624) still hold the previous block).  Synchronous. */
 size_t td_state_bytes(td_handle* h, int count);
 int td_export_state(td_handle* h, int b0, int count, void* host_dst);
 int td_import_state(td_handle* h, int b0, int count, const void* host_src);
