@@ -116,9 +116,10 @@ def main():
     torch.cuda.set_device(dev)
 
     from gym_TD.engine import TDEngine
+    from gym_TD import shard
 
     B, L, K, W = args.boards, args.map_size, args.steps, args.warmup
-    seeds = np.arange(B, dtype=np.int64) + args.seed + rank * B
+    seeds = shard.shard_seeds(args.seed, rank, B)
     eng = TDEngine(L, B, "def", False, 1, device=dev, np_seeds=seeds, py_seeds=seeds, autoreset=bool(args.autoreset), info=True)
     obs, _ = eng.reset_all()  # failing road draws (the reference raises/hangs) are redrawn
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
@@ -133,8 +134,7 @@ def main():
     del burn, warm
     stream = torch.cuda.current_stream(dev)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
-    ep_done = torch.zeros((), dtype=torch.int64, device=dev)
-    ep_ret = torch.zeros((), dtype=torch.float64, device=dev)
+    eng.episode_stats(clear=True)  # the device accumulates finished episodes of the timed steps
 
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -153,17 +153,11 @@ def main():
 
     kern_ms = [s.elapsed_time(e) for s, e in ev]
     avg_kernel_s = float(np.mean(kern_ms)) / 1e3
-    # episode stats of the last step (gathered after timing: the one collective of the data path)
-    d = eng.done.to(torch.bool)
-    ep_done += d.sum()
-    ep_ret += torch.where(d, eng.ep_return, torch.zeros_like(eng.ep_return)).sum()
+    # after timing: MAX of the clocks over ranks, and the episode statistics of the
+    # timed steps gathered to rank 0 (the only exchange; RCCL on GPUs)
     flags = eng.flags()
-    t = torch.tensor([elapsed, avg_kernel_s], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        stats = torch.stack([ep_done.double(), ep_ret])
-        gathered = [torch.zeros_like(stats) for _ in range(world)] if rank == 0 else None
-        dist.gather(stats, gathered, dst=0)
+    t = shard.max_over_ranks(torch.tensor([elapsed, avg_kernel_s], dtype=torch.float64, device=dev))
+    per_rank = shard.gather_stats(eng.episode_stats(clear=True))
     elapsed, avg_kernel_s = float(t[0]), float(t[1])
 
     if rank == 0:
@@ -195,6 +189,9 @@ def main():
                          "kernel": "td_step_kernel<10>", "avg_kernel_us": avg_kernel_s * 1e6,
                          "algorithmic_bytes_per_launch": B * bpe},
             "board_flags_nonzero": int((flags != 0).sum()),
+            "episodes": {"finished": int(per_rank[:, 0].sum()),
+                         "mean_return": float(per_rank[:, 1].sum() / max(float(per_rank[:, 0].sum()), 1.0)),
+                         "per_rank": [int(v) for v in per_rank[:, 0].tolist()]},
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(L, args.cpu_seconds, host_cores())

@@ -62,6 +62,7 @@ struct td_handle {
   uint8_t *d_scratch = nullptr, *d_mask = nullptr, *d_fail = nullptr;
   int stage_cap = 0;
   uint64_t* d_stamps = nullptr;  // TD_STAMPS diagnostic builds only (not owned)
+  double* d_epstats = nullptr;   // [2] finished episodes, sum of their returns
   // Layout refill runs on a side stream: step kernels append to queue[cur]; a
   // refill takes the current buffer and steps switch to the other one.
   hipStream_t side = nullptr;
@@ -308,6 +309,7 @@ td_handle* td_create(const td_config* cfg, int map_size, int n_boards, int mode,
   rc |= dalloc(&h->d_fail, B);
   rc |= dalloc(&h->d_stage, (size_t)h->stage_cap * h->lw);
   rc |= dalloc(&h->d_stage_ids, (size_t)h->stage_cap);
+  rc |= dalloc(&h->d_epstats, 2);
   if (!rc && hipMemcpy(h->d_cfg, &h->dcfg, sizeof(TdDevCfg), hipMemcpyHostToDevice) != hipSuccess) rc = fail("cfg upload");
   if (!rc && hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking) != hipSuccess) rc = fail("side stream");
   if (!rc && hipEventCreateWithFlags(&h->ev_main, hipEventDisableTiming) != hipSuccess) rc = fail("event");
@@ -326,7 +328,7 @@ void td_destroy(td_handle* h) {
   (void)hipDeviceSynchronize();
   void* dptrs[] = {h->d_cfg, h->d_hdr, h->d_en_lp, h->d_en_mg, h->d_en_inf, h->d_tw_cd, h->d_tw_inf,
                    h->d_cells, h->d_opp, h->d_hot, h->d_np, h->d_nxt, h->d_scratch, h->d_queue, h->d_qcount,
-                   h->d_mask, h->d_fail, h->d_stage, h->d_stage_ids};
+                   h->d_mask, h->d_fail, h->d_stage, h->d_stage_ids, h->d_epstats};
   for (void* p : dptrs)
     if (p) (void)hipFree(p);
   if (h->ev_main) (void)hipEventDestroy(h->ev_main);
@@ -480,9 +482,18 @@ int td_step(td_handle* h, const td_step_io* io, void* stream) {
   a.real_def = io->real_def; a.real_atk = io->real_atk; a.fail_def = io->fail_def; a.fail_atk = io->fail_atk;
   a.win = io->win; a.allow_next = io->allow_next; a.ep_return = io->ep_return; a.ep_len = io->ep_len;
   a.stamps = h->d_stamps;
+  a.ep_stats = h->d_epstats;
   HIP_OK(launch_step(a, s, false));
   h->steps += 1;
   if (h->autoreset && (h->steps % kRefillEvery) == 0 && start_refill(h, s)) return -1;
+  return 0;
+}
+
+int td_episode_stats(td_handle* h, double* dev_out, int clear, void* stream) {
+  if (!h || !dev_out) return fail("td_episode_stats: NULL argument");
+  hipStream_t s = (hipStream_t)stream;
+  HIP_OK(hipMemcpyAsync(dev_out, h->d_epstats, 2 * sizeof(double), hipMemcpyDeviceToDevice, s));
+  if (clear) HIP_OK(hipMemsetAsync(h->d_epstats, 0, 2 * sizeof(double), s));
   return 0;
 }
 

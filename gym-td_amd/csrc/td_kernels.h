@@ -44,6 +44,7 @@ struct StepArgs {
   uint8_t* allow_next;
   double* ep_return;
   int32_t* ep_len;
+  double* ep_stats;  // [2]: finished episodes, sum of their returns (accumulated by the step kernel)
   const uint8_t* reset_mask;  // reset kernel only (nullptr = all boards)
 };
 

@@ -1213,6 +1213,10 @@ __device__ void step_board(Smem<NC>& S, const Ctx& x, const StepArgs& a, int b, 
     if (a.real_def && !a.multi) a.real_def[b] = real_def;
     if (a.ep_return) a.ep_return[b] = ep_ret;
     if (a.ep_len) a.ep_len[b] = ep_steps;
+    if (done && a.ep_stats) {  // device-side episode accounting (SURVEY §8(b) td_episode_stats)
+      atomicAdd(&a.ep_stats[0], 1.0);
+      atomicAdd(&a.ep_stats[1], ep_ret);
+    }
   }
   if (MODE != MODE_2P && x.lane < 8) hot[4 + x.lane] = R.cache;
   STAMP(8);

@@ -227,6 +227,13 @@ class TDEngine(object):
         torch.cuda.synchronize(self.device)
         _lib.check(_lib.lib.td_import_state(self._h, b0, count, buf.ctypes.data))
 
+    def episode_stats(self, clear=False):
+        """Device f64 [2]: episodes finished since the last clear and the sum of their returns."""
+        out = torch.empty(2, dtype=torch.float64, device=self.device)
+        _lib.check(_lib.lib.td_episode_stats(self._h, _lib.ctypes.c_void_p(out.data_ptr()), int(bool(clear)),
+                                             self._stream()))
+        return out
+
     def flags(self):
         f = np.zeros(self.B, dtype=np.int32)
         _lib.check(_lib.lib.td_get_flags(self._h, _lib.ptr(f, _lib.ctypes.c_int32)))

@@ -1,0 +1,48 @@
+"""Board sharding over ranks (one process per GPU) and the episode-stats gather.
+
+Boards are independent: rank r of a world of size W steps the
+contiguous block [r * B, (r + 1) * B) of the global batch, and board i's seeds are
+``base + i`` for its global index i, so a board's trajectory is the same whatever
+the number of GPUs.  Nothing is exchanged on the data path; the only collectives
+are the timing MAX and the gather of per-rank episode statistics, which run over
+RCCL (``nccl`` backend) on GPUs and over gloo in the CPU tests.
+"""
+import numpy as np
+import torch
+import torch.distributed as dist
+
+
+def shard_range(rank, boards_per_rank):
+    """Global board indices [lo, hi) owned by ``rank``."""
+    return rank * boards_per_rank, (rank + 1) * boards_per_rank
+
+
+def shard_seeds(base, rank, boards_per_rank):
+    """Seeds of the rank's boards: ``base`` + global board index."""
+    lo, hi = shard_range(rank, boards_per_rank)
+    return np.arange(lo, hi, dtype=np.int64) + int(base)
+
+
+def episode_stats(done, ep_return):
+    """(finished episodes, sum of their returns) of one step's outputs, as f64 [2]."""
+    d = done.to(torch.bool)
+    n = d.sum().to(torch.float64)
+    s = torch.where(d, ep_return.to(torch.float64), torch.zeros((), dtype=torch.float64, device=ep_return.device)).sum()
+    return torch.stack([n, s])
+
+
+def max_over_ranks(t):
+    """In-place MAX over ranks (no-op without a process group)."""
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return t
+
+
+def gather_stats(stats, dst=0):
+    """Gather every rank's stats tensor on ``dst``; returns [W, ...] there, None elsewhere."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return stats.unsqueeze(0)
+    rank, world = dist.get_rank(), dist.get_world_size()
+    out = [torch.zeros_like(stats) for _ in range(world)] if rank == dst else None
+    dist.gather(stats, out, dst=dst)
+    return torch.stack(out) if rank == dst else None

@@ -136,6 +136,13 @@ int td_reset_layouts(td_handle* h, const uint32_t* recs, const int32_t* boards, 
 /* One env step for all boards (asynchronous on `stream`). */
 int td_step(td_handle* h, const td_step_io* io, void* stream);
 
+/* Episodes finished by td_step since the last clear (SURVEY.md §8(b) td_episode_stats):
+ * dev_out[0] = count, dev_out[1] = sum of their returns (f64, device memory, asynchronous
+ * on `stream`; the sum is accumulated with atomics, so its rounding order is unspecified).
+ * clear != 0 zeroes the accumulators after the copy.  The per-rank values are what the
+ * multi-GPU driver gathers over RCCL. */
+int td_episode_stats(td_handle* h, double* dev_out, int clear, void* stream);
+
 /* Layout records. */
 int td_layout_words(int map_size);
 int td_layout_from_roads(int map_size, int num_roads, const int32_t* cells, const int32_t* offsets, uint32_t* rec);

@@ -163,7 +163,8 @@ def test_autoreset_matches_explicit_reset():
         orc = [O.Env(L, O.MODE_DEF, 1, s, s, cfg, O.Hyper(), road_attempts=20000) for s in seeds]
         rets = [0.0] * B
         rng = np.random.RandomState(3)
-        finished = 0
+        finished, finished_sum = 0, 0.0
+        ea.episode_stats(clear=True)
         for k in range(400):
             acts = rng.randint(0, 6 * L * L + 1, size=B).astype(np.int64)
             ea.step(def_act=torch.from_numpy(acts))
@@ -178,6 +179,7 @@ def test_autoreset_matches_explicit_reset():
                 if d:
                     assert canon.fhex(ea.ep_return[b].item()) == canon.fhex(rets[b])
                     assert ea.ep_len[b].item() == orc[b]._board.steps
+                    finished_sum += rets[b]
                     rets[b] = 0.0
                     orc[b].reset()
                     finished += 1
@@ -187,6 +189,10 @@ def test_autoreset_matches_explicit_reset():
             else:
                 assert torch.equal(ea.obs, eb.obs)
         assert finished > 0
+        # device-side episode accounting (td_episode_stats): count exact, f64 sum up to order
+        st = ea.episode_stats().cpu().numpy()
+        assert st[0] == finished
+        assert st[1] == pytest.approx(finished_sum, rel=1e-12, abs=1e-9)
     finally:
         ea.close()
         eb.close()

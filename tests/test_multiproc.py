@@ -1,0 +1,99 @@
+"""The N > 1 path on CPU (gloo, world size 2): board sharding and the episode-stats
+gather that bench.py runs over RCCL on GPUs.
+
+Each rank steps its own contiguous block of boards (here with the oracle, the
+same per-board algorithm the HIP path is checked against), accumulates the
+finished episodes with ``gym_TD.shard.episode_stats`` and gathers them to rank 0;
+rank 0 checks the totals against one process stepping every board.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as tmp
+
+from gym_TD import shard
+from oracle import td_oracle as O
+
+L, BOARDS_PER_RANK, STEPS = 10, 3, 80  # seeds 2000..2005: every first layout draw succeeds
+
+
+def _run_boards(seeds):
+    """Oracle TD-def boards with 1-LP bases (short episodes): per-step done / ep_return arrays."""
+    cfg = O.Config(base_LP=1)
+    envs = [O.Env(L, O.MODE_DEF, 1, int(s), int(s), cfg, O.Hyper(), road_attempts=20000) for s in seeds]
+    rngs = [np.random.RandomState(int(s) + 1) for s in seeds]  # board-owned action streams
+    ret = np.zeros(len(envs))
+    out = []
+    for _ in range(STEPS):
+        acts = [r.randint(0, 6 * L * L + 1) for r in rngs]
+        done = np.zeros(len(envs), bool)
+        ep = np.zeros(len(envs))
+        for i, (e, a) in enumerate(zip(envs, acts)):
+            _, r, d, _ = e.step(int(a))
+            ret[i] += r
+            if d:
+                done[i], ep[i] = True, ret[i]
+                ret[i] = 0.0
+                e.reset()
+        out.append((done, ep))
+    return out
+
+
+def _stats(trace):
+    tot = torch.zeros(2, dtype=torch.float64)
+    for done, ep in trace:
+        tot += shard.episode_stats(torch.from_numpy(done), torch.from_numpy(ep))
+    return tot
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        seeds = shard.shard_seeds(2000, rank, BOARDS_PER_RANK)
+        stats = _stats(_run_boards(seeds))
+        t = shard.max_over_ranks(torch.tensor([float(rank + 1)], dtype=torch.float64))
+        got = shard.gather_stats(stats)
+        if rank == 0:
+            q.put((got.numpy().tolist(), float(t[0])))
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_shard_partition():
+    for world in (1, 2, 4, 8):
+        blocks = [shard.shard_seeds(5, r, 16) for r in range(world)]
+        assert np.array_equal(np.concatenate(blocks), np.arange(5, 5 + 16 * world))
+        assert shard.shard_range(world - 1, 16) == (16 * (world - 1), 16 * world)
+
+
+def test_gloo_two_ranks_match_one_process():
+    world = 2
+    ctx = tmp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        per_rank, tmax = q.get(timeout=300)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    assert tmax == float(world)
+    one = _stats(_run_boards(shard.shard_seeds(2000, 0, world * BOARDS_PER_RANK)))
+    per_rank = np.asarray(per_rank)
+    assert per_rank.shape == (world, 2)
+    assert per_rank[:, 0].sum() == float(one[0]) > 0
+    assert per_rank[:, 1].sum() == pytest.approx(float(one[1]), rel=1e-12, abs=1e-9)
