@@ -7,9 +7,19 @@
 Workload (BASELINE.json configs[1]/[3] shape, per GPU): TD-def-small (10x10),
 ``--boards`` boards per GPU (default 65,536 = the metric's batch), built-in lv1
 opponent, uniform random defender actions over [0, 601) drawn on the device
-before the timed region, auto-reset on.  Boards are seeded base + global index
+before the timed region, auto-reset on.  ``--workload`` selects the other
+SURVEY.md 8(d) shapes for their own measurement lines (not the metric):
+``2p-middle-multi`` (16,384 x TD-2p 20x20, multi-action defender flags uniform in
+{0,1,2}, attacker clusters uniform in {0..4}) and ``def-large`` (16,384 x TD-def
+30x30, the per-GPU share of configs[4]).  Boards are seeded base + global index
 (trajectories do not depend on the GPU count) and burned in ``--burnin`` steps
-(half an episode) untimed, so the timed steps see mid-episode tower counts.
+untimed.  The burn-in staggers the episodes: at burn-in step k the boards whose
+global index is k modulo the episode limit (1,200 steps) are reset explicitly, so
+after a full burn-in the boards' episode phases are spread uniformly and the
+timed steps see the steady state of a long rollout -- about B / 1,200 auto-resets
+(layout draws included) per step and every tower count of an episode -- instead
+of the synchronised start of a fresh batch, where every board would reset in
+the same step.
 Scaling is weak: every rank owns its own boards; the only collective is the
 timing all-reduce and the episode-stat gather after the timed region.
 
@@ -35,6 +45,21 @@ import torch.distributed as dist  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 
 
+# name -> (map size, mode, multi-action, default boards per GPU, metric)
+WORKLOADS = {
+    "def-small": (10, "def", False, 65536, "env-steps/sec (whole node), 10x10 board, batch=65k, at 1/2/4/8 MI355X"),
+    "2p-middle-multi": (20, "2p", True, 16384, "env-steps/sec (whole node), TD-2p-middle 20x20 multi-action, "
+                                                "16k boards per GPU"),
+    "def-large": (30, "def", False, 16384, "env-steps/sec (whole node), TD-def-large 30x30, 16k boards per GPU"),
+}
+ENV_ID = {"def-small": "TD-def-small-v0", "2p-middle-multi": "TD-2p-middle-v0 (allow_multiple_actions)",
+          "def-large": "TD-def-large-v0"}
+DATA = {("def", False): "synthetic: uniform random defender actions, built-in lv1 opponent, seeded boards",
+        ("2p", True): "synthetic: defender flags uniform in {0,1,2} (6,L,L), attacker clusters uniform in {0..4} (3,8), "
+                      "seeded boards"}
+N_ACTION_BUFS = 8  # distinct pre-drawn action batches cycled through the timed steps (multi-action shapes)
+
+
 def algorithmic_bytes(L, mode="def", multi=False):
     """obs f32 (45 L L) + action int64 + reward f64 + done u8 per env-step."""
     obs = 45 * L * L * 4
@@ -45,15 +70,16 @@ def algorithmic_bytes(L, mode="def", multi=False):
 
 # --------------------------------------------------------------------------- CPU baseline
 def _cpu_worker(args):
-    L, seconds, seed = args
+    L, mode, multi, seconds, seed = args
     from oracle import td_oracle as O
     import warnings
     warnings.simplefilter("ignore")
     rng = np.random.RandomState(seed)
     s = seed
+    omode = {"def": O.MODE_DEF, "atk": O.MODE_ATK, "2p": O.MODE_2P}[mode]
     while True:
         try:
-            env = O.Env(L, O.MODE_DEF, 1, s, s, road_attempts=20000)
+            env = O.Env(L, omode, 1, s, s, O.Config(), O.Hyper(allow_multiple_actions=multi), road_attempts=20000)
             break
         except O.RoadGenError:
             s += 100003
@@ -61,7 +87,12 @@ def _cpu_worker(args):
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < seconds:
         for _ in range(50):
-            _, _, d, _ = env.step(int(rng.randint(0, 6 * L * L + 1)))
+            da = aa = None
+            if mode != "atk":
+                da = rng.randint(0, 3, size=(6, L, L)) if multi else int(rng.randint(0, 6 * L * L + 1))
+            if mode != "def":
+                aa = rng.randint(0, 5, size=(3, 8))
+            _, _, d, _ = env.step(da, aa)
             n += 1
             if d:
                 while True:  # the reference raises here for a few L=10 draws; draw again
@@ -73,14 +104,14 @@ def _cpu_worker(args):
     return n, time.perf_counter() - t0
 
 
-def cpu_baseline(L, seconds, procs):
+def cpu_baseline(L, mode, multi, seconds, procs, workload):
     with mp.get_context("spawn").Pool(procs) as pool:
-        res = pool.map(_cpu_worker, [(L, seconds, 90001 + i) for i in range(procs)])
+        res = pool.map(_cpu_worker, [(L, mode, multi, seconds, 90001 + i) for i in range(procs)])
     steps = sum(r[0] for r in res)
     wall = max(r[1] for r in res)
     return {"value": steps / wall, "unit": "env-steps/s", "cores": procs, "kind": "port",
-            "sample": "oracle/td_oracle.py (Python restatement of the reference step, parity-pinned) TD-def-small "
-                      "random defender actions, %d processes x %.0f s, %d env-steps" % (procs, seconds, steps)}
+            "sample": "oracle/td_oracle.py (Python restatement of the reference step, parity-pinned) %s "
+                      "random actions, %d processes x %.0f s, %d env-steps" % (workload, procs, seconds, steps)}
 
 
 def host_cores():
@@ -97,9 +128,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--boards", type=int, default=65536, help="boards per GPU")
-    ap.add_argument("--map-size", type=int, default=10)
-    ap.add_argument("--burnin", type=int, default=600)
+    ap.add_argument("--workload", default="def-small", choices=sorted(WORKLOADS))
+    ap.add_argument("--boards", type=int, default=None, help="boards per GPU (default: the workload's)")
+    ap.add_argument("--burnin", type=int, default=1200)
+    ap.add_argument("--stagger", type=int, default=1, help="stagger episode phases during burn-in (see docstring)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -117,21 +149,44 @@ def main():
 
     from gym_TD.engine import TDEngine
     from gym_TD import shard
+    from gym_TD import params as P
 
-    B, L, K, W = args.boards, args.map_size, args.steps, args.warmup
+    L, mode, multi, B_default, metric = WORKLOADS[args.workload]
+    B = args.boards or B_default
+    K, W = args.steps, args.warmup
     seeds = shard.shard_seeds(args.seed, rank, B)
-    eng = TDEngine(L, B, "def", False, 1, device=dev, np_seeds=seeds, py_seeds=seeds, autoreset=bool(args.autoreset), info=True)
+    eng = TDEngine(L, B, mode, multi, 1, device=dev, np_seeds=seeds, py_seeds=seeds, autoreset=bool(args.autoreset),
+                   info=True)
     obs, _ = eng.reset_all()  # failing road draws (the reference raises/hangs) are redrawn
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
-    n_act = 6 * L * L + 1
-    burn = torch.randint(0, n_act, (max(args.burnin, 1), B), device=dev, generator=g, dtype=torch.int64)
-    for k in range(args.burnin):
-        eng.step(def_act=burn[k])
-    warm = torch.randint(0, n_act, (max(W, 1), B), device=dev, generator=g, dtype=torch.int64)
-    for k in range(W):
-        eng.step(def_act=warm[k])
-    acts = torch.randint(0, n_act, (K, B), device=dev, generator=g, dtype=torch.int64)
-    del burn, warm
+
+    def draw(n):
+        """n pre-drawn (defender, attacker) action batches on the device."""
+        out = []
+        for _ in range(n):
+            d = a = None
+            if mode != "atk":
+                d = (torch.randint(0, 3, (B, 6, L, L), device=dev, generator=g, dtype=torch.int64) if multi
+                     else torch.randint(0, 6 * L * L + 1, (B,), device=dev, generator=g, dtype=torch.int64))
+            if mode != "def":
+                a = torch.randint(0, 5, (B, 3, 8), device=dev, generator=g, dtype=torch.int64)
+            out.append((d, a))
+        return out
+
+    # the discrete shapes draw every step's actions up front; the multi-action shapes
+    # (315 MB of int64 flags per step at 20x20) cycle N_ACTION_BUFS batches, each
+    # larger than the L2s and the 256 MiB MALL, so every step still reads its actions from HBM
+    pool = draw(N_ACTION_BUFS) if multi else None
+    period = P.hyper_parameters.max_episode_steps
+    gidx = np.arange(B) + rank * B
+    for k in range(args.burnin + W):
+        if args.stagger and k < args.burnin and k < period and k > 0:
+            m = (gidx % period) == k
+            if m.any():
+                eng.reset(m)  # a failing draw leaves the board in its first episode (the reference raises)
+        d, a = (pool[k % N_ACTION_BUFS] if multi else draw(1)[0])
+        eng.step(def_act=d, atk_act=a)
+    acts = pool if multi else draw(K)
     stream = torch.cuda.current_stream(dev)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
     eng.episode_stats(clear=True)  # the device accumulates finished episodes of the timed steps
@@ -143,7 +198,8 @@ def main():
     t0 = time.perf_counter()
     for k in range(K):
         ev[k][0].record(stream)
-        eng.step(def_act=acts[k])
+        d, a = acts[k % len(acts)]
+        eng.step(def_act=d, atk_act=a)
         ev[k][1].record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -163,30 +219,32 @@ def main():
     if rank == 0:
         total_steps = world * B * K
         value = total_steps / elapsed
-        bpe = algorithmic_bytes(L)
+        bpe = algorithmic_bytes(L, mode, multi)
         achieved = B * bpe / avg_kernel_s / 1e9
         traffic = None
         tp = os.path.join(HERE, "profiles", "pmc_traffic.json")
         if os.path.exists(tp):
             try:
                 tj = json.load(open(tp))
-                key = "L%d_B%d" % (L, B)
+                key = "%s_B%d" % (args.workload, B)
                 if key in tj:
                     traffic = tj[key]["hbm_bytes_per_launch"]
             except Exception:  # noqa: BLE001
                 traffic = None
         out = {
-            "metric": "env-steps/sec (whole node), 10x10 board, batch=65k, at 1/2/4/8 MI355X",
+            "metric": metric,
             "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": K, "warmup": W,
             "ms_per_step": elapsed / K * 1e3, "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "f64",
-            "data": "synthetic: uniform random defender actions, built-in lv1 opponent, seeded boards",
-            "config": {"workload": "TD-def-small-v0 (10x10), %d boards per GPU, auto-reset, burn-in %d steps"
-                                   % (B, args.burnin), "global_batch": world * B, "boards_per_gpu": B,
+            "data": DATA[mode, multi],
+            "config": {"workload": "%s (%dx%d), %d boards per GPU, auto-reset, burn-in %d steps%s"
+                                   % (ENV_ID[args.workload], L, L, B, args.burnin,
+                                      ", episode phases staggered" if args.stagger else ""), "global_batch": world * B,
+                       "boards_per_gpu": B,
                        "map_size": L, "parallelism": "boards sharded per GPU (dp%d)" % world},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "td_step_kernel<10>", "avg_kernel_us": avg_kernel_s * 1e6,
+                         "kernel": "td_step_kernel<%d, %s>" % (L, mode.upper()), "avg_kernel_us": avg_kernel_s * 1e6,
                          "algorithmic_bytes_per_launch": B * bpe},
             "board_flags_nonzero": int((flags != 0).sum()),
             "episodes": {"finished": int(per_rank[:, 0].sum()),
@@ -194,7 +252,7 @@ def main():
                          "per_rank": [int(v) for v in per_rank[:, 0].tolist()]},
         }
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(L, args.cpu_seconds, host_cores())
+            out["cpu_baseline"] = cpu_baseline(L, mode, multi, args.cpu_seconds, host_cores(), args.workload)
         print(json.dumps(out), flush=True)
     eng.close()
     if world > 1:

@@ -43,7 +43,7 @@ int fail(const char* fmt, ...) {
     if (e_ != hipSuccess) return fail("%s: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, __LINE__); \
   } while (0)
 
-constexpr int kRefillEvery = 8;  // steps between refill launches (episodes last >= ~40 steps)
+constexpr int kRefillEvery = 8;  // steps between refill launches (a board consumes <= 1 layout per ~40 steps)
 
 }  // namespace
 
@@ -57,18 +57,18 @@ struct td_handle {
   double *d_en_lp = nullptr, *d_en_mg = nullptr, *d_tw_cd = nullptr;
   uint32_t *d_en_inf = nullptr, *d_tw_inf = nullptr, *d_cells = nullptr, *d_opp = nullptr, *d_np = nullptr;
   uint32_t* d_hot = nullptr;  // opponent hot record [B][HOT_WORDS]
-  uint32_t *d_nxt = nullptr, *d_qcount = nullptr, *d_stage = nullptr;  // d_queue / d_qcount: 2 buffers
-  int32_t *d_queue = nullptr, *d_stage_ids = nullptr;
+  uint32_t *d_nxt = nullptr, *d_stage = nullptr;  // staged-layout rings [B][NSLOT][slot_words]; caller records
+  uint32_t *d_lay_head = nullptr, *d_lay_tail = nullptr;  // ring counters (td_kernels.h)
+  int32_t* d_ovr_idx = nullptr;                           // td_reset_layouts: [B] index into d_stage or -1
   uint8_t *d_scratch = nullptr, *d_mask = nullptr, *d_fail = nullptr;
   int stage_cap = 0;
   uint64_t* d_stamps = nullptr;  // TD_STAMPS diagnostic builds only (not owned)
   double* d_epstats = nullptr;   // [2] finished episodes, sum of their returns
-  // Layout refill runs on a side stream: step kernels append to queue[cur]; a
-  // refill takes the current buffer and steps switch to the other one.
+  // Layout refills run on a side stream, at most one in flight; the step stream
+  // never waits for them (the rings give every board two episodes of slack).
   hipStream_t side = nullptr;
-  hipEvent_t ev_main = nullptr, ev_refill[2] = {nullptr, nullptr};
-  bool refill_pending[2] = {false, false};
-  int cur = 0;
+  hipEvent_t ev_main = nullptr, ev_refill = nullptr;
+  bool refill_inflight = false;
   long long steps = 0;
   std::vector<int32_t> last_reset_failed;
 };
@@ -147,7 +147,7 @@ StepArgs base_args(td_handle* h) {
   a.hdr = h->d_hdr; a.en_lp = h->d_en_lp; a.en_mg = h->d_en_mg; a.en_inf = h->d_en_inf;
   a.tw_cd = h->d_tw_cd; a.tw_inf = h->d_tw_inf; a.cells = h->d_cells; a.opp_mt = h->d_opp; a.opp_hot = h->d_hot;
   a.np_mt = h->d_np; a.nxt = h->d_nxt; a.scratch = h->d_scratch; a.scratch_stride = h->scratch_stride;
-  a.queue = h->d_queue + (size_t)h->cur * h->B; a.qcount = h->d_qcount + h->cur;
+  a.lay_head = h->d_lay_head; a.lay_tail = h->d_lay_tail; a.slot_words = slot_words(h->L);
   a.reset_fail = h->d_fail; a.cfg = h->d_cfg;
   return a;
 }
@@ -168,34 +168,36 @@ void parallel_for(int n, F fn) {
 // Drop staged layouts: they were drawn from a stream that has been replaced.
 int drop_staged(td_handle* h, int b) {
   HIP_OK(hipDeviceSynchronize());
-  HIP_OK(hipMemset(h->d_nxt + (size_t)b * h->lw, 0, 4));
+  const size_t ring = (size_t)NSLOT * slot_words(h->L);
+  HIP_OK(hipMemset(h->d_nxt + (size_t)b * ring, 0, ring * 4));
+  HIP_OK(hipMemset(h->d_lay_head + b, 0, 4));
+  HIP_OK(hipMemset(h->d_lay_tail + b, 0, 4));
   return 0;
 }
 
 int drop_all_staged(td_handle* h) {
   HIP_OK(hipDeviceSynchronize());
-  HIP_OK(hipMemset(h->d_nxt, 0, (size_t)h->B * h->lw * 4));
-  HIP_OK(hipMemset(h->d_qcount, 0, 8));
+  HIP_OK(hipMemset(h->d_nxt, 0, (size_t)h->B * NSLOT * slot_words(h->L) * 4));
+  HIP_OK(hipMemset(h->d_lay_head, 0, (size_t)h->B * 4));
+  HIP_OK(hipMemset(h->d_lay_tail, 0, (size_t)h->B * 4));
   return 0;
 }
 
-// Hand the current refill queue to the side stream (after the work on `s` that
-// filled it) and switch the step kernels to the other buffer.
-int start_refill(td_handle* h, hipStream_t s) {
-  const int q = h->cur;
+// Launch a ring refill on the side stream behind the work queued on `s` so far,
+// unless the previous refill is still running (a refill that meets a layout the
+// reference would hang on runs for milliseconds; the next one catches up).
+int start_refill(td_handle* h, hipStream_t s, bool force) {
+  if (h->refill_inflight && !force) {
+    hipError_t q = hipEventQuery(h->ev_refill);
+    if (q == hipErrorNotReady) return 0;
+    if (q != hipSuccess) HIP_OK(q);
+  }
   StepArgs a = base_args(h);
   HIP_OK(hipEventRecord(h->ev_main, s));
   HIP_OK(hipStreamWaitEvent(h->side, h->ev_main, 0));
   HIP_OK(launch_refill(a, h->side));
-  HIP_OK(hipEventRecord(h->ev_refill[q], h->side));
-  h->refill_pending[q] = true;
-  h->cur ^= 1;
-  // the buffer steps now append to was handed out two refills ago: its refill
-  // (and the queue reset behind it) must be done before the next step reads it
-  if (h->refill_pending[h->cur]) {
-    HIP_OK(hipStreamWaitEvent(s, h->ev_refill[h->cur], 0));
-    h->refill_pending[h->cur] = false;
-  }
+  HIP_OK(hipEventRecord(h->ev_refill, h->side));
+  h->refill_inflight = true;
   return 0;
 }
 
@@ -205,9 +207,8 @@ int run_reset(td_handle* h, const std::vector<uint8_t>& mask, float* obs, hipStr
   StepArgs a = base_args(h);
   a.obs = obs;
   a.reset_mask = h->d_mask;
-  a.stage_next = h->autoreset;
   HIP_OK(launch_step(a, s, true));
-  if (h->autoreset && start_refill(h, s)) return -1;
+  if (h->autoreset && start_refill(h, s, true)) return -1;
   HIP_OK(hipStreamSynchronize(s));
   HIP_OK(hipStreamSynchronize(h->side));
   return 0;
@@ -301,20 +302,19 @@ td_handle* td_create(const td_config* cfg, int map_size, int n_boards, int mode,
   rc |= dalloc(&h->d_opp, B * OPP_WORDS);
   rc |= dalloc(&h->d_hot, B * HOT_WORDS);
   rc |= dalloc(&h->d_np, B * OPP_WORDS);
-  rc |= dalloc(&h->d_nxt, B * h->lw);
+  rc |= dalloc(&h->d_nxt, B * NSLOT * slot_words(map_size));
+  rc |= dalloc(&h->d_lay_head, B);
+  rc |= dalloc(&h->d_lay_tail, B);
+  rc |= dalloc(&h->d_ovr_idx, B);
   rc |= dalloc(&h->d_scratch, B * h->scratch_stride);
-  rc |= dalloc(&h->d_queue, 2 * B);
-  rc |= dalloc(&h->d_qcount, 2);
   rc |= dalloc(&h->d_mask, B);
   rc |= dalloc(&h->d_fail, B);
   rc |= dalloc(&h->d_stage, (size_t)h->stage_cap * h->lw);
-  rc |= dalloc(&h->d_stage_ids, (size_t)h->stage_cap);
   rc |= dalloc(&h->d_epstats, 2);
   if (!rc && hipMemcpy(h->d_cfg, &h->dcfg, sizeof(TdDevCfg), hipMemcpyHostToDevice) != hipSuccess) rc = fail("cfg upload");
   if (!rc && hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking) != hipSuccess) rc = fail("side stream");
   if (!rc && hipEventCreateWithFlags(&h->ev_main, hipEventDisableTiming) != hipSuccess) rc = fail("event");
-  for (int q = 0; q < 2 && !rc; ++q)
-    if (hipEventCreateWithFlags(&h->ev_refill[q], hipEventDisableTiming) != hipSuccess) rc = fail("event");
+  if (!rc && hipEventCreateWithFlags(&h->ev_refill, hipEventDisableTiming) != hipSuccess) rc = fail("event");
   if (rc) { std::string e = g_err; td_destroy(h); g_err = e; return nullptr; }
   std::vector<uint32_t> seeds(B);
   for (size_t b = 0; b < B; ++b) seeds[b] = (uint32_t)b;
@@ -327,13 +327,12 @@ void td_destroy(td_handle* h) {
   (void)hipSetDevice(h->device);
   (void)hipDeviceSynchronize();
   void* dptrs[] = {h->d_cfg, h->d_hdr, h->d_en_lp, h->d_en_mg, h->d_en_inf, h->d_tw_cd, h->d_tw_inf,
-                   h->d_cells, h->d_opp, h->d_hot, h->d_np, h->d_nxt, h->d_scratch, h->d_queue, h->d_qcount,
-                   h->d_mask, h->d_fail, h->d_stage, h->d_stage_ids, h->d_epstats};
+                   h->d_cells, h->d_opp, h->d_hot, h->d_np, h->d_nxt, h->d_scratch, h->d_lay_head, h->d_lay_tail,
+                   h->d_ovr_idx, h->d_mask, h->d_fail, h->d_stage, h->d_epstats};
   for (void* p : dptrs)
     if (p) (void)hipFree(p);
   if (h->ev_main) (void)hipEventDestroy(h->ev_main);
-  for (int q = 0; q < 2; ++q)
-    if (h->ev_refill[q]) (void)hipEventDestroy(h->ev_refill[q]);
+  if (h->ev_refill) (void)hipEventDestroy(h->ev_refill);
   if (h->side) (void)hipStreamDestroy(h->side);
   delete h;
 }
@@ -459,16 +458,25 @@ int td_reset_layouts(td_handle* h, const uint32_t* recs, const int32_t* boards, 
     if (boards[i] < 0 || boards[i] >= h->B || recs[(size_t)i * h->lw] != TD_LAYOUT_MAGIC)
       return fail("td_reset_layouts: bad board id or layout record %d", i);
   HIP_OK(hipDeviceSynchronize());
+  std::vector<int32_t> idx((size_t)h->B, -1);
   for (int i0 = 0; i0 < n; i0 += h->stage_cap) {
-    int m = std::min(h->stage_cap, n - i0);
+    const int m = std::min(h->stage_cap, n - i0);
+    std::vector<uint8_t> mask((size_t)h->B, 0);
+    std::fill(idx.begin(), idx.end(), -1);
+    for (int i = 0; i < m; ++i) { idx[(size_t)boards[i0 + i]] = i; mask[(size_t)boards[i0 + i]] = 1; }
     HIP_OK(hipMemcpy(h->d_stage, recs + (size_t)i0 * h->lw, (size_t)m * h->lw * 4, hipMemcpyHostToDevice));
-    HIP_OK(hipMemcpy(h->d_stage_ids, boards + i0, (size_t)m * 4, hipMemcpyHostToDevice));
-    HIP_OK(launch_stage_layouts(h->d_nxt, h->d_stage, h->d_stage_ids, m, h->lw, s));
+    HIP_OK(hipMemcpy(h->d_ovr_idx, idx.data(), (size_t)h->B * 4, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(h->d_mask, mask.data(), (size_t)h->B, hipMemcpyHostToDevice));
+    HIP_OK(hipMemset(h->d_fail, 0, (size_t)h->B));
+    StepArgs a = base_args(h);
+    a.obs = obs;
+    a.reset_mask = h->d_mask;
+    a.ovr_idx = h->d_ovr_idx;
+    a.ovr_rec = h->d_stage;
+    HIP_OK(launch_step(a, s, true));
     HIP_OK(hipStreamSynchronize(s));
   }
-  std::vector<uint8_t> mask((size_t)h->B, 0);
-  for (int i = 0; i < n; ++i) mask[(size_t)boards[i]] = 1;
-  return run_reset(h, mask, obs, s);
+  return 0;
 }
 
 int td_step(td_handle* h, const td_step_io* io, void* stream) {
@@ -485,7 +493,7 @@ int td_step(td_handle* h, const td_step_io* io, void* stream) {
   a.ep_stats = h->d_epstats;
   HIP_OK(launch_step(a, s, false));
   h->steps += 1;
-  if (h->autoreset && (h->steps % kRefillEvery) == 0 && start_refill(h, s)) return -1;
+  if (h->autoreset && (h->steps % kRefillEvery) == 0 && start_refill(h, s, false)) return -1;
   return 0;
 }
 

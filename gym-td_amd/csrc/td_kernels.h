@@ -22,13 +22,20 @@ struct StepArgs {
   uint32_t* opp_mt;     // [B][626] CPython-random MT words of the built-in opponent ([624..625] unused)
   uint32_t* opp_hot;    // [B][HOT_WORDS] its position, lazy-twist boundary, count and next 8 draws
   uint32_t* np_mt;      // [B][625] numpy-legacy state of the layout stream (TDGymBasic.np_random)
-  uint32_t* nxt;        // [B][8 + L*L] staged next-episode layout (word 0 = magic while unconsumed)
+  // Staged next-episode layouts: a ring of NSLOT records per board (slot_words
+  // words each, 128-B aligned).  Layout number n of a board's stream lives in slot
+  // n % NSLOT with word 0 = slot_tag(n) once it is complete; lay_tail counts the
+  // layouts drawn (written by the refill / reset kernels only), lay_head the
+  // layouts consumed (written by the step / reset kernels only).
+  uint32_t* nxt;        // [B][NSLOT][slot_words]
+  uint32_t* lay_head;   // [B]
+  uint32_t* lay_tail;   // [B]
+  int slot_words;
   uint8_t* scratch;     // [B][scratch_stride] road-generation scratch
   size_t scratch_stride;
-  int32_t* queue;       // [B] boards whose staged layout was consumed (refill queue)
-  uint32_t* qcount;     // queue length
   uint8_t* reset_fail;  // [B] reset kernel: road generation failed (board left unchanged)
-  int stage_next;       // reset kernel: queue reset boards for a staged next layout
+  const int32_t* ovr_idx;   // reset kernel, td_reset_layouts: [B] record index in ovr_rec, or -1
+  const uint32_t* ovr_rec;  // caller-supplied layout records (layout_words(L) each)
   uint64_t* stamps;     // TD_STAMPS diagnostic builds only: [B][16] s_memtime per phase
   const TdDevCfg* cfg;
   const int64_t* def_act;
@@ -49,10 +56,12 @@ struct StepArgs {
 };
 
 hipError_t launch_step(const StepArgs& a, hipStream_t s, bool reset);
-hipError_t launch_stage_layouts(uint32_t* nxt, const uint32_t* recs, const int32_t* boards, int n, int words,
-                                hipStream_t s);
-// Generate staged layouts for the queued boards (one lane per board), then clear the queue.
+// Draw staged layouts for every board whose ring has a free slot (side stream).
 hipError_t launch_refill(const StepArgs& a, hipStream_t s);
+
+constexpr int NSLOT = 2;  // staged layouts per board: two episodes of slack for the refill
+__host__ __device__ inline uint32_t slot_tag(uint32_t n) { return 0x80000000u | (n & 0x7fffffffu); }
+__host__ __device__ inline int slot_words(int L) { return (8 + L * L + 31) & ~31; }
 
 constexpr int kRoadAttempts = 1000;  // bound of each create_road_v2 retry loop (reference: unbounded)
 constexpr int kLayoutRetries = 64;   // auto-reset: failing draws skipped before giving up

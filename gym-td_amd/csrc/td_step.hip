@@ -56,6 +56,17 @@ __device__ __forceinline__ double rdl(double v, int l) {
   return __hiloint2double((int)rdl((uint32_t)__double2hiint(v), l), (int)rdl((uint32_t)__double2loint(v), l));
 }
 
+// Agent-scope relaxed accesses through the global address space (global_load /
+// global_store ... sc1, never flat): the words two concurrently running grids
+// hand over (layout tags, ring counters).
+typedef __attribute__((address_space(1))) uint32_t gu32;
+__device__ __forceinline__ uint32_t ld_relaxed(const uint32_t* p) {
+  return __hip_atomic_load((gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_relaxed(uint32_t* p, uint32_t v) {
+  __hip_atomic_store((gu32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // ---------------------------------------------------------------------------
 // per-board LDS image
 // ---------------------------------------------------------------------------
@@ -907,9 +918,12 @@ __device__ void load_board(Smem<NC>& S, U& u, const Ctx& x, const StepArgs& a, i
 template <int NC>
 __device__ void reset_board(Smem<NC>& S, U& u, const Ctx& x, const uint32_t* rec) {
   const TdDevCfg& C = x.C;
+  // vector loads only (lane-indexed, then readlane): a record handed over by a
+  // concurrently running refill must not come through the scalar cache
+  const uint32_t hw = rec[x.lane & (LAYOUT_HDR - 1)];
   for (int i = x.lane; i < x.NCr; i += 64) { S.cell[i] = rec[LAYOUT_HDR + i]; S.twr[i] = 0; }
-  u.num_roads = (int)rec[1]; u.end_cell = (int)rec[2]; u.maxdist = (int)rec[3];
-  u.set_starts(rec[4], rec[5], rec[6]);
+  u.num_roads = (int)rdl(hw, 1); u.end_cell = (int)rdl(hw, 2); u.maxdist = (int)rdl(hw, 3);
+  u.set_starts(rdl(hw, 4), rdl(hw, 5), rdl(hw, 6));
   u.cost_def = C.def_init_cost; u.cost_atk = C.atk_init_cost;
   u.base_LP = C.base_LP; u.steps = 0; u.progress = 0.0;
   u.atk_cd = 0; u.def_cd = 0; u.n = 0; u.nt = 0; u.ep_ret = 0.0;
@@ -1177,13 +1191,19 @@ __device__ void step_board(Smem<NC>& S, const Ctx& x, const StepArgs& a, int b, 
 
   if (done) u.episodes += 1;
   bool was_reset = false;
+  uint32_t lay_head = 0;
   if (done && a.autoreset) {
-    const uint32_t* rec = a.nxt + (size_t)b * (LAYOUT_HDR + x.NCr);
-    if (rec[0] == TD_LAYOUT_MAGIC) {
+    // consume staged layout number lay_head, published by the refill kernel on the
+    // side stream while this grid may be running: relaxed poll of its tag, then one
+    // agent-scope acquire before the plain loads of the record (MI355X_MICROARCH.md
+    // § visibility, "Valid forms"; the producer side is publish_slot)
+    lay_head = a.lay_head[b];
+    const uint32_t* rec = a.nxt + ((size_t)b * NSLOT + lay_head % NSLOT) * a.slot_words;
+    const uint32_t tag = ld_relaxed(rec);
+    if (tag == slot_tag(lay_head)) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       reset_board(S, u, x, rec);
       was_reset = true;
-      // the new episode's static / tower planes replace the ones written above:
-      // drain those stores first so the rewrite lands after them
     } else {
       u.flags |= FLAG_NO_LAYOUT;  // refill fell behind: the board keeps stepping its finished episode
     }
@@ -1198,10 +1218,8 @@ __device__ void step_board(Smem<NC>& S, const Ctx& x, const StepArgs& a, int b, 
 
   if (MODE != MODE_2P) R.prefetch_finish(x.lane);
   if (x.lane == 0) {
-    if (was_reset) {
-      a.nxt[(size_t)b * (LAYOUT_HDR + x.NCr)] = 0u;  // staged layout consumed: queue a refill
-      a.queue[atomicAdd(a.qcount, 1u)] = b;
-    }
+    if (was_reset)  // the record has been read into LDS: its slot may be redrawn
+      st_relaxed(a.lay_head + b, lay_head + 1u);
     hot[0] = R.pos;
     hot[1] = R.tw;
     hot[2] = R.cn;
@@ -1252,14 +1270,16 @@ struct LayoutSmem {
   uint8_t scratch[14 * NC + 64];
 };
 
-// TDGymBasic.reset's draws (:42-51) for board b: the layout goes to its staged
-// slot nxt[b] (word 0 = magic written last), failing draws are skipped up to
-// ``retries`` times.  Returns the road status of the last draw (wave-uniform).
+// TDGymBasic.reset's draws (:42-51) for board b into slot `slot` of its ring, as
+// layout number `n` of the stream: failing draws are skipped up to ``retries``
+// times.  The record is published for a step grid that may be running on another
+// stream: plain stores, every lane's vmcnt(0), the barrier, ONE agent-scope
+// release, then the tag by an sc1 store (MI355X_MICROARCH.md § visibility, "Valid
+// forms", producer bullet).  Returns the road status of the last draw.
 template <int NC>
-__device__ int wave_layout(LayoutSmem<NC>& G, const StepArgs& a, int b, int retries) {
+__device__ int wave_layout(LayoutSmem<NC>& G, const StepArgs& a, int b, int retries, uint32_t* slot, uint32_t n) {
   const int lane = (int)threadIdx.x, L = a.L, lw = LAYOUT_HDR + L * L;
   uint32_t* gmt = a.np_mt + (size_t)b * OPP_WORDS;
-  uint32_t* grec = a.nxt + (size_t)b * lw;
   for (int i = lane; i < OPP_WORDS; i += 64) G.mt[i] = gmt[i];
   __syncthreads();
   int st = ROAD_ERR_BOUND;
@@ -1276,17 +1296,23 @@ __device__ int wave_layout(LayoutSmem<NC>& G, const StepArgs& a, int b, int retr
   __syncthreads();
   for (int i = lane; i < OPP_WORDS; i += 64) gmt[i] = G.mt[i];
   if (st == ROAD_OK) {
-    for (int i = 1 + lane; i < lw; i += 64) grec[i] = G.rec[i];
-    __threadfence();
+    for (int i = 1 + lane; i < lw; i += 64) slot[i] = G.rec[i];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (lane == 0) grec[0] = TD_LAYOUT_MAGIC;
+    if (lane == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      st_relaxed(slot, slot_tag(n));
+    }
   }
   return st;
 }
 
-// TDGymBasic.reset for the boards in reset_mask: the staged layout when there is
-// one, else a draw from the board's numpy stream now (no retry: a failing draw is
-// reported in reset_fail and the board is left unchanged, as the reference raises).
+// TDGymBasic.reset for the boards in reset_mask (the device is idle: td_capi
+// synchronises first).  The layout is the caller's record (td_reset_layouts), else
+// the board's next staged layout, else a draw from its numpy stream now; a failing
+// draw (no retry) is reported in reset_fail and leaves the board unchanged, as the
+// reference raises.
 template <int LT>
 __global__ __launch_bounds__(64) void td_reset_kernel(StepArgs a) {
   constexpr int NC = LT ? LT * LT : MAX_KERNEL_L * MAX_KERNEL_L;
@@ -1298,14 +1324,27 @@ __global__ __launch_bounds__(64) void td_reset_kernel(StepArgs a) {
   if (b >= a.B) return;
   if (a.reset_mask && !a.reset_mask[b]) return;
   const int L = LT ? LT : a.L;
-  uint32_t* rec = a.nxt + (size_t)b * (LAYOUT_HDR + L * L);
-  if (rec[0] != TD_LAYOUT_MAGIC) {
-    const int st = wave_layout(sh.gen, a, b, 0);
-    __syncthreads();
-    if (st != ROAD_OK) {
-      if (threadIdx.x == 0) a.reset_fail[b] = (uint8_t)st;
-      return;
+  const uint32_t* rec;
+  bool from_ring = false;
+  uint32_t head = 0;
+  const int ov = a.ovr_idx ? a.ovr_idx[b] : -1;
+  if (ov >= 0) {
+    rec = a.ovr_rec + (size_t)ov * (LAYOUT_HDR + L * L);
+  } else {
+    head = a.lay_head[b];
+    const uint32_t tail = a.lay_tail[b];
+    uint32_t* slot = a.nxt + ((size_t)b * NSLOT + head % NSLOT) * a.slot_words;
+    if (tail == head) {  // nothing staged: draw now
+      const int st = wave_layout(sh.gen, a, b, 0, slot, head);
+      __syncthreads();
+      if (st != ROAD_OK) {
+        if (threadIdx.x == 0) a.reset_fail[b] = (uint8_t)st;
+        return;
+      }
+      if (threadIdx.x == 0) a.lay_tail[b] = tail + 1u;
     }
+    rec = slot;
+    from_ring = true;
   }
   Smem<NC>& S = sh.board;
   stage_cfg(S, a.cfg);
@@ -1320,33 +1359,44 @@ __global__ __launch_bounds__(64) void td_reset_kernel(StepArgs a) {
   store_board(S, u, x, a, b);
   if (x.lane == 0) {
     a.reset_fail[b] = 0;
-    rec[0] = 0u;
-    if (a.stage_next) a.queue[atomicAdd(a.qcount, 1u)] = b;
+    if (from_ring) a.lay_head[b] = head + 1u;
   }
 }
 
-// Stage the next-episode layout of every queued board: one wave per board
-// (grid-stride over the queue), then clear the queue.  Runs on a side stream,
-// concurrently with later steps (td_capi.hip double-buffers the queue).
+// Keep every board's ring of staged layouts full: lanes check 64 boards at once
+// (layouts drawn minus consumed < NSLOT), then the wave draws the missing layouts
+// of those boards one by one, lane 0 running the serial generator out of LDS.  Runs
+// on a side stream concurrently with the step grids; td_capi keeps at most one in
+// flight and never makes the step stream wait for it.
 template <int LT>
 __global__ __launch_bounds__(64) void td_refill_kernel(StepArgs a) {
   constexpr int NC = LT ? LT * LT : MAX_KERNEL_L * MAX_KERNEL_L;
   __shared__ LayoutSmem<NC> G;
-  const uint32_t n = *a.qcount;
-  for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
-    wave_layout(G, a, a.queue[i], kLayoutRetries);
-    __syncthreads();
+  const int lane = (int)threadIdx.x;
+  for (int base = (int)blockIdx.x * 64; base < a.B; base += (int)gridDim.x * 64) {
+    const int b = base + lane;
+    uint32_t head = 0, tail = 0;
+    if (b < a.B) {
+      head = ld_relaxed(a.lay_head + b);  // a step grid may be advancing it right now
+      tail = a.lay_tail[b];
+    }
+    uint64_t m = ballot(b < a.B && tail - head < (uint32_t)NSLOT);
+    while (m) {
+      const int l = ctz64(m);
+      m &= m - 1;
+      const int bb = base + l;
+      uint32_t t = rdl(tail, l);
+      const uint32_t h = rdl(head, l);
+      while (t - h < (uint32_t)NSLOT) {
+        uint32_t* slot = a.nxt + ((size_t)bb * NSLOT + t % NSLOT) * a.slot_words;
+        const int st = wave_layout(G, a, bb, kLayoutRetries, slot, t);
+        __syncthreads();
+        if (st != ROAD_OK) break;  // 65 failing draws in a row: the next refill tries again
+        ++t;
+      }
+      if (lane == 0) a.lay_tail[bb] = t;
+    }
   }
-}
-
-// Copy staged layout records into the boards' next-episode slots.
-__global__ __launch_bounds__(64) void td_stage_layouts_kernel(uint32_t* nxt, const uint32_t* recs, const int32_t* boards,
-                                                          int n, int words) {
-  const int i = blockIdx.x;
-  if (i >= n) return;
-  uint32_t* dst = nxt + (size_t)boards[i] * words;
-  const uint32_t* src = recs + (size_t)i * words;
-  for (int k = (int)threadIdx.x; k < words; k += 64) dst[k] = src[k];
 }
 
 template <int LT>
@@ -1369,7 +1419,8 @@ hipError_t launch_step(const StepArgs& a, hipStream_t s, bool reset) {
 
 template <int LT>
 static void launch_refill2(const StepArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(td_refill_kernel<LT>, dim3(1024), dim3(64), 0, s, a);
+  const int waves = std::min((a.B + 63) / 64, 1024);
+  hipLaunchKernelGGL(td_refill_kernel<LT>, dim3(waves), dim3(64), 0, s, a);
 }
 
 hipError_t launch_refill(const StepArgs& a, hipStream_t s) {
@@ -1379,15 +1430,6 @@ hipError_t launch_refill(const StepArgs& a, hipStream_t s) {
     case 30: launch_refill2<30>(a, s); break;
     default: launch_refill2<0>(a, s); break;
   }
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  return hipMemsetAsync(a.qcount, 0, sizeof(uint32_t), s);
-}
-
-hipError_t launch_stage_layouts(uint32_t* nxt, const uint32_t* recs, const int32_t* boards, int n, int words,
-                                hipStream_t s) {
-  if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(td_stage_layouts_kernel, dim3(n), dim3(64), 0, s, nxt, recs, boards, n, words);
   return hipGetLastError();
 }
 

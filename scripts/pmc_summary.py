@@ -1,10 +1,10 @@
 """Summarise a profile_session.sh run (gpurun_out/prof) into profiles/.
 
-  python scripts/pmc_summary.py ROUND [B] [L]
+  python scripts/pmc_summary.py ROUND [B] [WORKLOAD]
 
 writes profiles/<ROUND>_kernel_stats.csv (rocprofv3 --kernel-trace --stats),
 profiles/<ROUND>_pmc.json (per-launch counter means of the step kernel) and
-updates profiles/pmc_traffic.json["L<L>_B<B>"] with the HBM bytes per launch:
+updates profiles/pmc_traffic.json["<WORKLOAD>_B<B>"] (bench.py's key) with the HBM bytes per launch:
 (2 x FETCH_SIZE + WRITE_SIZE) x 1024 -- FETCH_SIZE / WRITE_SIZE are in KiB and
 FETCH_SIZE counts half the bytes of 16-B-per-lane reads on gfx950
 (/opt/skills/guides/MI355X_MICROARCH.md, HBM section).
@@ -33,9 +33,11 @@ def step_counters(name):
 def main():
     rnd = sys.argv[1]
     B = int(sys.argv[2]) if len(sys.argv) > 2 else 65536
-    L = int(sys.argv[3]) if len(sys.argv) > 3 else 10
+    wl = sys.argv[3] if len(sys.argv) > 3 else "def-small"
+    L, mode = {"def-small": (10, "DEF"), "2p-middle-multi": (20, "2P"), "def-large": (30, "DEF")}[wl]
     out = os.path.join(HERE, "profiles")
-    shutil.copy(os.path.join(PROF, "kt", "kt_kernel_stats.csv"), os.path.join(out, "%s_kernel_stats.csv" % rnd))
+    tag = rnd if wl == "def-small" else "%s_%s" % (rnd, wl)
+    shutil.copy(os.path.join(PROF, "kt", "kt_kernel_stats.csv"), os.path.join(out, "%s_kernel_stats.csv" % tag))
     pmc, launches = {}, {}
     for n in ("pmc_fetch", "pmc_write", "pmc_sq1", "pmc_sq2"):
         if os.path.exists(os.path.join(PROF, n)):
@@ -45,17 +47,17 @@ def main():
     fetch = pmc["FETCH_SIZE"] * 2 * 1024
     write = pmc["WRITE_SIZE"] * 1024
     summary = {
-        "kernel": "td_step_kernel<%d, DEF>" % L, "boards": B, "launches_per_pass": launches,
+        "kernel": "td_step_kernel<%d, %s>" % (L, mode), "boards": B, "launches_per_pass": launches,
         "counters_per_launch": pmc,
         "hbm_read_bytes_per_launch": fetch, "hbm_write_bytes_per_launch": write,
         "hbm_bytes_per_launch": fetch + write,
         "per_board": {"read_bytes": fetch / B, "write_bytes": write / B,
                       "valu_insts": pmc.get("SQ_INSTS_VALU", 0) / B, "salu_insts": pmc.get("SQ_INSTS_SALU", 0) / B},
     }
-    json.dump(summary, open(os.path.join(out, "%s_pmc.json" % rnd), "w"), indent=1)
+    json.dump(summary, open(os.path.join(out, "%s_pmc.json" % tag), "w"), indent=1)
     tp = os.path.join(out, "pmc_traffic.json")
     tj = json.load(open(tp)) if os.path.exists(tp) else {}
-    tj["L%d_B%d" % (L, B)] = {"hbm_bytes_per_launch": fetch + write, "read": fetch, "write": write, "round": rnd}
+    tj["%s_B%d" % (wl, B)] = {"hbm_bytes_per_launch": fetch + write, "read": fetch, "write": write, "round": rnd}
     json.dump(tj, open(tp, "w"), indent=1)
     print(json.dumps({k: summary[k] for k in ("hbm_read_bytes_per_launch", "hbm_write_bytes_per_launch", "per_board")}))
 

@@ -3,11 +3,12 @@
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out/prof
 export TMPDIR=/tmp
+WL=${WL:-def-small}
 B=${B:-65536}
 run() { local name=$1 secs=$2; shift 2; echo "== $name" >&2; timeout -k 10 "$secs" "$@" > "gpurun_out/prof/$name.log" 2>&1; local rc=$?; echo "== $name rc=$rc" >&2; tail -3 "gpurun_out/prof/$name.log" >&2; return $rc; }
-run phases 300 env TDSTEP_LIB=$PWD/gym-td_amd/lib/libtdstep_stamps.so python scripts/probe_phases.py $B 10 600 || exit $?
+[ -n "$NO_PHASES" ] || run phases 300 env TDSTEP_LIB=$PWD/gym-td_amd/lib/libtdstep_stamps.so python scripts/probe_phases.py $B 10 600 || exit $?
 run counters_list 120 rocprofv3 -L || true
-BENCH="python bench.py --steps 20 --warmup 2 --burnin 100 --no-cpu-baseline --boards $B"
+BENCH="python bench.py --workload $WL --steps 20 --warmup 2 --burnin 100 --no-cpu-baseline --boards $B"
 run kt 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof/kt -o kt --output-format csv -- $BENCH || exit $?
 run pmc_fetch 400 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/prof/pmc_fetch -o pmc --output-format csv -- $BENCH || exit $?
 run pmc_write 400 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/prof/pmc_write -o pmc --output-format csv -- $BENCH || exit $?

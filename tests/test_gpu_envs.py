@@ -1,0 +1,219 @@
+"""GPU parity of the batched paths the golden replays do not reach: TD-atk and
+TD-2p boards stepped together in one launch (every built-in opponent level,
+discrete and multi-action, the info tensors), and the TDVecEnv rollout surface
+(auto-reset with failing layout draws, sharding invariance of trajectories).
+Everything is compared bit-exactly with the CPU oracle on the same seeds."""
+import numpy as np
+import pytest
+import torch
+
+import goldens as G
+from oracle import canon, policies
+from oracle import td_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+if not torch.cuda.is_available():  # collected on CPU too, so skip cleanly
+    pytest.skip("needs a GPU", allow_module_level=True)
+
+from gym_TD import envs as E  # noqa: E402
+from gym_TD.engine import TDEngine  # noqa: E402
+
+from test_gpu_parity import reference_settings  # noqa: E402
+
+ROAD_ATTEMPTS = 1000  # td_kernels.h kRoadAttempts: the device's bound of each create_road_v2 loop
+
+
+def _first_ok_seeds(L, n, start, mode, multi, difficulty, cfg=None):
+    """Seeds whose first layout draw succeeds, with their oracle envs."""
+    hp = O.Hyper(allow_multiple_actions=multi)
+    seeds, envs = [], []
+    s = start
+    while len(seeds) < n:
+        try:
+            envs.append(O.Env(L, G.MODES[mode], difficulty, s, s, cfg or O.Config(), hp, road_attempts=ROAD_ATTEMPTS))
+            seeds.append(s)
+        except O.RoadGenError:
+            pass
+        s += 1
+    return seeds, envs
+
+
+def _fc_list(row):
+    return [int(v) for v in row if v >= 0]
+
+
+@pytest.mark.parametrize("L,B,mode,multi,difficulty,steps", [
+    (10, 24, "atk", False, 0, 150),
+    (10, 24, "atk", False, 1, 150),
+    (10, 24, "atk", False, 2, 150),
+    (20, 12, "atk", False, 2, 100),
+    (10, 24, "2p", False, 1, 150),
+    (10, 16, "2p", True, 1, 120),
+    (10, 16, "def", True, 1, 120),
+    (10, 24, "def", False, 0, 150),
+])
+def test_batched_modes_vs_oracle(L, B, mode, multi, difficulty, steps):
+    """B boards of one mode in one launch vs B oracle envs: reward bits, done,
+    state digest, observation bytes and the info tensors of every board."""
+    seeds, orc = _first_ok_seeds(L, B, 3000 + 97 * difficulty, mode, multi, difficulty)
+    eng = TDEngine(L, B, mode, multi, difficulty, np_seeds=seeds, py_seeds=seeds, autoreset=False)
+    try:
+        _, failed = eng.reset()
+        assert not failed
+        rng = np.random.RandomState(L * 31 + difficulty)
+        for k in range(steps):
+            da = aa = None
+            if mode != "atk":
+                if multi:
+                    da = np.stack([policies.multi_def(rng, L) for _ in range(B)]).astype(np.int64)
+                else:
+                    da = np.array([policies.discrete_def(rng, L, o._board.map[0], 0.5) for o in orc], dtype=np.int64)
+            if mode != "def":
+                aa = np.stack([policies.atk(rng) for _ in range(B)]).astype(np.int64)
+            eng.step(def_act=None if da is None else torch.from_numpy(da),
+                     atk_act=None if aa is None else torch.from_numpy(aa))
+            ob, rw, dn = eng.obs.cpu().numpy(), eng.reward.cpu().numpy(), eng.done.cpu().numpy()
+            win, an = eng.win.cpu().numpy(), eng.allow_next.cpu().numpy()
+            rd = eng.real_def.cpu().numpy() if eng.real_def is not None else None
+            fd = eng.fail_def.cpu().numpy() if eng.fail_def is not None else None
+            ra = eng.real_atk.cpu().numpy() if eng.real_atk is not None else None
+            fa = eng.fail_atk.cpu().numpy() if eng.fail_atk is not None else None
+            st = eng.export_state()
+            for b, o in enumerate(orc):
+                if o._board.done():
+                    continue  # finished in an earlier step (no auto-reset here)
+                d_b = None if da is None else (da[b] if multi else int(da[b]))
+                wo, wr, wd, info = o.step(d_b, None if aa is None else aa[b])
+                tag = (mode, multi, difficulty, k, b)
+                assert canon.fhex(rw[b]) == canon.fhex(wr), tag
+                assert bool(dn[b]) == wd, tag
+                assert canon.state_digest(eng.board_state(b, st)) == canon.state_digest(canon.oracle_state(o)), tag
+                assert np.array_equal(ob[b], wo), (tag, np.argwhere(ob[b] != wo)[:5].tolist())
+                w = info["Win"]
+                if isinstance(w, dict):
+                    w = w["Defender"] if mode != "atk" else w["Attacker"]
+                assert (int(win[b]) if win[b] >= 0 else None) == (None if w is None else int(w)), tag
+                anm = info["AllowNextMove"]
+                if mode == "2p":
+                    assert bool(an[b] & 1) == anm["Attacker"] and bool(an[b] & 2) == anm["Defender"], tag
+                elif mode == "atk":
+                    assert bool(an[b] & 1) == anm, tag
+                else:
+                    assert bool(an[b] & 2) == anm, tag
+                real, fc = info["RealAction"], info["FailCode"]
+                if mode == "def":
+                    if multi:
+                        assert np.array_equal(rd[b], real), tag
+                    else:
+                        assert int(rd[b]) == int(real) and int(fd[b]) == int(fc), tag
+                elif mode == "atk":
+                    assert np.array_equal(ra[b], real), tag
+                    assert _fc_list(fa[b]) == list(fc), tag
+                else:
+                    if multi:
+                        assert np.array_equal(ra[b], real["Attacker"]) and np.array_equal(rd[b], real["Defender"]), tag
+                    else:
+                        if isinstance(real, dict):  # no defender success this step
+                            assert np.array_equal(ra[b], real["Attacker"]), tag
+                            assert int(rd[b]) == L * L * 6, tag
+                        else:  # TDMulti.py:257: the defender action replaced the dict
+                            assert int(rd[b]) == int(real), tag
+                        assert _fc_list(fa[b]) == fc["Attacker"] and int(fd[b]) == fc["Defender"], tag
+        assert (eng.flags() == 0).all()
+    finally:
+        eng.close()
+
+
+def _oracle_reset_skipping(env):
+    """Auto-reset of the device: a failing layout draw (the reference raises or
+    hangs) is skipped and the next draw of the same stream is taken."""
+    skipped = 0
+    while True:
+        try:
+            return env.reset(), skipped
+        except O.RoadGenError:
+            skipped += 1
+
+
+def test_vecenv_autoreset_vs_oracle():
+    """TDVecEnv with auto-reset over many short episodes (1-LP bases): the obs
+    returned for a finished board is its next episode's first obs, episode
+    return / length describe the finished episode, and failing layout draws are
+    skipped exactly as the oracle skips them."""
+    L, B, steps = 10, 96, 400
+    ov = dict(base_LP=1, defender_init_cost=0, defender_cost_rate=0.02)  # weak defence: ~5 episodes per board
+    cfg = O.Config(**ov)
+    seeds, orc = _first_ok_seeds(L, B, 4000, "def", False, 1, cfg)
+    with reference_settings(ov, False):
+        ve = E.TDVecEnv(L, B, "def", seed=0)
+    eng = ve.engine
+    eng.seed(np_seeds=seeds, py_seeds=seeds)
+    try:
+        obs = ve.reset().cpu().numpy()
+        for b, o in enumerate(orc):
+            assert np.array_equal(obs[b], o._board.get_states())
+        rets = np.zeros(B)
+        rng = np.random.RandomState(9)
+        resets = skipped = 0
+        for k in range(steps):
+            acts = np.array([policies.discrete_def(rng, L) for o in orc], dtype=np.int64)
+            obs_t, rew_t, done_t, infos = ve.step(torch.from_numpy(acts).cuda())
+            ob, rw, dn = obs_t.cpu().numpy(), rew_t.cpu().numpy(), done_t.cpu().numpy()
+            er, el = infos["episode_return"].cpu().numpy(), infos["episode_length"].cpu().numpy()
+            for b, o in enumerate(orc):
+                wo, wr, wd, _ = o.step(int(acts[b]))
+                rets[b] += wr
+                assert canon.fhex(rw[b]) == canon.fhex(wr), (k, b)
+                assert bool(dn[b]) == wd, (k, b)
+                if wd:
+                    assert canon.fhex(er[b]) == canon.fhex(rets[b]) and int(el[b]) == o._board.steps, (k, b)
+                    rets[b] = 0.0
+                    wo, s = _oracle_reset_skipping(o)
+                    skipped += s
+                    resets += 1
+                assert np.array_equal(ob[b], wo), (k, b, np.argwhere(ob[b] != wo)[:5].tolist())
+        assert resets > 3 * B  # several episodes per board
+        assert skipped > 0, "no failing layout draw was exercised; widen the run"
+        assert (eng.flags() == 0).all()
+    finally:
+        ve.close()
+
+
+@pytest.mark.parametrize("mode,multi", [("def", False), ("2p", True)])
+def test_vecenv_sharding_invariance(mode, multi):
+    """Board i of the global batch follows the same trajectory whether it is
+    stepped in one TDVecEnv of 64 boards or in the second of two shards of 32
+    (trajectories do not depend on the GPU count)."""
+    L, B, steps = 10, 64, 200
+    with reference_settings({"base_LP": 2}, multi):
+        whole = E.TDVecEnv(L, B, mode, seed=777)
+        parts = [E.TDVecEnv(L, B // 2, mode, seed=777, global_offset=r * (B // 2)) for r in range(2)]
+    try:
+        ow = whole.reset()
+        op = torch.cat([p.reset() for p in parts])
+        assert torch.equal(ow, op)
+        assert whole.roadgen_failures == sum(p.roadgen_failures for p in parts)
+        g = torch.Generator(device="cuda").manual_seed(3)
+        for k in range(steps):
+            if multi:
+                d = torch.randint(0, 3, (B, 6, L, L), device="cuda", generator=g, dtype=torch.int64)
+            else:
+                d = torch.randint(0, 6 * L * L + 1, (B,), device="cuda", generator=g, dtype=torch.int64)
+            a = torch.randint(0, 5, (B, 3, 8), device="cuda", generator=g, dtype=torch.int64)
+            act = (lambda lo, hi: d[lo:hi]) if mode == "def" else (lambda lo, hi: (d[lo:hi], a[lo:hi]))
+            ow, rw, dw, iw = whole.step(act(0, B))
+            res = [p.step(act(r * (B // 2), (r + 1) * (B // 2))) for r, p in enumerate(parts)]
+            assert torch.equal(ow, torch.cat([r[0] for r in res])), k
+            assert torch.equal(rw, torch.cat([r[1] for r in res])), k
+            assert torch.equal(dw, torch.cat([r[2] for r in res])), k
+            for key in ("episode_return", "episode_length", "Win"):
+                assert torch.equal(iw[key], torch.cat([r[3][key] for r in res])), (k, key)
+        sw = whole.engine.episode_stats().cpu().numpy()
+        sp = sum(p.engine.episode_stats().cpu().numpy() for p in parts)
+        assert sw[0] == sp[0] > 0
+        assert sw[1] == pytest.approx(sp[1], rel=1e-12, abs=1e-9)
+    finally:
+        whole.close()
+        for p in parts:
+            p.close()
