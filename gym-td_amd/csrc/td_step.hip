@@ -700,108 +700,42 @@ __device__ __forceinline__ float bitf(uint32_t m, int ch) { return (float)((m >>
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-// Channel-independent data of cells 4q .. 4q+3, kept in registers while a lane
-// sweeps the channels: the binary-channel bits and the channel-9 values.
-struct QuadData {
-  u32x4 bits;
-  f32x4 d9;
-};
-
-template <int NC>
-__device__ __forceinline__ QuadData quad_data(const Smem<NC>& S, int q) {
-  QuadData d;
-  const uint4 w = *reinterpret_cast<const uint4*>(&S.cell[4 * q]);
-  const uint32_t tw = *reinterpret_cast<const uint32_t*>(&S.twr[4 * q]);
-  d.bits = u32x4{cell_bits(w.x, tw & 0xffu), cell_bits(w.y, (tw >> 8) & 0xffu),
-                 cell_bits(w.z, (tw >> 16) & 0xffu), cell_bits(w.w, tw >> 24)};
-  d.d9 = f32x4{S.d9[cw_dist(w.x)], S.d9[cw_dist(w.y)], S.d9[cw_dist(w.z)], S.d9[cw_dist(w.w)]};
-  return d;
-}
-
 // Channel kinds of the observation (TDBoard.get_states, :112-143).
-enum ObsKind : int { OK_BIN, OK_CONST, OK_D9, OK_ENEMY, OK_NONE };
+enum ObsKind : int { OK_BIN, OK_CONST, OK_D9, OK_ENEMY };
 __host__ __device__ constexpr int obs_kind(int ch) {
-  return ch < 0 ? OK_NONE
-       : ch == 9 ? OK_D9
+  return ch == 9 ? OK_D9
        : (ch < 32 && ((kBinaryChannels >> ch) & 1u)) ? OK_BIN
        : (ch >= 25 && ch < 41) ? OK_ENEMY
        : OK_CONST;
 }
 
-// Channel ch of a lane's quad, for a channel kind K known at compile time (ch may
-// differ between lanes but is always of kind K).
-template <int K, int NC>
-__device__ __forceinline__ f32x4 obs_chan(const Smem<NC>& S, const QuadData& d, int ch, int q, bool any_enemy) {
-  if constexpr (K == OK_BIN) {
-    return __builtin_convertvector((d.bits >> (uint32_t)ch) & 1u, f32x4);
-  } else if constexpr (K == OK_D9) {
-    return d.d9;
-  } else if constexpr (K == OK_CONST) {  // 5, 10-13, 21-24, 41-44: one value for the whole plane
-    const float c = S.chv[ch];
-    return f32x4{c, c, c, c};
-  } else {
-    f32x4 v = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-    if (any_enemy) {  // wave-uniform
-      const int e = ch - 25, st = e >> 2, t = e & 3;
-      const uint32_t g4 = *reinterpret_cast<const uint32_t*>(&S.grp[t][4 * q]);
-      const uint32_t g0 = g4 & 0xffu, g1 = (g4 >> 8) & 0xffu, g2 = (g4 >> 16) & 0xffu, g3 = g4 >> 24;
-      // branch-free: read a clamped slot, keep it only where the cell has a group
-      const float f0 = S.gst[g0 & (ECAP - 1)][st], f1 = S.gst[g1 & (ECAP - 1)][st];
-      const float f2 = S.gst[g2 & (ECAP - 1)][st], f3 = S.gst[g3 & (ECAP - 1)][st];
-      v = f32x4{g0 != 0xffu ? f0 : 0.0f, g1 != 0xffu ? f1 : 0.0f, g2 != 0xffu ? f2 : 0.0f, g3 != 0xffu ? f3 : 0.0f};
-    }
-    return v;
-  }
-}
-
-// Channel ch (runtime) of a lane's quad.
+// Before the observation the cell words are replaced (in LDS) by what the planes
+// read of a cell: the binary-channel bits (cell_bits, bits 0-20) and the distance
+// to the end (bits 24-31) for channel 9.  The board's own cell words must have been
+// written back first (store_cells).
 template <int NC>
-__device__ __forceinline__ f32x4 obs_quad(const Smem<NC>& S, const QuadData& d, int ch, int q, bool any_enemy) {
-  switch (obs_kind(ch)) {
-    case OK_BIN: return obs_chan<OK_BIN>(S, d, ch, q, any_enemy);
-    case OK_D9: return obs_chan<OK_D9>(S, d, ch, q, any_enemy);
-    case OK_ENEMY: return obs_chan<OK_ENEMY>(S, d, ch, q, any_enemy);
-    default: return obs_chan<OK_CONST>(S, d, ch, q, any_enemy);
+__device__ __forceinline__ void pack_obs_cells(Smem<NC>& S, const Ctx& x) {
+  for (int i = x.lane; i < x.NCr; i += 64) {
+    const uint32_t w = S.cell[i];
+    S.cell[i] = cell_bits(w, S.twr[i]) | ((uint32_t)cw_dist(w) << 24);
   }
+  __syncthreads();
 }
 
 template <int NC>
 __device__ __forceinline__ float obs_value(const Smem<NC>& S, int ch, int cell, bool any_enemy) {
-  const uint32_t w = S.cell[cell];
-  if (ch < 32 && ((kBinaryChannels >> ch) & 1u)) return bitf(cell_bits(w, S.twr[cell]), ch);
-  if (ch == 9) return S.d9[cw_dist(w)];
-  if (ch >= 25 && ch < 41) {
-    if (!any_enemy) return 0.0f;
-    const int e = ch - 25;
-    const uint32_t g = S.grp[e & 3][cell];
-    return g == 0xFFu ? 0.0f : S.gst[g][e >> 2];
+  const uint32_t w = S.cell[cell];  // packed by pack_obs_cells
+  switch (obs_kind(ch)) {
+    case OK_BIN: return bitf(w, ch);
+    case OK_D9: return S.d9[w >> 24];
+    case OK_ENEMY: {
+      if (!any_enemy) return 0.0f;
+      const int e = ch - 25;
+      const uint32_t g = S.grp[e & 3][cell];
+      return g == 0xFFu ? 0.0f : S.gst[g][e >> 2];
+    }
+    default: return S.chv[ch];
   }
-  return S.chv[ch];
-}
-
-// Two channels written by one store instruction when a plane has <= 32 quads:
-// lanes of group 0 write channel A, lanes of group 1 channel B.  Pairs are of one
-// kind wherever possible so the wave executes one code path per store.
-template <int CA, int CB, int Q, int NC>
-__device__ __forceinline__ void obs_pair(const Smem<NC>& S, const QuadData& d, f32x4* o4, int q, int g,
-                                         bool any_enemy) {
-  constexpr int KA = obs_kind(CA), KB = obs_kind(CB);
-  f32x4 v;
-  int ch;
-  if constexpr (KB == OK_NONE) {
-    if (g) return;
-    ch = CA;
-    v = obs_chan<KA>(S, d, CA, q, any_enemy);
-  } else if constexpr (KA == KB) {
-    ch = g ? CB : CA;
-    v = obs_chan<KA>(S, d, ch, q, any_enemy);
-  } else {
-    ch = g ? CB : CA;
-    const f32x4 va = obs_chan<KA>(S, d, CA, q, any_enemy), vb = obs_chan<KB>(S, d, CB, q, any_enemy);
-    v = g ? vb : va;
-  }
-  o4[ch * Q + q] = v;
-  __builtin_amdgcn_sched_barrier(0);  // one channel in flight: keeps the VGPR count at the kernel's level
 }
 
 // Observation stores are non-temporal: 1.2 GB per launch written once and never
@@ -809,28 +743,52 @@ __device__ __forceinline__ void obs_pair(const Smem<NC>& S, const QuadData& d, f
 // every state load behind them waits on a write-back (measured: 16 % slower).
 __device__ __forceinline__ void obs_store(f32x4* p, f32x4 v) { __builtin_nontemporal_store(v, p); }
 
-// The (45, L, L) float32 observation, 16-byte stores.  Lanes own quads (four
-// cells) and keep the channel-independent data in registers.  With at most 32
-// quads per plane (L = 10: 25) floor(64 / quads) lane groups write that many
-// adjacent planes per store instruction, in plane order; otherwise lane l owns
-// quads l, l + 64, ... and each store covers up to 64 quads of one plane.
+// The (45, L, L) float32 observation of one board.  The wave writes the batch's
+// observation stream in 128-B-aligned 1-KB windows: store k covers the 16-B units
+// [A + 64k, A + 64k + 64) of the stream, A = the board's first unit rounded down to
+// a 128-B line, and lanes outside the board are masked off.  Every line is then
+// written whole by one instruction except the two the board shares with its
+// neighbours (a board is 18,000 B at L = 10, not a multiple of 128).  Non-temporal
+// stores of partial lines run at ~0.85x the rate of whole ones
+// (scripts/membench.hip: 4.3 vs 5.0-5.1 TB/s), so the channel-major walk of the
+// planes (800-B runs per store) is not line-aligned enough.  Lane unit i of the board
+// is channel i / Q, quad i % Q (Q = L*L/4 quads of 4 cells per plane).
 template <int NC, int LT>
 __device__ __forceinline__ void write_obs(const Smem<NC>& S, const Ctx& x, float* out, bool any_enemy) {
-  f32x4* o4 = reinterpret_cast<f32x4*>(out);
   const int ncr = LT ? LT * LT : x.NCr;
   if ((ncr & 3) == 0) {
-    const int Q = ncr / 4;
-    if (Q <= 32) {
-      const int G = 64 / Q, q = x.lane % Q, g = x.lane / Q;
-      if (g < G) {
-        const QuadData d = quad_data(S, q);
-        for (int ch = g; ch < NCH; ch += G) obs_store(o4 + ch * Q + q, obs_quad(S, d, ch, q, any_enemy));
+    const int Q = ncr / 4, n4 = NCH * Q;
+    f32x4* o4 = reinterpret_cast<f32x4*>(out);
+    const int mis = (int)((reinterpret_cast<uintptr_t>(o4) >> 4) & 7u);  // units of the line before the board
+    const uint4* cell4 = reinterpret_cast<const uint4*>(S.cell);
+    for (int i = x.lane - mis; i < n4; i += 64) {
+      if (i < 0) continue;
+      const int ch = i / Q, q = i - ch * Q;
+      const int kind = obs_kind(ch);
+      f32x4 v;
+      if (kind == OK_BIN) {
+        const uint4 w = cell4[q];
+        const uint32_t c = (uint32_t)ch;
+        v = f32x4{(float)((w.x >> c) & 1u), (float)((w.y >> c) & 1u), (float)((w.z >> c) & 1u),
+                  (float)((w.w >> c) & 1u)};
+      } else if (kind == OK_CONST) {
+        const float c = S.chv[ch];
+        v = f32x4{c, c, c, c};
+      } else if (kind == OK_D9) {
+        const uint4 w = cell4[q];
+        v = f32x4{S.d9[w.x >> 24], S.d9[w.y >> 24], S.d9[w.z >> 24], S.d9[w.w >> 24]};
+      } else if (any_enemy) {  // wave-uniform
+        const int e = ch - 25, st = e >> 2, t = e & 3;
+        const uint32_t g4 = *reinterpret_cast<const uint32_t*>(&S.grp[t][4 * q]);
+        const uint32_t g0 = g4 & 0xffu, g1 = (g4 >> 8) & 0xffu, g2 = (g4 >> 16) & 0xffu, g3 = g4 >> 24;
+        // branch-free: read a clamped slot, keep it only where the cell has a group
+        const float f0 = S.gst[g0 & (ECAP - 1)][st], f1 = S.gst[g1 & (ECAP - 1)][st];
+        const float f2 = S.gst[g2 & (ECAP - 1)][st], f3 = S.gst[g3 & (ECAP - 1)][st];
+        v = f32x4{g0 != 0xffu ? f0 : 0.0f, g1 != 0xffu ? f1 : 0.0f, g2 != 0xffu ? f2 : 0.0f, g3 != 0xffu ? f3 : 0.0f};
+      } else {
+        v = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
       }
-    } else {
-      for (int q = x.lane; q < Q; q += 64) {
-        const QuadData d = quad_data(S, q);
-        for (int ch = 0; ch < NCH; ++ch) obs_store(o4 + ch * Q + q, obs_quad(S, d, ch, q, any_enemy));
-      }
+      obs_store(o4 + i, v);
     }
   } else {
     const int nf = NCH * ncr;
@@ -931,6 +889,15 @@ __device__ void reset_board(Smem<NC>& S, U& u, const Ctx& x, const uint32_t* rec
   __syncthreads();
 }
 
+// Cell words back to HBM when map[6] changed or a new layout was loaded (before
+// pack_obs_cells reuses the LDS copy).
+template <int NC>
+__device__ __forceinline__ void store_cells(const Smem<NC>& S, const U& u, const Ctx& x, const StepArgs& a, int b) {
+  const size_t cb = (size_t)b * x.NCr;
+  if (u.cells_dirty)
+    for (int i = x.lane; i < x.NCr; i += 64) a.cells[cb + i] = S.cell[i];
+}
+
 template <int NC>
 __device__ void store_board(const Smem<NC>& S, const U& u, const Ctx& x, const StepArgs& a, int b) {
   if (x.lane == 0) {
@@ -943,10 +910,8 @@ __device__ void store_board(const Smem<NC>& S, const U& u, const Ctx& x, const S
     h.pad[0] = h.pad[1] = h.pad[2] = h.pad[3] = 0;
     a.hdr[b] = h;
   }
-  const size_t tb = (size_t)b * TCAP, cb = (size_t)b * x.NCr;
-  if (u.cells_dirty)
-    for (int i = x.lane; i < x.NCr; i += 64) a.cells[cb + i] = S.cell[i];
-  // enemies were written back at the end of board_step
+  const size_t tb = (size_t)b * TCAP;
+  // cells were written back by store_cells, enemies at the end of board_step
   if (x.lane < u.nt) { a.tw_cd[tb + x.lane] = S.tCd[x.lane]; a.tw_inf[tb + x.lane] = S.tInf[x.lane]; }
 }
 
@@ -1211,6 +1176,8 @@ __device__ void step_board(Smem<NC>& S, const Ctx& x, const StepArgs& a, int b, 
   STAMP(5);
   enemy_stats(S, u, x);  // no-op for a board without enemies (e.g. just reset)
   channel_scalars(S, u, x);
+  store_cells(S, u, x, a, b);
+  pack_obs_cells(S, x);
   STAMP(6);
   write_obs<NC, LT>(S, x, obs, u.n > 0);
   STAMP(7);
@@ -1355,6 +1322,8 @@ __global__ __launch_bounds__(64) void td_reset_kernel(StepArgs a) {
   u.flags = 0;
   reset_board(S, u, x, rec);
   channel_scalars(S, u, x);
+  store_cells(S, u, x, a, b);
+  pack_obs_cells(S, x);
   if (a.obs) write_obs<NC, LT>(S, x, a.obs + (size_t)b * NCH * x.NCr, false);
   store_board(S, u, x, a, b);
   if (x.lane == 0) {

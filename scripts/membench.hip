@@ -119,12 +119,122 @@ __global__ __launch_bounds__(64) void mixed_t(f32x4* out, f32x4* st, int B) {
   if (lane < 24) sb[lane] = r0;
 }
 
+
+// (j) 256-thread workgroups, one wave per board (4 boards per workgroup), nt stores
+__global__ __launch_bounds__(256) void flat4_nt(f32x4* out, int B) {
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (b >= B) return;
+  f32x4* o = out + (size_t)b * BOARD_F4;
+  for (int i = lane; i < BOARD_F4; i += 64) __builtin_nontemporal_store(f32x4{(float)i, 1.f, 2.f, 3.f}, o + i);
+}
+
+// (k) persistent waves: grid-stride over boards, nt stores
+__global__ __launch_bounds__(64) void persist_nt(f32x4* out, int B) {
+  const int lane = threadIdx.x;
+  for (int b = blockIdx.x; b < B; b += gridDim.x) {
+    f32x4* o = out + (size_t)b * BOARD_F4;
+    for (int i = lane; i < BOARD_F4; i += 64) __builtin_nontemporal_store(f32x4{(float)i, 1.f, 2.f, 3.f}, o + i);
+  }
+}
+
+// (l) stream with nt stores
+__global__ __launch_bounds__(256) void stream_nt(f32x4* out, size_t n) {
+  for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
+    __builtin_nontemporal_store(f32x4{(float)i, 1.f, 2.f, 3.f}, out + i);
+}
+
+// (m) one wave per board, boards padded to 128-B aligned starts (18,048 B stride)
+constexpr int BOARD_F4_PAD = 1128;
+__global__ __launch_bounds__(64) void flat_nt_al(f32x4* out, int B) {
+  const int b = blockIdx.x, lane = threadIdx.x;
+  if (b >= B) return;
+  f32x4* o = out + (size_t)b * BOARD_F4_PAD;
+  for (int i = lane; i < BOARD_F4; i += 64) __builtin_nontemporal_store(f32x4{(float)i, 1.f, 2.f, 3.f}, o + i);
+}
+
+// (n) one wave per TWO boards (36,000 contiguous bytes), nt
+__global__ __launch_bounds__(64) void flat2_nt(f32x4* out, int B) {
+  const int b = blockIdx.x * 2, lane = threadIdx.x;
+  if (b >= B) return;
+  f32x4* o = out + (size_t)b * BOARD_F4;
+  for (int i = lane; i < 2 * BOARD_F4; i += 64) __builtin_nontemporal_store(f32x4{(float)i, 1.f, 2.f, 3.f}, o + i);
+}
+
+// (o) flat, plain stores, 256-thread blocks 4 boards
+__global__ __launch_bounds__(256) void flat4(f32x4* out, int B) {
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (b >= B) return;
+  f32x4* o = out + (size_t)b * BOARD_F4;
+  for (int i = lane; i < BOARD_F4; i += 64) o[i] = f32x4{(float)i, 1.f, 2.f, 3.f};
+}
+
+// (p) one wave per board, nt stores in 128-B-aligned 1-KB windows of the batch's
+// stream: only the two lines a board shares with its neighbours are partial
+__global__ __launch_bounds__(64) void flat_nt_shift(f32x4* out, int B) {
+  const int b = blockIdx.x, lane = threadIdx.x;
+  if (b >= B) return;
+  const long lo = (long)b * BOARD_F4, hi = lo + BOARD_F4, a0 = lo & ~7l;
+  for (long g = a0 + lane; g < hi; g += 64)
+    if (g >= lo) __builtin_nontemporal_store(f32x4{(float)g, 1.f, 2.f, 3.f}, out + g);
+}
+
+// (q) pairs pattern, nt, boards at 128-B-aligned starts
+__global__ __launch_bounds__(64) void pairs_nt_al(f32x4* out, int B) {
+  const int b = blockIdx.x, lane = threadIdx.x, q = lane % Q, g = lane / Q;
+  if (b >= B || g >= 2) return;
+  f32x4* o = out + (size_t)b * BOARD_F4_PAD;
+  for (int i = 0; i < 23; ++i) {
+    const int ch = 2 * i + g;
+    if (ch < NCH) __builtin_nontemporal_store(f32x4{(float)ch, 1.f, 2.f, 3.f}, o + ch * Q + q);
+  }
+}
+
+// (r) pairs pattern, plain, boards at 128-B-aligned starts
+__global__ __launch_bounds__(64) void pairs_al(f32x4* out, int B) {
+  const int b = blockIdx.x, lane = threadIdx.x, q = lane % Q, g = lane / Q;
+  if (b >= B || g >= 2) return;
+  f32x4* o = out + (size_t)b * BOARD_F4_PAD;
+  for (int i = 0; i < 23; ++i) {
+    const int ch = 2 * i + g;
+    if (ch < NCH) o[ch * Q + q] = f32x4{(float)ch, 1.f, 2.f, 3.f};
+  }
+}
+
+// (s) = (p) with the step's state traffic: 3 KB read first, 384 B written back
+__global__ __launch_bounds__(64) void mixed_shift(f32x4* out, f32x4* st, int B) {
+  const int b = blockIdx.x, lane = threadIdx.x;
+  if (b >= B) return;
+  f32x4* sb = st + (size_t)b * 192;
+  const f32x4 r0 = sb[lane], r1 = sb[64 + lane], r2 = sb[128 + lane];
+  const float v = r0.x + r1.y + r2.z;
+  const long lo = (long)b * BOARD_F4, hi = lo + BOARD_F4, a0 = lo & ~7l;
+  for (long g = a0 + lane; g < hi; g += 64)
+    if (g >= lo) __builtin_nontemporal_store(f32x4{v, 1.f, 2.f, (float)g}, out + g);
+  if (lane < 24) sb[lane] = r0 + r1;
+}
+
+// (t) = mixed (pairs, plain) but nt
+__global__ __launch_bounds__(64) void mixed_nt(f32x4* out, f32x4* st, int B) {
+  const int b = blockIdx.x, lane = threadIdx.x, q = lane % Q, g = lane / Q;
+  if (b >= B) return;
+  f32x4* sb = st + (size_t)b * 192;
+  const f32x4 r0 = sb[lane], r1 = sb[64 + lane], r2 = sb[128 + lane];
+  const float v = r0.x + r1.y + r2.z;
+  f32x4* o = out + (size_t)b * BOARD_F4;
+  if (g < 2)
+    for (int i = 0; i < 23; ++i) {
+      const int ch = 2 * i + g;
+      if (ch < NCH) __builtin_nontemporal_store(f32x4{v, 1.f, 2.f, (float)ch}, o + ch * Q + q);
+    }
+  if (lane < 24) sb[lane] = r0 + r1;
+}
+
 int main(int argc, char** argv) {
   const int B = argc > 1 ? atoi(argv[1]) : 65536;
   const size_t n4 = (size_t)B * BOARD_F4, bytes = n4 * 16;
   f32x4* out;
   int* in;
-  CK(hipMalloc(&out, bytes));
+  CK(hipMalloc(&out, bytes + (size_t)B * 48 + 4096));
   CK(hipMalloc(&in, (size_t)B * 64 * 4));
   CK(hipMemset(in, 0, (size_t)B * 64 * 4));
   f32x4* st;
@@ -163,6 +273,21 @@ int main(int argc, char** argv) {
   run("m_r1_s2k", [&] { hipLaunchKernelGGL((mixed_t<1, 6304, 2000>), dim3(B), dim3(64), 0, 0, out, st, B); });
   run("m_r1_s4k", [&] { hipLaunchKernelGGL((mixed_t<1, 6304, 4000>), dim3(B), dim3(64), 0, 0, out, st, B); });
   run("stream", [&] { hipLaunchKernelGGL(stream, dim3(4096), dim3(256), 0, 0, out, n4); });
+  run("stream_nt", [&] { hipLaunchKernelGGL(stream_nt, dim3(4096), dim3(256), 0, 0, out, n4); });
+  run("stream_nt16k", [&] { hipLaunchKernelGGL(stream_nt, dim3(16384), dim3(256), 0, 0, out, n4); });
+  run("flat4_nt", [&] { hipLaunchKernelGGL(flat4_nt, dim3((B + 3) / 4), dim3(256), 0, 0, out, B); });
+  run("flat4", [&] { hipLaunchKernelGGL(flat4, dim3((B + 3) / 4), dim3(256), 0, 0, out, B); });
+  run("persist2k", [&] { hipLaunchKernelGGL(persist_nt, dim3(2048), dim3(64), 0, 0, out, B); });
+  run("persist8k", [&] { hipLaunchKernelGGL(persist_nt, dim3(8192), dim3(64), 0, 0, out, B); });
+  run("flat_nt_al", [&] { hipLaunchKernelGGL(flat_nt_al, dim3(B), dim3(64), 0, 0, out, B); });
+  run("flat_nt_shift", [&] { hipLaunchKernelGGL(flat_nt_shift, dim3(B), dim3(64), 0, 0, out, B); });
+  run("pairs_nt_al", [&] { hipLaunchKernelGGL(pairs_nt_al, dim3(B), dim3(64), 0, 0, out, B); });
+  run("pairs_al", [&] { hipLaunchKernelGGL(pairs_al, dim3(B), dim3(64), 0, 0, out, B); });
+  run("mixed_shift", [&] { hipLaunchKernelGGL(mixed_shift, dim3(B), dim3(64), 0, 0, out, st, B); });
+  run("mixed_nt", [&] { hipLaunchKernelGGL(mixed_nt, dim3(B), dim3(64), 0, 0, out, st, B); });
+  run("flat_nt2", [&] { hipLaunchKernelGGL(flat_nt, dim3(B), dim3(64), 0, 0, out, B); });
+  run("flat_nt_al2", [&] { hipLaunchKernelGGL(flat_nt_al, dim3(B), dim3(64), 0, 0, out, B); });
+  run("flat2_nt", [&] { hipLaunchKernelGGL(flat2_nt, dim3(B / 2), dim3(64), 0, 0, out, B); });
   CK(hipFree(out));
   CK(hipFree(in));
   return 0;
