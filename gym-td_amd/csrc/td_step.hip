@@ -308,31 +308,65 @@ __device__ int defender_op(Smem<NC>& S, U& u, const Ctx& x, int op, int cell) {
 }
 
 // Multi-action defender: the serial (r, c, t) scan of TDDefense.py:42-60 /
-// TDMulti.py:209-227.  Cells where no operation can change the board are skipped:
-// per 64-cell chunk a ballot marks the cells whose flagged build / lvup / destruct
-// would succeed in the CURRENT state, the first such cell runs the reference's
-// exact serial sequence, and the ballot is recomputed.  Skipped cells would only
-// have produced failures, which leave no trace in multi-action mode.
+// TDMulti.py:209-227.  The (6, L, L) int64 flags are read first with 16-B loads
+// (8 in flight per lane) and folded into one 6-bit flag byte per cell in LDS (the
+// group map grp[0], unused until enemy_stats).  Cells where no operation can change
+// the board are skipped: per 64-cell chunk a ballot marks the cells whose flagged
+// build / lvup / destruct would succeed in the CURRENT state, the first such cell
+// runs the reference's exact serial sequence, and the ballot is recomputed.
+// Skipped cells would only have produced failures, which leave no trace in
+// multi-action mode.  The real actions (grp[1]) go out as int64 (6, L, L) in
+// 128-B-aligned windows, like the observation.
 template <int NC>
 __device__ void defender_scan(Smem<NC>& S, U& u, const Ctx& x, const int64_t* A, int64_t* R, bool active) {
   const TdDevCfg& C = x.C;
-  for (int base = 0; base < x.NCr; base += 64) {
-    const int cell = base + x.lane;
-    const bool valid = cell < x.NCr;
-    uint32_t fl = 0;
-    bool bad = false;
-    if (valid) {
+  const int ncr = x.NCr, n = 6 * ncr;
+  uint8_t* flag = &S.grp[0][0];
+  uint8_t* real = &S.grp[1][0];
+  uint32_t* fw = reinterpret_cast<uint32_t*>(flag);
+  for (int i = x.lane; i < (2 * NC) / 4; i += 64) fw[i] = 0u;  // grp[0] and grp[1]
+  __syncthreads();
+  bool bad = false;
+  if ((ncr & 1) == 0) {  // 16-B units of two cells of one plane
+    typedef long long i64x2 __attribute__((ext_vector_type(2)));
+    const i64x2* A2 = reinterpret_cast<const i64x2*>(A);
+    const int n2 = n / 2;
+    constexpr int K = 8;
+    for (int base = 0; base < n2; base += 64 * K) {
+      i64x2 v[K];
 #pragma unroll
-      for (int ch = 0; ch < 6; ++ch) {
-        int64_t v = A[(size_t)ch * x.NCr + cell];
-        if (v == 1) fl |= 1u << ch;
-        if (v < 0 || v > 2) bad = true;
+      for (int k = 0; k < K; ++k) {
+        const int e = base + 64 * k + x.lane;
+        v[k] = e < n2 ? __builtin_nontemporal_load(A2 + e) : i64x2{0, 0};
+      }
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const int e = base + 64 * k + x.lane;
+        if (e < n2) {
+          const int pl = (2 * e) / ncr, c = 2 * e - pl * ncr;
+          bad |= (unsigned long long)v[k].x > 2ull || (unsigned long long)v[k].y > 2ull;
+          const uint32_t bits = ((v[k].x == 1 ? 1u : 0u) << (8 * (c & 3)) | (v[k].y == 1 ? 1u : 0u) << (8 * ((c + 1) & 3)))
+                                << pl;
+          if (bits) atomicOr(&fw[c >> 2], bits);
+        }
       }
     }
-    if (ballot(bad)) u.flags |= FLAG_BAD_ACTION;
-    uint32_t rl = 0;
+  } else {
+    for (int e = x.lane; e < n; e += 64) {
+      const int64_t v = A[e];
+      const int pl = e / ncr, c = e - pl * ncr;
+      bad |= v < 0 || v > 2;
+      if (v == 1) atomicOr(&fw[c >> 2], (1u << pl) << (8 * (c & 3)));
+    }
+  }
+  if (ballot(bad)) u.flags |= FLAG_BAD_ACTION;
+  __syncthreads();
+  for (int base = 0; base < ncr && active; base += 64) {
+    const int cell = base + x.lane;
+    const bool valid = cell < ncr;
+    const uint32_t fl = valid ? flag[cell] : 0u;
     int last = -1;
-    while (active) {
+    while (true) {
       bool cand = false;
       if (valid && fl && x.lane > last) {
         uint32_t w = S.cell[cell];
@@ -362,12 +396,27 @@ __device__ void defender_scan(Smem<NC>& S, U& u, const Ctx& x, const int64_t* A,
         if (tower_lvup(S, u, x, c) == FC_OK) { rb |= 16u; u.def_cd = C.def_interval; }
       if ((f >> 5) & 1u)
         if (tower_destruct(S, u, x, c) == FC_OK) { rb |= 32u; u.def_cd = C.def_interval; }
-      if (x.lane == j) rl = rb;
+      if (x.lane == j) real[c] = (uint8_t)rb;
       last = j;
     }
-    if (R && valid) {
-#pragma unroll
-      for (int ch = 0; ch < 6; ++ch) R[(size_t)ch * x.NCr + cell] = (rl >> ch) & 1u;
+  }
+  __syncthreads();
+  if (R) {
+    if ((ncr & 1) == 0) {
+      typedef long long i64x2 __attribute__((ext_vector_type(2)));
+      i64x2* R2 = reinterpret_cast<i64x2*>(R);
+      const int n2 = n / 2, mis = (int)((reinterpret_cast<uintptr_t>(R2) >> 4) & 7u);
+      for (int e = x.lane - mis; e < n2; e += 64) {
+        if (e < 0) continue;
+        const int pl = (2 * e) / ncr, c = 2 * e - pl * ncr;
+        const uint32_t r2 = *reinterpret_cast<const uint16_t*>(real + c);
+        __builtin_nontemporal_store(i64x2{(long long)((r2 >> pl) & 1u), (long long)((r2 >> (8 + pl)) & 1u)}, R2 + e);
+      }
+    } else {
+      for (int e = x.lane; e < n; e += 64) {
+        const int pl = e / ncr;
+        R[e] = (real[e - pl * ncr] >> pl) & 1u;
+      }
     }
   }
 }
