@@ -25,7 +25,8 @@ timing all-reduce and the episode-stat gather after the timed region.
 
 One JSON line on rank 0: metric/value/unit, ``roofline`` for the step kernel
 (HIP events on the launch stream, algorithmic bytes per launch) and
-``cpu_baseline`` (the oracle port timed on this host's cores, rank 0, N=1).
+``cpu_baseline`` (the C restatement oracle/td_cpu.c on this host's cores, rank 0,
+N=1; ``cpu_baseline_python`` times the Python restatement the same way).
 """
 import argparse
 import json
@@ -104,7 +105,8 @@ def _cpu_worker(args):
     return n, time.perf_counter() - t0
 
 
-def cpu_baseline(L, mode, multi, seconds, procs, workload):
+def cpu_baseline_python(L, mode, multi, seconds, procs, workload):
+    """The Python restatement (oracle/td_oracle.py), one process per core."""
     with mp.get_context("spawn").Pool(procs) as pool:
         res = pool.map(_cpu_worker, [(L, mode, multi, seconds, 90001 + i) for i in range(procs)])
     steps = sum(r[0] for r in res)
@@ -112,6 +114,18 @@ def cpu_baseline(L, mode, multi, seconds, procs, workload):
     return {"value": steps / wall, "unit": "env-steps/s", "cores": procs, "kind": "port",
             "sample": "oracle/td_oracle.py (Python restatement of the reference step, parity-pinned) %s "
                       "random actions, %d processes x %.0f s, %d env-steps" % (workload, procs, seconds, steps)}
+
+
+def cpu_baseline(L, mode, multi, seconds, threads, workload):
+    """The plain-C restatement (oracle/td_cpu.c, golden-pinned), OpenMP over the host
+    cores: 16 envs per thread, random actions, auto-reset, every observation built."""
+    from oracle import td_cpu
+    n_envs = 16 * threads
+    steps, wall = td_cpu.bench(L, mode, multi, n_envs, seconds, threads)
+    return {"value": steps / wall, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "sample": "oracle/td_cpu.c (C restatement of the reference step, pinned by the golden vectors) %s, "
+                      "%d envs on %d OpenMP threads x %.0f s, random actions, auto-reset, %d env-steps"
+                      % (workload, n_envs, threads, seconds, steps)}
 
 
 def host_cores():
@@ -133,7 +147,8 @@ def main():
     ap.add_argument("--burnin", type=int, default=1200)
     ap.add_argument("--stagger", type=int, default=1, help="stagger episode phases during burn-in (see docstring)")
     ap.add_argument("--seed", type=int, default=0)
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--py-cpu-seconds", type=float, default=5.0, help="Python restatement leg (0 = skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--autoreset", type=int, default=1, help="diagnostic: 0 keeps finished boards stepping (not the metric)")
     args = ap.parse_args()
@@ -253,6 +268,9 @@ def main():
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(L, mode, multi, args.cpu_seconds, host_cores(), args.workload)
+            if args.py_cpu_seconds > 0:
+                out["cpu_baseline_python"] = cpu_baseline_python(L, mode, multi, args.py_cpu_seconds, host_cores(),
+                                                                 args.workload)
         print(json.dumps(out), flush=True)
     eng.close()
     if world > 1:
