@@ -354,10 +354,7 @@ int td_set_autoreset(td_handle* h, int on) {
 
 int td_seed(td_handle* h, const uint32_t* np_seeds, const uint32_t* py_seeds) {
   if (!h) return fail("NULL handle");
-  const size_t B = (size_t)h->B, W = MT_N + 1;
-  std::vector<uint32_t> st(B * W);
-  (void)st;
-  (void)W;
+  const size_t B = (size_t)h->B;
   if (np_seeds) {
     std::vector<uint32_t> nw(B * OPP_WORDS);
     parallel_for((int)B, [&](int b) {

@@ -790,7 +790,11 @@ __device__ __forceinline__ float obs_value(const Smem<NC>& S, int ch, int cell, 
 // Observation stores are non-temporal: 1.2 GB per launch written once and never
 // read back by the kernel; as plain stores the dirty lines fill the XCD L2s and
 // every state load behind them waits on a write-back (measured: 16 % slower).
+#ifdef TD_OBS_PLAIN  // A/B diagnostic builds only
+__device__ __forceinline__ void obs_store(f32x4* p, f32x4 v) { *p = v; }
+#else
 __device__ __forceinline__ void obs_store(f32x4* p, f32x4 v) { __builtin_nontemporal_store(v, p); }
+#endif
 
 // The (45, L, L) float32 observation of one board.  The wave writes the batch's
 // observation stream in 128-B-aligned 1-KB windows: store k covers the 16-B units
