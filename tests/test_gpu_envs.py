@@ -217,3 +217,134 @@ def test_vecenv_sharding_invariance(mode, multi):
         whole.close()
         for p in parts:
             p.close()
+
+
+def test_reset_layouts_uses_caller_records():
+    """td_reset_layouts: boards restart from caller-supplied layout records (here the
+    host restatement's first draw of each board's stream) without touching the
+    streams or the staged rings; the result equals a plain reset() of the same seeds."""
+    from gym_TD.engine import generate_layout
+    L, B = 10, 16
+    seeds, _ = _first_ok_seeds(L, B, 5000, "def", False, 1)
+    ref = TDEngine(L, B, "def", False, 1, np_seeds=seeds, py_seeds=seeds, autoreset=True)
+    eng = TDEngine(L, B, "def", False, 1, np_seeds=seeds, py_seeds=seeds, autoreset=True)
+    try:
+        want, failed = ref.reset()
+        assert not failed
+        want = want.clone()
+        before = [eng.get_np_state(b).copy() for b in range(B)]
+        recs = []
+        for s in seeds:
+            st = np.random.RandomState(s).get_state()
+            w = np.array(list(st[1]) + [int(st[2])], dtype=np.uint32)
+            status, rec = generate_layout(w, L)
+            assert status == 0
+            recs.append(rec)
+        obs = eng.reset_layouts(np.stack(recs), np.arange(B))
+        assert torch.equal(obs, want)
+        for b in range(B):
+            assert eng.get_np_state(b).tolist() == before[b].tolist()
+            assert canon.state_digest(eng.board_state(b)) == canon.state_digest(ref.board_state(b))
+        # both keep stepping identically (the same opponent streams, auto-reset from the rings)
+        g = torch.Generator(device="cuda").manual_seed(11)
+        for k in range(50):
+            a = torch.randint(0, 6 * L * L + 1, (B,), device="cuda", generator=g, dtype=torch.int64)
+            ref.step(def_act=a)
+            eng.step(def_act=a)
+            assert torch.equal(ref.obs, eng.obs) and torch.equal(ref.reward, eng.reward), k
+    finally:
+        ref.close()
+        eng.close()
+
+
+def test_export_import_roundtrip():
+    """td_export_state / td_import_state carry a board's whole step state (lists,
+    costs, cool-downs, map[6], the opponent stream): an engine loaded from another's
+    export continues bit-identically."""
+    L, B = 10, 24
+    seeds, _ = _first_ok_seeds(L, B, 6000, "def", False, 1)
+    a_eng = TDEngine(L, B, "def", False, 1, np_seeds=seeds, py_seeds=seeds, autoreset=False)
+    b_eng = TDEngine(L, B, "def", False, 1, np_seeds=[s + 1 for s in seeds], py_seeds=[s + 7 for s in seeds],
+                     autoreset=False)
+    try:
+        a_eng.reset()
+        b_eng.reset()
+        rng = np.random.RandomState(4)
+        for k in range(120):
+            a_eng.step(def_act=torch.from_numpy(rng.randint(0, 6 * L * L + 1, size=B).astype(np.int64)))
+        b_eng.import_state(a_eng.export_state())
+        for b in range(B):
+            assert canon.state_digest(b_eng.board_state(b)) == canon.state_digest(a_eng.board_state(b))
+        for k in range(120):
+            act = torch.from_numpy(rng.randint(0, 6 * L * L + 1, size=B).astype(np.int64))
+            a_eng.step(def_act=act)
+            b_eng.step(def_act=act)
+            assert torch.equal(a_eng.obs, b_eng.obs) and torch.equal(a_eng.reward, b_eng.reward), k
+            assert torch.equal(a_eng.done, b_eng.done), k
+    finally:
+        a_eng.close()
+        b_eng.close()
+
+
+def test_paramconfig_reaches_live_engines():
+    """paramConfig (TDParam.py:98-100) re-uploads the constant block of live engines.
+    The reference's enemies and towers keep the values they captured when created, so
+    the comparison restarts both sides on fresh episodes (same streams) after the call:
+    from there the device follows the oracle under the new values."""
+    import gym_TD
+    from gym_TD import params as P
+    L, B = 10, 8
+    ov = dict(reward_time=0.004, tower_range=[[4, 4], [3, 3], [5, 5], [4, 4]],
+              enemy_speed=[[.2, .2], [.2, .2], [.15, .15], [.1, .1]], defender_init_cost=30)
+    seeds, orc = _first_ok_seeds(L, B, 7000, "def", False, 1)
+    saved = {k: getattr(P.config, k) for k in ov}
+    eng = TDEngine(L, B, "def", False, 1, np_seeds=seeds, py_seeds=seeds, autoreset=False)
+    try:
+        eng.reset()
+        rng = np.random.RandomState(8)
+        for k in range(90):
+            if k == 30:
+                gym_TD.paramConfig(**ov)
+                for o in orc:
+                    for key, v in ov.items():
+                        setattr(o.cfg, key, v)
+                    o.reset()
+                _, failed = eng.reset()
+                assert not failed
+            acts = np.array([policies.discrete_def(rng, L, o._board.map[0], 0.5) for o in orc], dtype=np.int64)
+            eng.step(def_act=torch.from_numpy(acts))
+            ob, rw = eng.obs.cpu().numpy(), eng.reward.cpu().numpy()
+            st = eng.export_state()
+            for b, o in enumerate(orc):
+                wo, wr, _, _ = o.step(int(acts[b]))
+                assert canon.fhex(rw[b]) == canon.fhex(wr), (k, b)
+                assert canon.state_digest(eng.board_state(b, st)) == canon.state_digest(canon.oracle_state(o)), (k, b)
+                assert np.array_equal(ob[b], wo), (k, b)
+    finally:
+        gym_TD.paramConfig(**saved)
+        eng.close()
+
+
+def test_capacity_overflow_is_flagged():
+    """A config that summons past the 128-enemy cap (SURVEY a12 bounds the default
+    config at 121) sets FLAG_EN_OVERFLOW and refuses the extra summons instead of
+    corrupting the board."""
+    from test_gpu_parity import reference_settings
+    L, B = 10, 4
+    ov = dict(attacker_init_cost=200, max_cost=200, enemy_cost=[[1, 1], [1, 1], [1, 1], [1, 1]],
+              enemy_speed=[[.01, .01], [.01, .01], [.01, .01], [.01, .01]], defender_init_cost=0, defender_cost_rate=0)
+    seeds, _ = _first_ok_seeds(L, B, 8000, "def", False, 1)
+    with reference_settings(ov, False):
+        eng = TDEngine(L, B, "def", False, 1, np_seeds=seeds, py_seeds=seeds, autoreset=False)
+    try:
+        eng.reset()
+        empty = torch.full((B,), 6 * L * L, dtype=torch.int64, device="cuda")
+        for k in range(40):
+            eng.step(def_act=empty)
+        fl = eng.flags()
+        assert (fl & 1).all(), fl
+        for b in range(B):
+            assert len(eng.board_state(b)["enemies"]) == 128
+        assert bool(torch.isfinite(eng.obs).all())  # count/8 planes exceed 1 here, as in the reference
+    finally:
+        eng.close()
