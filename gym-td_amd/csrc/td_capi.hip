@@ -43,7 +43,8 @@ int fail(const char* fmt, ...) {
     if (e_ != hipSuccess) return fail("%s: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, __LINE__); \
   } while (0)
 
-constexpr int kRefillEvery = 8;  // steps between refill launches (a board consumes <= 1 layout per ~40 steps)
+constexpr int kRefillEvery = 1;  // steps between refill launches (when a side stream is free)
+constexpr int kSideStreams = 2;  // refills in flight at once: one stuck on a long draw does not stall the next
 
 }  // namespace
 
@@ -58,17 +59,19 @@ struct td_handle {
   uint32_t *d_en_inf = nullptr, *d_tw_inf = nullptr, *d_cells = nullptr, *d_opp = nullptr, *d_np = nullptr;
   uint32_t* d_hot = nullptr;  // opponent hot record [B][HOT_WORDS]
   uint32_t *d_nxt = nullptr, *d_stage = nullptr;  // staged-layout rings [B][NSLOT][slot_words]; caller records
-  uint32_t *d_lay_head = nullptr, *d_lay_tail = nullptr;  // ring counters (td_kernels.h)
+  uint32_t *d_lay_head = nullptr, *d_lay_tail = nullptr, *d_lay_claim = nullptr;  // rings (td_kernels.h)
   int32_t* d_ovr_idx = nullptr;                           // td_reset_layouts: [B] index into d_stage or -1
   uint8_t *d_scratch = nullptr, *d_mask = nullptr, *d_fail = nullptr;
   int stage_cap = 0;
   uint64_t* d_stamps = nullptr;  // TD_STAMPS diagnostic builds only (not owned)
   double* d_epstats = nullptr;   // [2] finished episodes, sum of their returns
-  // Layout refills run on a side stream, at most one in flight; the step stream
-  // never waits for them (the rings give every board two episodes of slack).
-  hipStream_t side = nullptr;
-  hipEvent_t ev_main = nullptr, ev_refill = nullptr;
-  bool refill_inflight = false;
+  // Layout refills run on kSideStreams side streams, at most one in flight on each;
+  // the step stream never waits for them (the rings give every board NSLOT
+  // episodes of slack, and per-board claims keep concurrent refills apart).
+  hipStream_t side[kSideStreams] = {};
+  hipEvent_t ev_main = nullptr, ev_refill[kSideStreams] = {};
+  bool refill_inflight[kSideStreams] = {};
+  int next_side = 0;
   long long steps = 0;
   std::vector<int32_t> last_reset_failed;
 };
@@ -147,7 +150,8 @@ StepArgs base_args(td_handle* h) {
   a.hdr = h->d_hdr; a.en_lp = h->d_en_lp; a.en_mg = h->d_en_mg; a.en_inf = h->d_en_inf;
   a.tw_cd = h->d_tw_cd; a.tw_inf = h->d_tw_inf; a.cells = h->d_cells; a.opp_mt = h->d_opp; a.opp_hot = h->d_hot;
   a.np_mt = h->d_np; a.nxt = h->d_nxt; a.scratch = h->d_scratch; a.scratch_stride = h->scratch_stride;
-  a.lay_head = h->d_lay_head; a.lay_tail = h->d_lay_tail; a.slot_words = slot_words(h->L);
+  a.lay_head = h->d_lay_head; a.lay_tail = h->d_lay_tail; a.lay_claim = h->d_lay_claim;
+  a.slot_words = slot_words(h->L);
   a.reset_fail = h->d_fail; a.cfg = h->d_cfg;
   return a;
 }
@@ -172,6 +176,7 @@ int drop_staged(td_handle* h, int b) {
   HIP_OK(hipMemset(h->d_nxt + (size_t)b * ring, 0, ring * 4));
   HIP_OK(hipMemset(h->d_lay_head + b, 0, 4));
   HIP_OK(hipMemset(h->d_lay_tail + b, 0, 4));
+  HIP_OK(hipMemset(h->d_lay_claim + b, 0, 4));
   return 0;
 }
 
@@ -180,24 +185,31 @@ int drop_all_staged(td_handle* h) {
   HIP_OK(hipMemset(h->d_nxt, 0, (size_t)h->B * NSLOT * slot_words(h->L) * 4));
   HIP_OK(hipMemset(h->d_lay_head, 0, (size_t)h->B * 4));
   HIP_OK(hipMemset(h->d_lay_tail, 0, (size_t)h->B * 4));
+  HIP_OK(hipMemset(h->d_lay_claim, 0, (size_t)h->B * 4));
   return 0;
 }
 
-// Launch a ring refill on the side stream behind the work queued on `s` so far,
-// unless the previous refill is still running (a refill that meets a layout the
-// reference would hang on runs for milliseconds; the next one catches up).
+// Launch a ring refill behind the work queued on `s` so far, on the next side
+// stream whose previous refill has finished (a refill that meets a layout the
+// reference would never finish runs for milliseconds; the other stream carries on).
+// `force` (reset paths, device idle) always launches.
 int start_refill(td_handle* h, hipStream_t s, bool force) {
-  if (h->refill_inflight && !force) {
-    hipError_t q = hipEventQuery(h->ev_refill);
-    if (q == hipErrorNotReady) return 0;
-    if (q != hipSuccess) HIP_OK(q);
+  int q = -1;
+  for (int k = 0; k < kSideStreams && q < 0; ++k) {
+    const int i = (h->next_side + k) % kSideStreams;
+    if (!h->refill_inflight[i] || force) { q = i; break; }
+    const hipError_t e = hipEventQuery(h->ev_refill[i]);
+    if (e == hipSuccess) q = i;
+    else if (e != hipErrorNotReady) HIP_OK(e);
   }
+  if (q < 0) return 0;
   StepArgs a = base_args(h);
   HIP_OK(hipEventRecord(h->ev_main, s));
-  HIP_OK(hipStreamWaitEvent(h->side, h->ev_main, 0));
-  HIP_OK(launch_refill(a, h->side));
-  HIP_OK(hipEventRecord(h->ev_refill, h->side));
-  h->refill_inflight = true;
+  HIP_OK(hipStreamWaitEvent(h->side[q], h->ev_main, 0));
+  HIP_OK(launch_refill(a, h->side[q]));
+  HIP_OK(hipEventRecord(h->ev_refill[q], h->side[q]));
+  h->refill_inflight[q] = true;
+  h->next_side = (q + 1) % kSideStreams;
   return 0;
 }
 
@@ -209,8 +221,7 @@ int run_reset(td_handle* h, const std::vector<uint8_t>& mask, float* obs, hipStr
   a.reset_mask = h->d_mask;
   HIP_OK(launch_step(a, s, true));
   if (h->autoreset && start_refill(h, s, true)) return -1;
-  HIP_OK(hipStreamSynchronize(s));
-  HIP_OK(hipStreamSynchronize(h->side));
+  HIP_OK(hipDeviceSynchronize());
   return 0;
 }
 
@@ -305,6 +316,7 @@ td_handle* td_create(const td_config* cfg, int map_size, int n_boards, int mode,
   rc |= dalloc(&h->d_nxt, B * NSLOT * slot_words(map_size));
   rc |= dalloc(&h->d_lay_head, B);
   rc |= dalloc(&h->d_lay_tail, B);
+  rc |= dalloc(&h->d_lay_claim, B);
   rc |= dalloc(&h->d_ovr_idx, B);
   rc |= dalloc(&h->d_scratch, B * h->scratch_stride);
   rc |= dalloc(&h->d_mask, B);
@@ -312,9 +324,11 @@ td_handle* td_create(const td_config* cfg, int map_size, int n_boards, int mode,
   rc |= dalloc(&h->d_stage, (size_t)h->stage_cap * h->lw);
   rc |= dalloc(&h->d_epstats, 2);
   if (!rc && hipMemcpy(h->d_cfg, &h->dcfg, sizeof(TdDevCfg), hipMemcpyHostToDevice) != hipSuccess) rc = fail("cfg upload");
-  if (!rc && hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking) != hipSuccess) rc = fail("side stream");
+  for (int q = 0; q < kSideStreams && !rc; ++q)
+    if (hipStreamCreateWithFlags(&h->side[q], hipStreamNonBlocking) != hipSuccess) rc = fail("side stream");
   if (!rc && hipEventCreateWithFlags(&h->ev_main, hipEventDisableTiming) != hipSuccess) rc = fail("event");
-  if (!rc && hipEventCreateWithFlags(&h->ev_refill, hipEventDisableTiming) != hipSuccess) rc = fail("event");
+  for (int q = 0; q < kSideStreams && !rc; ++q)
+    if (hipEventCreateWithFlags(&h->ev_refill[q], hipEventDisableTiming) != hipSuccess) rc = fail("event");
   if (rc) { std::string e = g_err; td_destroy(h); g_err = e; return nullptr; }
   std::vector<uint32_t> seeds(B);
   for (size_t b = 0; b < B; ++b) seeds[b] = (uint32_t)b;
@@ -328,12 +342,14 @@ void td_destroy(td_handle* h) {
   (void)hipDeviceSynchronize();
   void* dptrs[] = {h->d_cfg, h->d_hdr, h->d_en_lp, h->d_en_mg, h->d_en_inf, h->d_tw_cd, h->d_tw_inf,
                    h->d_cells, h->d_opp, h->d_hot, h->d_np, h->d_nxt, h->d_scratch, h->d_lay_head, h->d_lay_tail,
-                   h->d_ovr_idx, h->d_mask, h->d_fail, h->d_stage, h->d_epstats};
+                   h->d_lay_claim, h->d_ovr_idx, h->d_mask, h->d_fail, h->d_stage, h->d_epstats};
   for (void* p : dptrs)
     if (p) (void)hipFree(p);
   if (h->ev_main) (void)hipEventDestroy(h->ev_main);
-  if (h->ev_refill) (void)hipEventDestroy(h->ev_refill);
-  if (h->side) (void)hipStreamDestroy(h->side);
+  for (int q = 0; q < kSideStreams; ++q)
+    if (h->ev_refill[q]) (void)hipEventDestroy(h->ev_refill[q]);
+  for (int q = 0; q < kSideStreams; ++q)
+    if (h->side[q]) (void)hipStreamDestroy(h->side[q]);
   delete h;
 }
 
@@ -488,9 +504,11 @@ int td_step(td_handle* h, const td_step_io* io, void* stream) {
   a.win = io->win; a.allow_next = io->allow_next; a.ep_return = io->ep_return; a.ep_len = io->ep_len;
   a.stamps = h->d_stamps;
   a.ep_stats = h->d_epstats;
+  // the refill goes first: it waits for the previous step only, so a board whose ring
+  // is dry in this step can wait for it (td_step.hip step_board) without a cycle
+  if (h->autoreset && (h->steps % kRefillEvery) == 0 && start_refill(h, s, false)) return -1;
   HIP_OK(launch_step(a, s, false));
   h->steps += 1;
-  if (h->autoreset && (h->steps % kRefillEvery) == 0 && start_refill(h, s, false)) return -1;
   return 0;
 }
 

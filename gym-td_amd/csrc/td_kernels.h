@@ -30,6 +30,7 @@ struct StepArgs {
   uint32_t* nxt;        // [B][NSLOT][slot_words]
   uint32_t* lay_head;   // [B]
   uint32_t* lay_tail;   // [B]
+  uint32_t* lay_claim;  // [B] 1 while a refill wave draws the board's layouts
   int slot_words;
   uint8_t* scratch;     // [B][scratch_stride] road-generation scratch
   size_t scratch_stride;
@@ -59,11 +60,19 @@ hipError_t launch_step(const StepArgs& a, hipStream_t s, bool reset);
 // Draw staged layouts for every board whose ring has a free slot (side stream).
 hipError_t launch_refill(const StepArgs& a, hipStream_t s);
 
-constexpr int NSLOT = 2;  // staged layouts per board: two episodes of slack for the refill
+constexpr int NSLOT = 4;  // staged layouts per board: four episodes of slack for the refill
 __host__ __device__ inline uint32_t slot_tag(uint32_t n) { return 0x80000000u | (n & 0x7fffffffu); }
 __host__ __device__ inline int slot_words(int L) { return (8 + L * L + 31) & ~31; }
+// Boards scanned per refill wave: one wave per board up to 4,096 boards, at most
+// 4,096 waves above (16 boards per wave at 65,536), so a board in need rarely
+// queues behind another board's draw in the same wave.
+__host__ __device__ inline int refill_group(int B) {
+  const int g = (B + 4095) / 4096;
+  return g < 1 ? 1 : (g > 64 ? 64 : g);
+}
 
 constexpr int kRoadAttempts = 1000;  // bound of each create_road_v2 retry loop (reference: unbounded)
 constexpr int kLayoutRetries = 64;   // auto-reset: failing draws skipped before giving up
+constexpr uint64_t kTakeSpinTicks = 100000000ull;  // 1 s of the 100-MHz clock: longest wait for a refill wave
 
 }  // namespace td

@@ -67,6 +67,27 @@ __device__ __forceinline__ void st_relaxed(uint32_t* p, uint32_t v) {
   __hip_atomic_store((gu32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// A board's layout stream (np_mt) and its ring tail are written only by the refill
+// wave holding the board's claim word (several refills may be in flight on side
+// streams).  Take it with an agent-scope CAS + acquire; give it back after the
+// wave's stores have drained, behind an agent-scope release.
+__device__ __forceinline__ bool claim_board(uint32_t* claim, int lane) {
+  uint32_t got = 0;
+  if (lane == 0) got = atomicCAS(claim, 0u, 1u) == 0u ? 1u : 0u;
+  got = __builtin_amdgcn_readfirstlane(got);
+  if (got) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  return got != 0;
+}
+__device__ __forceinline__ void release_board(uint32_t* claim, int lane) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (lane == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    st_relaxed(claim, 0u);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // per-board LDS image
 // ---------------------------------------------------------------------------
@@ -1211,19 +1232,32 @@ __device__ void step_board(Smem<NC>& S, const Ctx& x, const StepArgs& a, int b, 
   bool was_reset = false;
   uint32_t lay_head = 0;
   if (done && a.autoreset) {
-    // consume staged layout number lay_head, published by the refill kernel on the
-    // side stream while this grid may be running: relaxed poll of its tag, then one
-    // agent-scope acquire before the plain loads of the record (MI355X_MICROARCH.md
-    // § visibility, "Valid forms"; the producer side is publish_slot)
+    // consume staged layout number lay_head, published by a refill kernel on a side
+    // stream while this grid may be running: relaxed sc1 poll of its tag, then one
+    // agent-scope acquire before the plain vector loads of the record
+    // (MI355X_MICROARCH.md § visibility, "Valid forms"; producer side: wave_layout)
     lay_head = a.lay_head[b];
     const uint32_t* rec = a.nxt + ((size_t)b * NSLOT + lay_head % NSLOT) * a.slot_words;
-    const uint32_t tag = ld_relaxed(rec);
-    if (tag == slot_tag(lay_head)) {
+    const uint32_t want = slot_tag(lay_head);
+    bool ready = ld_relaxed(rec) == want;
+    if (!ready && ld_relaxed(a.lay_claim + b) != 0u) {
+      // the ring ran dry while a refill wave holds the board: it is drawing exactly
+      // this layout (typically one the reference never finishes, 2-5 ms of one lane
+      // at the 1,000-attempt bound); wait for its tag, bounded
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      while (!ready && ld_relaxed(a.lay_claim + b) != 0u &&
+             __builtin_amdgcn_s_memrealtime() - t0 < kTakeSpinTicks) {
+        __builtin_amdgcn_s_sleep(64);
+        ready = ld_relaxed(rec) == want;
+      }
+      ready = ready || ld_relaxed(rec) == want;
+    }
+    if (ready) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       reset_board(S, u, x, rec);
       was_reset = true;
     } else {
-      u.flags |= FLAG_NO_LAYOUT;  // refill fell behind: the board keeps stepping its finished episode
+      u.flags |= FLAG_NO_LAYOUT;  // no layout staged or being drawn: the board keeps stepping its finished episode
     }
   }
   STAMP(5);
@@ -1385,7 +1419,7 @@ __global__ __launch_bounds__(64) void td_reset_kernel(StepArgs a) {
   }
 }
 
-// Keep every board's ring of staged layouts full: lanes check 64 boards at once
+// Keep every board's ring of staged layouts full: lanes check G boards at once
 // (layouts drawn minus consumed < NSLOT), then the wave draws the missing layouts
 // of those boards one by one, lane 0 running the serial generator out of LDS.  Runs
 // on a side stream concurrently with the step grids; td_capi keeps at most one in
@@ -1395,20 +1429,23 @@ __global__ __launch_bounds__(64) void td_refill_kernel(StepArgs a) {
   constexpr int NC = LT ? LT * LT : MAX_KERNEL_L * MAX_KERNEL_L;
   __shared__ LayoutSmem<NC> G;
   const int lane = (int)threadIdx.x;
-  for (int base = (int)blockIdx.x * 64; base < a.B; base += (int)gridDim.x * 64) {
+  const int grp = refill_group(a.B);
+  for (int base = (int)blockIdx.x * grp; base < a.B; base += (int)gridDim.x * grp) {
     const int b = base + lane;
+    const bool mine = lane < grp && b < a.B;
     uint32_t head = 0, tail = 0;
-    if (b < a.B) {
+    if (mine) {
       head = ld_relaxed(a.lay_head + b);  // a step grid may be advancing it right now
-      tail = a.lay_tail[b];
+      tail = ld_relaxed(a.lay_tail + b);
     }
-    uint64_t m = ballot(b < a.B && tail - head < (uint32_t)NSLOT);
+    uint64_t m = ballot(mine && tail - head < (uint32_t)NSLOT);
     while (m) {
       const int l = ctz64(m);
       m &= m - 1;
       const int bb = base + l;
-      uint32_t t = rdl(tail, l);
-      const uint32_t h = rdl(head, l);
+      if (!claim_board(a.lay_claim + bb, lane)) continue;  // another refill is drawing its layouts
+      uint32_t t = ld_relaxed(a.lay_tail + bb);
+      const uint32_t h = ld_relaxed(a.lay_head + bb);
       while (t - h < (uint32_t)NSLOT) {
         uint32_t* slot = a.nxt + ((size_t)bb * NSLOT + t % NSLOT) * a.slot_words;
         const int st = wave_layout(G, a, bb, kLayoutRetries, slot, t);
@@ -1416,7 +1453,8 @@ __global__ __launch_bounds__(64) void td_refill_kernel(StepArgs a) {
         if (st != ROAD_OK) break;  // 65 failing draws in a row: the next refill tries again
         ++t;
       }
-      if (lane == 0) a.lay_tail[bb] = t;
+      if (lane == 0) st_relaxed(a.lay_tail + bb, t);
+      release_board(a.lay_claim + bb, lane);
     }
   }
 }
@@ -1441,7 +1479,8 @@ hipError_t launch_step(const StepArgs& a, hipStream_t s, bool reset) {
 
 template <int LT>
 static void launch_refill2(const StepArgs& a, hipStream_t s) {
-  const int waves = std::min((a.B + 63) / 64, 1024);
+  const int grp = refill_group(a.B);
+  const int waves = (a.B + grp - 1) / grp;
   hipLaunchKernelGGL(td_refill_kernel<LT>, dim3(waves), dim3(64), 0, s, a);
 }
 

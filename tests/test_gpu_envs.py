@@ -348,3 +348,61 @@ def test_capacity_overflow_is_flagged():
         assert bool(torch.isfinite(eng.obs).all())  # count/8 planes exceed 1 here, as in the reference
     finally:
         eng.close()
+
+
+def _obs_checksum(obs):
+    """Per-board checksum of the observation bits (two int64 sums), on the device."""
+    w = obs.flatten(1).view(torch.int32).to(torch.int64)
+    idx = torch.arange(1, w.shape[1] + 1, device=w.device, dtype=torch.int64)
+    return torch.stack([w.sum(1), (w * idx).sum(1)], 1)
+
+
+@pytest.mark.parametrize("B,steps", [(16384, 200), (512, 1500)])
+def test_autoreset_under_load_matches_explicit_reset(B, steps):
+    """The staged-layout rings under load: 16,384 boards with 1-LP bases and a weak
+    defence finish ~250 episodes per step; 512 boards step so fast that one draw
+    the reference never finishes (2-5 ms of one lane) spans hundreds of steps.
+    Phase 1 runs the auto-reset engine 200
+    steps back to back with no host synchronisation, so the refill kernel publishes
+    layouts while step grids consume them; per-step observation checksums, rewards
+    and dones stay on the device.  Phase 2 replays the same actions on an engine
+    reset explicitly (the reset kernel draws each layout on the spot, failing draws
+    skipped as the refill skips them).  Every board must agree at every step."""
+    from test_gpu_parity import reference_settings
+    L = 10
+    ov = dict(base_LP=1, defender_init_cost=0, defender_cost_rate=0.02)
+    seeds = np.arange(B, dtype=np.int64) + 20000
+    with reference_settings(ov, False):
+        ea = TDEngine(L, B, "def", False, 1, np_seeds=seeds, py_seeds=seeds, autoreset=True)
+        eb = TDEngine(L, B, "def", False, 1, np_seeds=seeds, py_seeds=seeds, autoreset=False)
+    try:
+        ea.reset_all()
+        eb.reset_all()
+        assert torch.equal(ea.obs, eb.obs)
+        g = torch.Generator(device="cuda").manual_seed(21)
+        acts = torch.randint(0, 6 * L * L + 1, (steps, B), device="cuda", generator=g, dtype=torch.int64)
+        hist = []
+        for k in range(steps):  # phase 1: asynchronous
+            ea.step(def_act=acts[k])
+            hist.append((_obs_checksum(ea.obs), ea.reward.clone(), ea.done.clone()))
+        torch.cuda.synchronize()
+        resets = 0
+        for k in range(steps):  # phase 2: explicit resets
+            eb.step(def_act=acts[k])
+            cs, rw, dn = hist[k]
+            assert torch.equal(rw, eb.reward) and torch.equal(dn, eb.done), k
+            d = eb.done.cpu().numpy().astype(bool)
+            if d.any():
+                resets += int(d.sum())
+                _, failed = eb.reset(d)
+                while failed:
+                    m = np.zeros(B, dtype=np.uint8)
+                    m[failed] = 1
+                    _, failed = eb.reset(m)
+            bad = torch.nonzero((cs != _obs_checksum(eb.obs)).any(1)).flatten()
+            assert bad.numel() == 0, (k, bad[:8].tolist())
+        assert resets > steps * B // 100
+        assert (ea.flags() == 0).all()
+    finally:
+        ea.close()
+        eb.close()
