@@ -9,7 +9,8 @@ run() { local name=$1 secs=$2; shift 2; echo "== $name" >&2; timeout -k 10 "$sec
 [ -n "$NO_PHASES" ] || run phases 300 env TDSTEP_LIB=$PWD/gym-td_amd/lib/libtdstep_stamps.so python scripts/probe_phases.py $B 10 600 || exit $?
 run counters_list 120 rocprofv3 -L || true
 BENCH="python bench.py --workload $WL --steps 20 --warmup 2 --burnin 100 --no-cpu-baseline --boards $B"
-run kt 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof/kt -o kt --output-format csv -- $BENCH || exit $?
+# kernel trace of the bench command itself (default arguments: the BENCH line's run)
+run kt 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof/kt -o kt --output-format csv -- python bench.py --workload $WL --boards $B || exit $?
 run pmc_fetch 400 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/prof/pmc_fetch -o pmc --output-format csv -- $BENCH || exit $?
 run pmc_write 400 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/prof/pmc_write -o pmc --output-format csv -- $BENCH || exit $?
 run pmc_sq1 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_SMEM SQ_INSTS_BRANCH -d gpurun_out/prof/pmc_sq1 -o pmc --output-format csv -- $BENCH || exit $?
