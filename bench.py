@@ -156,10 +156,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # TD_BENCH_DIST_BACKEND=gloo + TD_BENCH_SAME_DEVICE=1: rehearsal of the N > 1 control
+    # flow with every rank on cuda:0 of a one-GPU box (never the measured configuration)
+    backend = os.environ.get("TD_BENCH_DIST_BACKEND", "nccl")
+    gpu = 0 if os.environ.get("TD_BENCH_SAME_DEVICE") == "1" else local
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local if world > 1 else 0)
+        torch.cuda.set_device(gpu)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group(backend)
+    dev = torch.device("cuda", gpu if world > 1 else 0)
+    coll = dev if backend == "nccl" else torch.device("cpu")  # where the collectives' tensors live
     torch.cuda.set_device(dev)
 
     from gym_TD.engine import TDEngine
@@ -227,8 +235,8 @@ def main():
     # after timing: MAX of the clocks over ranks, and the episode statistics of the
     # timed steps gathered to rank 0 (the only exchange; RCCL on GPUs)
     flags = eng.flags()
-    t = shard.max_over_ranks(torch.tensor([elapsed, avg_kernel_s], dtype=torch.float64, device=dev))
-    per_rank = shard.gather_stats(eng.episode_stats(clear=True))
+    t = shard.max_over_ranks(torch.tensor([elapsed, avg_kernel_s], dtype=torch.float64, device=coll))
+    per_rank = shard.gather_stats(eng.episode_stats(clear=True).to(coll))
     elapsed, avg_kernel_s = float(t[0]), float(t[1])
 
     if rank == 0:
