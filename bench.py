@@ -58,7 +58,8 @@ ENV_ID = {"def-small": "TD-def-small-v0", "2p-middle-multi": "TD-2p-middle-v0 (a
 DATA = {("def", False): "synthetic: uniform random defender actions, built-in lv1 opponent, seeded boards",
         ("2p", True): "synthetic: defender flags uniform in {0,1,2} (6,L,L), attacker clusters uniform in {0..4} (3,8), "
                       "seeded boards"}
-N_ACTION_BUFS = 8  # distinct pre-drawn action batches cycled through the timed steps (multi-action shapes)
+N_ACTION_BUFS = 8
+EVENT_EVERY = 4  # timed steps per sampled kernel duration  # distinct pre-drawn action batches cycled through the timed steps (multi-action shapes)
 
 
 def algorithmic_bytes(L, mode="def", multi=False):
@@ -211,7 +212,11 @@ def main():
         eng.step(def_act=d, atk_act=a)
     acts = pool if multi else draw(K)
     stream = torch.cuda.current_stream(dev)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+    # HIP events bracket every EVENT_EVERY-th step kernel on its stream: the kernel's
+    # duration is sampled live over the timed region without a timing event pair
+    # (and its cache flush) behind every launch
+    sampled = set(range(0, K, EVENT_EVERY))
+    ev = {k: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for k in sampled}
     eng.episode_stats(clear=True)  # the device accumulates finished episodes of the timed steps
 
     torch.cuda.synchronize(dev)
@@ -220,17 +225,19 @@ def main():
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for k in range(K):
-        ev[k][0].record(stream)
+        if k in sampled:
+            ev[k][0].record(stream)
         d, a = acts[k % len(acts)]
         eng.step(def_act=d, atk_act=a)
-        ev[k][1].record(stream)
+        if k in sampled:
+            ev[k][1].record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
 
-    kern_ms = [s.elapsed_time(e) for s, e in ev]
+    kern_ms = [s.elapsed_time(e) for s, e in ev.values()]
     avg_kernel_s = float(np.mean(kern_ms)) / 1e3
     # after timing: MAX of the clocks over ranks, and the episode statistics of the
     # timed steps gathered to rank 0 (the only exchange; RCCL on GPUs)
@@ -268,6 +275,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "td_step_kernel<%d, %s>" % (L, mode.upper()), "avg_kernel_us": avg_kernel_s * 1e6,
+                         "kernel_samples": len(kern_ms) * world,
                          "algorithmic_bytes_per_launch": B * bpe},
             "board_flags_nonzero": int((flags != 0).sum()),
             "episodes": {"finished": int(per_rank[:, 0].sum()),

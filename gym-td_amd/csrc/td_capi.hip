@@ -43,7 +43,9 @@ int fail(const char* fmt, ...) {
     if (e_ != hipSuccess) return fail("%s: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, __LINE__); \
   } while (0)
 
-constexpr int kRefillEvery = 1;  // steps between refill launches (when a side stream is free)
+// Steps between refill launches (when a side stream is free): about one refill per
+// 100-250 us of stepping -- every step at 32k+ boards, every 4th below 8k.
+inline int refill_every(int B) { return B >= 32768 ? 1 : (B >= 8192 ? 2 : 4); }
 constexpr int kSideStreams = 2;  // refills in flight at once: one stuck on a long draw does not stall the next
 
 }  // namespace
@@ -506,7 +508,7 @@ int td_step(td_handle* h, const td_step_io* io, void* stream) {
   a.ep_stats = h->d_epstats;
   // the refill goes first: it waits for the previous step only, so a board whose ring
   // is dry in this step can wait for it (td_step.hip step_board) without a cycle
-  if (h->autoreset && (h->steps % kRefillEvery) == 0 && start_refill(h, s, false)) return -1;
+  if (h->autoreset && (h->steps % refill_every(h->B)) == 0 && start_refill(h, s, false)) return -1;
   HIP_OK(launch_step(a, s, false));
   h->steps += 1;
   return 0;
