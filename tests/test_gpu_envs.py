@@ -52,6 +52,11 @@ def _fc_list(row):
     (10, 16, "2p", True, 1, 120),
     (10, 16, "def", True, 1, 120),
     (10, 24, "def", False, 0, 150),
+    # sizes off the specialised kernels (generic L <= 32 build; odd L*L: scalar observation path)
+    (8, 16, "def", False, 1, 120),
+    (12, 12, "atk", False, 1, 100),
+    (15, 8, "2p", True, 1, 80),
+    (16, 8, "def", False, 1, 100),
 ])
 def test_batched_modes_vs_oracle(L, B, mode, multi, difficulty, steps):
     """B boards of one mode in one launch vs B oracle envs: reward bits, done,
