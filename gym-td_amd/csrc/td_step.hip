@@ -877,14 +877,17 @@ __device__ __forceinline__ void write_obs(const Smem<NC>& S, const Ctx& x, float
 // board load / reset / store
 // ---------------------------------------------------------------------------
 // The inputs of one board step, all loads issued before any is waited on.
-// Lane l holds enemy slot l (l < PF_EN), tower slot l & 31, cells l and l + 64, and one word
+// Lane l holds enemy slot l (l < PF_EN), tower slot l (l < PF_TW), cells l and l + 64, and one word
 // of `w`: lanes 0-23 the header, 24-25 the discrete defender action, 26-37 the
 // opponent stream's hot record.
 struct Prefetch {
   double lp, mg, tcd;
   uint32_t inf, tinf, c0, c1, w;
 };
-constexpr int PF_ACT = 24, PF_HOT = 26, PF_EN = 16;
+#ifndef TD_PF_TW
+#define TD_PF_TW 16
+#endif
+constexpr int PF_ACT = 24, PF_HOT = 26, PF_EN = 16, PF_TW = TD_PF_TW;
 static_assert(offsetof(TdHdr, steps) == 24 && offsetof(TdHdr, start_cell) == 56 && offsetof(TdHdr, episodes) == 76,
               "Prefetch header word map");
 
@@ -896,8 +899,10 @@ __device__ __forceinline__ void prefetch_issue(Prefetch& P, const StepArgs& a, i
     P.mg = a.en_mg[eb + lane];
     P.inf = a.en_inf[eb + lane];
   }
-  P.tcd = a.tw_cd[tb + (lane & (TCAP - 1))];
-  P.tinf = a.tw_inf[tb + (lane & (TCAP - 1))];
+  if (lane < PF_TW) {  // tower slots beyond PF_TW load after the header
+    P.tcd = a.tw_cd[tb + lane];
+    P.tinf = a.tw_inf[tb + lane];
+  }
   P.c0 = lane < ncr ? a.cells[cb + lane] : 0u;
   P.c1 = lane + 64 < ncr ? a.cells[cb + lane + 64] : 0u;
   const uint32_t* src;
@@ -936,13 +941,20 @@ __device__ void load_board(Smem<NC>& S, U& u, const Ctx& x, const StepArgs& a, i
   u.cells_dirty = false;
   if (x.lane < u.n && x.lane < PF_EN) { S.eLP[x.lane] = P.lp; S.eMg[x.lane] = P.mg; S.eInf[x.lane] = P.inf; }
   for (int i = PF_EN + x.lane; i < u.n; i += 64) { S.eLP[i] = a.en_lp[eb + i]; S.eMg[i] = a.en_mg[eb + i]; S.eInf[i] = a.en_inf[eb + i]; }
+  uint32_t tinf = P.tinf;
   if (x.lane < u.nt) {
-    S.tCd[x.lane] = P.tcd;
-    S.tInf[x.lane] = P.tinf;
+    double tcd = P.tcd;
+    if (x.lane >= PF_TW) {
+      const size_t tb = (size_t)b * TCAP;
+      tcd = a.tw_cd[tb + x.lane];
+      tinf = a.tw_inf[tb + x.lane];
+    }
+    S.tCd[x.lane] = tcd;
+    S.tInf[x.lane] = tinf;
   }
   __syncthreads();
   if (x.lane < u.nt)
-    S.twr[P.tinf & 0xfffu] = (uint8_t)(0x80u | (((P.tinf >> 14) & 1u) << 2) | ((P.tinf >> 12) & 3u));
+    S.twr[tinf & 0xfffu] = (uint8_t)(0x80u | (((tinf >> 14) & 1u) << 2) | ((tinf >> 12) & 3u));
   __syncthreads();
 }
 

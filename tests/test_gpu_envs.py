@@ -411,3 +411,36 @@ def test_autoreset_under_load_matches_explicit_reset(B, steps):
     finally:
         ea.close()
         eb.close()
+
+
+def test_many_towers_vs_oracle():
+    """Boards with more towers than the step prefetches up front (16): tower distance
+    1, rich defender.  Same bit-exact comparison as the batched tests."""
+    from test_gpu_parity import reference_settings
+    L, B, steps = 10, 12, 120
+    ov = dict(tower_distance=1, defender_init_cost=300, max_cost=400, defender_cost_rate=5)
+    cfg = O.Config(**ov)
+    seeds, orc = _first_ok_seeds(L, B, 9000, "def", False, 1, cfg)
+    with reference_settings(ov, False):
+        eng = TDEngine(L, B, "def", False, 1, np_seeds=seeds, py_seeds=seeds, autoreset=False)
+    try:
+        eng.reset()
+        rng = np.random.RandomState(12)
+        most = 0
+        for k in range(steps):
+            acts = np.array([policies.discrete_def(rng, L, o._board.map[0], 0.9) for o in orc], dtype=np.int64)
+            eng.step(def_act=torch.from_numpy(acts))
+            ob, rw = eng.obs.cpu().numpy(), eng.reward.cpu().numpy()
+            st = eng.export_state()
+            for b, o in enumerate(orc):
+                if o._board.done():
+                    continue
+                wo, wr, _, _ = o.step(int(acts[b]))
+                assert canon.fhex(rw[b]) == canon.fhex(wr), (k, b)
+                assert canon.state_digest(eng.board_state(b, st)) == canon.state_digest(canon.oracle_state(o)), (k, b)
+                assert np.array_equal(ob[b], wo), (k, b)
+                most = max(most, len(o._board.towers))
+        assert most > 16, most
+        assert (eng.flags() == 0).all()
+    finally:
+        eng.close()
