@@ -59,7 +59,8 @@ DATA = {("def", False): "synthetic: uniform random defender actions, built-in lv
         ("2p", True): "synthetic: defender flags uniform in {0,1,2} (6,L,L), attacker clusters uniform in {0..4} (3,8), "
                       "seeded boards"}
 N_ACTION_BUFS = 8
-EVENT_EVERY = 4  # timed steps per sampled kernel duration  # distinct pre-drawn action batches cycled through the timed steps (multi-action shapes)
+EVENT_EVERY = 4  # timed steps per sampled kernel duration
+FLAG_BITS = (("enemy_overflow", 1), ("tower_overflow", 2), ("bad_action", 4), ("no_layout", 8), ("bad_move", 16))  # distinct pre-drawn action batches cycled through the timed steps (multi-action shapes)
 
 
 def algorithmic_bytes(L, mode="def", multi=False):
@@ -278,6 +279,7 @@ def main():
                          "kernel_samples": len(kern_ms) * world,
                          "algorithmic_bytes_per_launch": B * bpe},
             "board_flags_nonzero": int((flags != 0).sum()),
+            "board_flags": {name: int(((flags & bit) != 0).sum()) for name, bit in FLAG_BITS if ((flags & bit) != 0).any()},
             "episodes": {"finished": int(per_rank[:, 0].sum()),
                          "mean_return": float(per_rank[:, 1].sum() / max(float(per_rank[:, 0].sum()), 1.0)),
                          "per_rank": [int(v) for v in per_rank[:, 0].tolist()]},

@@ -45,8 +45,12 @@ int fail(const char* fmt, ...) {
 
 // Steps between refill launches (when a side stream is free): about one refill per
 // 100-250 us of stepping -- every step at 32k+ boards, every 4th below 8k.
-inline int refill_every(int B) { return B >= 32768 ? 1 : (B >= 8192 ? 2 : 4); }
-constexpr int kSideStreams = 2;  // refills in flight at once: one stuck on a long draw does not stall the next
+#ifndef TD_REFILL_EVERY
+#define TD_REFILL_EVERY 4
+#endif
+inline int refill_every(int) { return TD_REFILL_EVERY; }
+constexpr int kSideStreams = 2;  // refill streams: one stuck on a long draw does not stall the next (the HIP
+                                 // runtime has 4 hardware queues per process; the step stream needs one)
 
 }  // namespace
 
@@ -67,12 +71,11 @@ struct td_handle {
   int stage_cap = 0;
   uint64_t* d_stamps = nullptr;  // TD_STAMPS diagnostic builds only (not owned)
   double* d_epstats = nullptr;   // [2] finished episodes, sum of their returns
-  // Layout refills run on kSideStreams side streams, at most one in flight on each;
-  // the step stream never waits for them (the rings give every board NSLOT
-  // episodes of slack, and per-board claims keep concurrent refills apart).
+  // Layout refills run on kSideStreams side streams in turn; the step stream never
+  // waits for them (the rings give every board NSLOT episodes of slack, and
+  // per-board claims keep concurrent refills apart).
   hipStream_t side[kSideStreams] = {};
-  hipEvent_t ev_main = nullptr, ev_refill[kSideStreams] = {};
-  bool refill_inflight[kSideStreams] = {};
+  hipEvent_t ev_main = nullptr;
   int next_side = 0;
   long long steps = 0;
   std::vector<int32_t> last_reset_failed;
@@ -179,6 +182,7 @@ int drop_staged(td_handle* h, int b) {
   HIP_OK(hipMemset(h->d_lay_head + b, 0, 4));
   HIP_OK(hipMemset(h->d_lay_tail + b, 0, 4));
   HIP_OK(hipMemset(h->d_lay_claim + b, 0, 4));
+  HIP_OK(hipMemset(h->d_scratch + (size_t)b * h->scratch_stride, 0, sizeof(RoadResume)));  // no pending draw
   return 0;
 }
 
@@ -188,29 +192,22 @@ int drop_all_staged(td_handle* h) {
   HIP_OK(hipMemset(h->d_lay_head, 0, (size_t)h->B * 4));
   HIP_OK(hipMemset(h->d_lay_tail, 0, (size_t)h->B * 4));
   HIP_OK(hipMemset(h->d_lay_claim, 0, (size_t)h->B * 4));
+  HIP_OK(hipMemset(h->d_scratch, 0, (size_t)h->B * h->scratch_stride));  // no pending draws
   return 0;
 }
 
-// Launch a ring refill behind the work queued on `s` so far, on the next side
-// stream whose previous refill has finished (a refill that meets a layout the
-// reference would never finish runs for milliseconds; the other stream carries on).
-// `force` (reset paths, device idle) always launches.
-int start_refill(td_handle* h, hipStream_t s, bool force) {
-  int q = -1;
-  for (int k = 0; k < kSideStreams && q < 0; ++k) {
-    const int i = (h->next_side + k) % kSideStreams;
-    if (!h->refill_inflight[i] || force) { q = i; break; }
-    const hipError_t e = hipEventQuery(h->ev_refill[i]);
-    if (e == hipSuccess) q = i;
-    else if (e != hipErrorNotReady) HIP_OK(e);
-  }
-  if (q < 0) return 0;
+// Launch a ring refill behind the work queued on `s` so far, on the side streams in
+// turn.  Refills are anchored to the step stream (each waits for the step before it,
+// then runs beside the next one), never to host time: the host may run thousands of
+// steps ahead of the GPU, and a refill launched "when a stream looks free" from there
+// would leave the GPU without refills for as long.  A refill stuck on a draw the
+// reference never finishes (milliseconds) delays only its own stream's queue.
+int start_refill(td_handle* h, hipStream_t s) {
+  const int q = h->next_side;
   StepArgs a = base_args(h);
   HIP_OK(hipEventRecord(h->ev_main, s));
   HIP_OK(hipStreamWaitEvent(h->side[q], h->ev_main, 0));
   HIP_OK(launch_refill(a, h->side[q]));
-  HIP_OK(hipEventRecord(h->ev_refill[q], h->side[q]));
-  h->refill_inflight[q] = true;
   h->next_side = (q + 1) % kSideStreams;
   return 0;
 }
@@ -222,7 +219,7 @@ int run_reset(td_handle* h, const std::vector<uint8_t>& mask, float* obs, hipStr
   a.obs = obs;
   a.reset_mask = h->d_mask;
   HIP_OK(launch_step(a, s, true));
-  if (h->autoreset && start_refill(h, s, true)) return -1;
+  if (h->autoreset && start_refill(h, s)) return -1;
   HIP_OK(hipDeviceSynchronize());
   return 0;
 }
@@ -299,7 +296,7 @@ td_handle* td_create(const td_config* cfg, int map_size, int n_boards, int mode,
   td_handle* h = new td_handle();
   h->L = map_size; h->NC = map_size * map_size; h->B = n_boards; h->mode = mode; h->multi = multi_action ? 1 : 0;
   h->difficulty = difficulty; h->device = device; h->lw = layout_words(map_size);
-  h->scratch_stride = (road_scratch_bytes(map_size) + 15) & ~(size_t)15;
+  h->scratch_stride = (sizeof(RoadResume) + road_scratch_bytes(map_size) + 15) & ~(size_t)15;
   h->stage_cap = std::min(n_boards, 4096);
   build_dev_cfg(*cfg, h->dcfg);
   const size_t B = (size_t)n_boards;
@@ -329,8 +326,6 @@ td_handle* td_create(const td_config* cfg, int map_size, int n_boards, int mode,
   for (int q = 0; q < kSideStreams && !rc; ++q)
     if (hipStreamCreateWithFlags(&h->side[q], hipStreamNonBlocking) != hipSuccess) rc = fail("side stream");
   if (!rc && hipEventCreateWithFlags(&h->ev_main, hipEventDisableTiming) != hipSuccess) rc = fail("event");
-  for (int q = 0; q < kSideStreams && !rc; ++q)
-    if (hipEventCreateWithFlags(&h->ev_refill[q], hipEventDisableTiming) != hipSuccess) rc = fail("event");
   if (rc) { std::string e = g_err; td_destroy(h); g_err = e; return nullptr; }
   std::vector<uint32_t> seeds(B);
   for (size_t b = 0; b < B; ++b) seeds[b] = (uint32_t)b;
@@ -348,8 +343,6 @@ void td_destroy(td_handle* h) {
   for (void* p : dptrs)
     if (p) (void)hipFree(p);
   if (h->ev_main) (void)hipEventDestroy(h->ev_main);
-  for (int q = 0; q < kSideStreams; ++q)
-    if (h->ev_refill[q]) (void)hipEventDestroy(h->ev_refill[q]);
   for (int q = 0; q < kSideStreams; ++q)
     if (h->side[q]) (void)hipStreamDestroy(h->side[q]);
   delete h;
@@ -508,7 +501,7 @@ int td_step(td_handle* h, const td_step_io* io, void* stream) {
   a.ep_stats = h->d_epstats;
   // the refill goes first: it waits for the previous step only, so a board whose ring
   // is dry in this step can wait for it (td_step.hip step_board) without a cycle
-  if (h->autoreset && (h->steps % refill_every(h->B)) == 0 && start_refill(h, s, false)) return -1;
+  if (h->autoreset && (h->steps % refill_every(h->B)) == 0 && start_refill(h, s)) return -1;
   HIP_OK(launch_step(a, s, false));
   h->steps += 1;
   return 0;
@@ -598,6 +591,18 @@ int td_debug_stamps(td_handle* h, uint64_t* dev) {
   return 0;
 }
 #endif
+
+// Diagnostic: board b's ring -- head, tail, claim, then the NSLOT slot tags.
+int td_debug_ring(td_handle* h, int b, uint32_t* out) {
+  if (!h || b < 0 || b >= h->B || !out) return fail("td_debug_ring: bad arguments");
+  HIP_OK(hipDeviceSynchronize());
+  HIP_OK(hipMemcpy(out, h->d_lay_head + b, 4, hipMemcpyDeviceToHost));
+  HIP_OK(hipMemcpy(out + 1, h->d_lay_tail + b, 4, hipMemcpyDeviceToHost));
+  HIP_OK(hipMemcpy(out + 2, h->d_lay_claim + b, 4, hipMemcpyDeviceToHost));
+  for (int s = 0; s < NSLOT; ++s)
+    HIP_OK(hipMemcpy(out + 3 + s, h->d_nxt + ((size_t)b * NSLOT + s) * slot_words(h->L), 4, hipMemcpyDeviceToHost));
+  return 0;
+}
 
 void td_py_seed(uint32_t* mt, uint32_t seed) { py_seed(mt, seed); }
 void td_np_seed(uint32_t* mt, uint32_t seed) { np_seed(mt, seed); }

@@ -32,7 +32,7 @@ struct StepArgs {
   uint32_t* lay_tail;   // [B]
   uint32_t* lay_claim;  // [B] 1 while a refill wave draws the board's layouts
   int slot_words;
-  uint8_t* scratch;     // [B][scratch_stride] road-generation scratch
+  uint8_t* scratch;     // [B][scratch_stride] a pending layout draw: RoadResume header + generator arrays
   size_t scratch_stride;
   uint8_t* reset_fail;  // [B] reset kernel: road generation failed (board left unchanged)
   const int32_t* ovr_idx;   // reset kernel, td_reset_layouts: [B] record index in ovr_rec, or -1
@@ -66,13 +66,17 @@ __host__ __device__ inline int slot_words(int L) { return (8 + L * L + 31) & ~31
 // Boards scanned per refill wave: one wave per board up to 4,096 boards, at most
 // 4,096 waves above (16 boards per wave at 65,536), so a board in need rarely
 // queues behind another board's draw in the same wave.
+#ifndef TD_REFILL_WAVES
+#define TD_REFILL_WAVES 1024
+#endif
 __host__ __device__ inline int refill_group(int B) {
-  const int g = (B + 4095) / 4096;
+  const int g = (B + TD_REFILL_WAVES - 1) / TD_REFILL_WAVES;
   return g < 1 ? 1 : (g > 64 ? 64 : g);
 }
 
 constexpr int kRoadAttempts = 1000;  // bound of each create_road_v2 retry loop (reference: unbounded)
 constexpr int kLayoutRetries = 64;   // auto-reset: failing draws skipped before giving up
+constexpr int kRefillWalks = 48;     // walks per board per refill launch (a draw resumes in the next launch)
 constexpr uint64_t kTakeSpinTicks = 100000000ull;  // 1 s of the 100-MHz clock: longest wait for a refill wave
 
 }  // namespace td

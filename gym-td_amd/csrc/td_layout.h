@@ -34,6 +34,15 @@ enum RoadStatus : int {
   ROAD_ERR_EMPTY = 2,     // IndexError at TDRoadGen.py:189 (branch road of length 0)
   ROAD_ERR_BOUND = 3,     // retry bound exceeded (the reference loops forever)
   ROAD_ERR_ARGS = 4,
+  ROAD_PENDING = 5,       // resumable draw: budget exhausted, state kept (RoadGen::draw)
+};
+
+// State of a layout draw between RoadGen::draw calls (with the scratch arrays and
+// the partial record).  16 words.
+enum RoadPhase : uint32_t { RP_NEW = 0, RP_ROAD1 = 1, RP_ROAD2 = 2, RP_BRANCH = 3 };
+struct RoadResume {
+  uint32_t phase, att, nr, ri, n1, cr, cc, d0, nm, np, maxdist, endc;
+  uint32_t start[3], pad;
 };
 
 TD_HD inline int layout_words(int L) { return LAYOUT_HDR + L * L; }
@@ -127,86 +136,117 @@ struct RoadGen {
 
   static TD_HD int iabs(int x) { return x < 0 ? -x : x; }
 
-  // create_road_v2 + TDBoard map planes; writes the layout record ``rec``.
-  TD_HD int generate(int num_roads, uint32_t* rec) {
-    if (L < 4 || L > MAX_L || num_roads < 1 || num_roads > 3) return ROAD_ERR_ARGS;
-    if (L / 4 <= L * 3 / 20) return ROAD_ERR_RANDINT;  // segment randint raises (TDRoadGen.py:41)
+  // TDGymBasic.reset's draws (num_roads, :42) + create_road_v2 (TDRoadGen.py:4-199)
+  // + the TDBoard map planes, as a resumable state machine: ``budget`` bounds the
+  // walks (retry-loop attempts) run in this call.  Returns ROAD_OK (record complete),
+  // a ROAD_ERR_* status (the reference raises, or the retry bound hit), or
+  // ROAD_PENDING with the draw's state kept in ``st``, the scratch arrays and the
+  // partial record -- a later call continues it draw for draw, so splitting a draw
+  // over calls gives exactly the draws of one uninterrupted run.
+  TD_HD int draw(RoadResume& st, int budget, uint32_t* rec) {
     const int NC = L * L;
-    for (int i = 0; i < NC; ++i) { s.field[i] = 0; s.rot[i] = 0; }
-    int lo = L / 3, hi = (L * 2 + 2) / 3;
-    int cr = (int)rng.np_randint(lo, hi), cc = (int)rng.np_randint(lo, hi);
-    s.field[cr * L + cc] = 1;
-    int d0 = (int)rng.np_randint(0, 4);
-    int n1 = 0, n2 = 0, att;
-    for (att = 0;; ++att) {  // :128-137
-      if (att >= max_attempts) return ROAD_ERR_BOUND;
-      int ok = walk(cr, cc, d0, s.r1, &n1);
-      if (!ok || n1 >= L) { erase(s.r1, n1); continue; }
-      break;
-    }
-    for (att = 0;; ++att) {  // :141-155
-      if (att >= max_attempts) return ROAD_ERR_BOUND;
-      int ok = walk(cr, cc, (d0 + 2) % 4, s.r2, &n2);
-      if (!ok || n1 + n2 + 1 >= L * 2) { erase(s.r2, n2); continue; }
-      int e2 = s.r2[n2 - 1], e1 = s.r1[n1 - 1];
-      if (iabs(e2 / L - e1 / L) + iabs(e2 % L - e1 % L) < L * 3 / 4) { erase(s.r2, n2); continue; }
-      break;
-    }
-    int nm = 0;  // main = reversed(road2) + [center] + road1  (:157-158)
-    for (int i = n2 - 1; i >= 0; --i) s.mainr[nm++] = s.r2[i];
-    s.mainr[nm++] = (uint16_t)(cr * L + cc);
-    for (int i = 0; i < n1; ++i) s.mainr[nm++] = s.r1[i];
-    int np = 0;  // selectable (:162-170)
-    for (int i = 0; i < nm;) {
-      if (!s.rot[s.mainr[i]]) {
-        if (i < nm - 1 && !s.rot[s.mainr[i + 1]]) s.picks[np++] = ((uint32_t)i << 16) | s.mainr[i];
-        i += 1;
-      } else {
-        i += 2;
-      }
-    }
-    // map planes from main road first (roads[0])
-    for (int i = 0; i < NC; ++i) rec[LAYOUT_HDR + i] = 0;
     uint32_t* cw = rec + LAYOUT_HDR;
-    int maxdist = 0;
-    int starts[3] = {0, 0, 0};
-    stamp_road(cw, s.mainr, nm, 0, nullptr, 0, &maxdist);
-    starts[0] = s.mainr[0];
-    int endc = s.mainr[nm - 1];
-    for (int ri = 1; ri < num_roads; ++ri) {  // :174-197
-      int k = 0, nb = 0;
-      for (att = 0;; ++att) {
-        if (att >= max_attempts) return ROAD_ERR_BOUND;
-        int klo = np * 2 / 5, khi = np * 4 / 5;
-        if (khi <= klo) return ROAD_ERR_RANDINT;
-        k = (int)rng.np_randint(klo, khi);
-        int nd = (int)rng.np_randint(0, 4);
-        int bcell = s.picks[k] & 0xffffu;
-        k = (int)(s.picks[k] >> 16);
-        int ok = walk(bcell / L, bcell % L, nd, s.rb, &nb);
-        if (!ok) { erase(s.rb, nb); continue; }
-        if (nb + nm - k >= L * 2) { erase(s.rb, nb); continue; }
-        if (nb == 0) return ROAD_ERR_EMPTY;
-        int eb = s.rb[nb - 1];
-        if (iabs(eb / L - endc / L) + iabs(eb % L - endc % L) < L * 3 / 4) { erase(s.rb, nb); continue; }
-        break;
+    if (st.phase == RP_NEW) {
+      st.nr = (uint32_t)rng.np_randint(1, 4);  // TDGymBasic.reset :42
+      const int nr = (int)st.nr;
+      if (L < 4 || L > MAX_L || nr < 1 || nr > 3) return fail(st, ROAD_ERR_ARGS, rec);
+      if (L / 4 <= L * 3 / 20) return fail(st, ROAD_ERR_RANDINT, rec);  // segment randint raises (:41)
+      for (int i = 0; i < NC; ++i) { s.field[i] = 0; s.rot[i] = 0; }
+      const int lo = L / 3, hi = (L * 2 + 2) / 3;
+      st.cr = (uint32_t)rng.np_randint(lo, hi);
+      st.cc = (uint32_t)rng.np_randint(lo, hi);
+      s.field[st.cr * L + st.cc] = 1;
+      st.d0 = (uint32_t)rng.np_randint(0, 4);
+      st.phase = RP_ROAD1; st.att = 0;
+    }
+    const int cr = (int)st.cr, cc = (int)st.cc, d0 = (int)st.d0;
+    while (st.phase == RP_ROAD1) {  // center -> end, :128-137
+      if ((int)st.att >= max_attempts) return fail(st, ROAD_ERR_BOUND, rec);
+      if (budget-- <= 0) return ROAD_PENDING;
+      ++st.att;
+      int n1 = 0;
+      const int ok = walk(cr, cc, d0, s.r1, &n1);
+      if (!ok || n1 >= L) { erase(s.r1, n1); continue; }
+      st.n1 = (uint32_t)n1; st.phase = RP_ROAD2; st.att = 0;
+    }
+    while (st.phase == RP_ROAD2) {  // center -> start, :141-155
+      if ((int)st.att >= max_attempts) return fail(st, ROAD_ERR_BOUND, rec);
+      if (budget-- <= 0) return ROAD_PENDING;
+      ++st.att;
+      const int n1 = (int)st.n1;
+      int n2 = 0;
+      const int ok = walk(cr, cc, (d0 + 2) % 4, s.r2, &n2);
+      if (!ok || n1 + n2 + 1 >= L * 2) { erase(s.r2, n2); continue; }
+      const int e2 = s.r2[n2 - 1], e1 = s.r1[n1 - 1];
+      if (iabs(e2 / L - e1 / L) + iabs(e2 % L - e1 % L) < L * 3 / 4) { erase(s.r2, n2); continue; }
+      // main = reversed(road2) + [center] + road1 (:157-158), branch points (:162-170)
+      int nm = 0;
+      for (int i = n2 - 1; i >= 0; --i) s.mainr[nm++] = s.r2[i];
+      s.mainr[nm++] = (uint16_t)(cr * L + cc);
+      for (int i = 0; i < n1; ++i) s.mainr[nm++] = s.r1[i];
+      int np = 0;
+      for (int i = 0; i < nm;) {
+        if (!s.rot[s.mainr[i]]) {
+          if (i < nm - 1 && !s.rot[s.mainr[i + 1]]) s.picks[np++] = ((uint32_t)i << 16) | s.mainr[i];
+          i += 1;
+        } else {
+          i += 2;
+        }
       }
+      // map planes from the main road first (roads[0])
+      for (int i = 0; i < NC; ++i) cw[i] = 0;
+      int maxdist = 0;
+      stamp_road(cw, s.mainr, nm, 0, nullptr, 0, &maxdist);
+      st.nm = (uint32_t)nm; st.np = (uint32_t)np; st.maxdist = (uint32_t)maxdist;
+      st.start[0] = s.mainr[0]; st.start[1] = st.start[2] = 0;
+      st.endc = s.mainr[nm - 1];
+      st.phase = RP_BRANCH; st.ri = 1; st.att = 0;
+    }
+    while (st.phase == RP_BRANCH && (int)st.ri < (int)st.nr) {  // :174-197
+      if ((int)st.att >= max_attempts) return fail(st, ROAD_ERR_BOUND, rec);
+      if (budget-- <= 0) return ROAD_PENDING;
+      ++st.att;
+      const int np = (int)st.np, nm = (int)st.nm, endc = (int)st.endc;
+      const int klo = np * 2 / 5, khi = np * 4 / 5;
+      if (khi <= klo) return fail(st, ROAD_ERR_RANDINT, rec);
+      int k = (int)rng.np_randint(klo, khi);
+      const int nd = (int)rng.np_randint(0, 4);
+      const int bcell = s.picks[k] & 0xffffu;
+      k = (int)(s.picks[k] >> 16);
+      int nb = 0;
+      const int ok = walk(bcell / L, bcell % L, nd, s.rb, &nb);
+      if (!ok) { erase(s.rb, nb); continue; }
+      if (nb + nm - k >= L * 2) { erase(s.rb, nb); continue; }
+      if (nb == 0) return fail(st, ROAD_ERR_EMPTY, rec);
+      const int eb = s.rb[nb - 1];
+      if (iabs(eb / L - endc / L) + iabs(eb % L - endc % L) < L * 3 / 4) { erase(s.rb, nb); continue; }
       // road = reversed(branch) + main[k:]
       for (int i = 0; i < nb / 2; ++i) { uint16_t t = s.rb[i]; s.rb[i] = s.rb[nb - 1 - i]; s.rb[nb - 1 - i] = t; }
-      stamp_road(cw, s.rb, nb, ri, s.mainr + k, nm - k, &maxdist);
-      starts[ri] = nb > 0 ? s.rb[0] : s.mainr[k];
+      int maxdist = (int)st.maxdist;
+      stamp_road(cw, s.rb, nb, (int)st.ri, s.mainr + k, nm - k, &maxdist);
+      st.maxdist = (uint32_t)maxdist;
+      st.start[st.ri] = (uint32_t)s.rb[0];
+      ++st.ri; st.att = 0;
     }
-    for (int ri = 0; ri < num_roads; ++ri) cw[starts[ri]] |= 1u << (5 + ri);
-    cw[endc] |= 1u << 4;
+    const int nr = (int)st.nr;
+    for (int ri = 0; ri < nr; ++ri) cw[st.start[ri]] |= 1u << (5 + ri);
+    cw[st.endc] |= 1u << 4;
     rec[0] = TD_LAYOUT_MAGIC;
-    rec[1] = (uint32_t)num_roads;
-    rec[2] = (uint32_t)endc;
-    rec[3] = (uint32_t)maxdist;
-    rec[4] = (uint32_t)starts[0];
-    rec[5] = (uint32_t)starts[1];
-    rec[6] = (uint32_t)starts[2];
+    rec[1] = (uint32_t)nr;
+    rec[2] = st.endc;
+    rec[3] = st.maxdist;
+    rec[4] = st.start[0];
+    rec[5] = nr > 1 ? st.start[1] : 0u;
+    rec[6] = nr > 2 ? st.start[2] : 0u;
     rec[7] = ROAD_OK;
+    st.phase = RP_NEW;
     return ROAD_OK;
+  }
+
+  TD_HD static int fail(RoadResume& st, int status, uint32_t* rec) {
+    rec[0] = 0; rec[1] = st.nr; rec[7] = (uint32_t)status;
+    st.phase = RP_NEW;
+    return status;
   }
 
   // One road's cells: rd[0..n) then tail[0..nt).  TDBoard.py:38-59.
@@ -269,14 +309,13 @@ TD_HD inline int layout_from_roads(int L, int num_roads, const int32_t* cells, c
   return ROAD_OK;
 }
 
-// TDGymBasic.reset (:42-51): num_roads = randint(1, 4) then create_road_v2, on one stream.
+// TDGymBasic.reset (:42-51): num_roads = randint(1, 4) then create_road_v2, on one
+// stream, in one uninterrupted call.
 template <class RNG>
 TD_HD inline int episode_layout_rng(RNG& rng, int L, void* scratch, int max_attempts, uint32_t* rec) {
   RoadGen<RNG> g{rng, L, road_scratch_carve(scratch, L), max_attempts};
-  int nr = (int)rng.np_randint(1, 4);
-  int st = g.generate(nr, rec);
-  if (st != ROAD_OK) { rec[0] = 0; rec[1] = (uint32_t)nr; rec[7] = (uint32_t)st; }
-  return st;
+  RoadResume st{};
+  return g.draw(st, 0x7fffffff, rec);
 }
 
 // Host form on a 625-word numpy state (RandomState.get_state() words + position).

@@ -1252,6 +1252,7 @@ __device__ void step_board(Smem<NC>& S, const Ctx& x, const StepArgs& a, int b, 
     const uint32_t* rec = a.nxt + ((size_t)b * NSLOT + lay_head % NSLOT) * a.slot_words;
     const uint32_t want = slot_tag(lay_head);
     bool ready = ld_relaxed(rec) == want;
+#ifndef TD_NO_SPIN
     if (!ready && ld_relaxed(a.lay_claim + b) != 0u) {
       // the ring ran dry while a refill wave holds the board: it is drawing exactly
       // this layout (typically one the reference never finishes, 2-5 ms of one lane
@@ -1264,6 +1265,7 @@ __device__ void step_board(Smem<NC>& S, const Ctx& x, const StepArgs& a, int b, 
       }
       ready = ready || ld_relaxed(rec) == want;
     }
+#endif
     if (ready) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       reset_board(S, u, x, rec);
@@ -1326,42 +1328,73 @@ __global__ __launch_bounds__(64) void td_step_kernel(StepArgs a) {
 // ---------------------------------------------------------------------------
 // episode layouts on the device
 // ---------------------------------------------------------------------------
-// LDS image of one layout draw: the board's numpy stream, the output record and
-// create_road_v2's scratch.  Lane 0 runs the (serial) generator entirely out of
-// LDS; the other lanes stage the stream and the record in and out.
+// LDS image of one layout draw: the board's numpy stream, the output record,
+// create_road_v2's scratch and the draw's resume state.  Lane 0 runs the (serial)
+// generator entirely out of LDS; the other lanes stage everything in and out.
 template <int NC>
 struct LayoutSmem {
   uint32_t mt[OPP_WORDS];
   uint32_t rec[LAYOUT_HDR + NC];
   uint8_t scratch[14 * NC + 64];
+  RoadResume res;
 };
+
+// Layout draws are resumable (RoadGen::draw): a refill gives each board a budget of
+// walks per launch, and a draw that runs out (in practice one the reference never
+// finishes, ~1,000 walks per retry loop) keeps its state in the board's HBM scratch
+// -- the RoadResume header, then the generator's arrays -- with the partial record
+// in the ring slot (its tag still the old one) and the stream position in np_mt.
+// The next refill continues it draw for draw.  So a refill launch runs at most
+// ~kRefillWalks walks per board -- except for a board whose ring is empty, whose
+// draw runs to the end at once (rare: the initial fill, or episodes shorter than the
+// refill can follow).
+__device__ __forceinline__ RoadResume* resume_hdr(const StepArgs& a, int b) {
+  return reinterpret_cast<RoadResume*>(a.scratch + (size_t)b * a.scratch_stride);
+}
 
 // TDGymBasic.reset's draws (:42-51) for board b into slot `slot` of its ring, as
 // layout number `n` of the stream: failing draws are skipped up to ``retries``
-// times.  The record is published for a step grid that may be running on another
+// times, at most ``budget`` walks are run (ROAD_PENDING: continued by a later call).
+// A finished record is published for a step grid that may be running on another
 // stream: plain stores, every lane's vmcnt(0), the barrier, ONE agent-scope
 // release, then the tag by an sc1 store (MI355X_MICROARCH.md § visibility, "Valid
 // forms", producer bullet).  Returns the road status of the last draw.
 template <int NC>
-__device__ int wave_layout(LayoutSmem<NC>& G, const StepArgs& a, int b, int retries, uint32_t* slot, uint32_t n) {
+__device__ int wave_layout(LayoutSmem<NC>& G, const StepArgs& a, int b, int retries, uint32_t* slot, uint32_t n,
+                           int budget) {
   const int lane = (int)threadIdx.x, L = a.L, lw = LAYOUT_HDR + L * L;
+  const int sbytes = (int)road_scratch_bytes(L);
   uint32_t* gmt = a.np_mt + (size_t)b * OPP_WORDS;
+  RoadResume* ghdr = resume_hdr(a, b);
+  uint8_t* gscr = a.scratch + (size_t)b * a.scratch_stride + sizeof(RoadResume);
   for (int i = lane; i < OPP_WORDS; i += 64) G.mt[i] = gmt[i];
+  if (lane < 16) reinterpret_cast<uint32_t*>(&G.res)[lane] = reinterpret_cast<const uint32_t*>(ghdr)[lane];
   __syncthreads();
+  const bool resumed = G.res.phase != RP_NEW;  // wave-uniform
+  if (resumed) {
+    for (int i = lane; i < sbytes / 4; i += 64) reinterpret_cast<uint32_t*>(G.scratch)[i] = reinterpret_cast<const uint32_t*>(gscr)[i];
+    for (int i = 1 + lane; i < lw; i += 64) G.rec[i] = slot[i];
+    __syncthreads();
+  }
   int st = ROAD_ERR_BOUND;
   if (lane == 0) {
     LazyMt rng{G.mt, 0, 0};
     rng.load();
+    RoadGen<LazyMt> g{rng, L, road_scratch_carve(G.scratch, L), kRoadAttempts};
     for (int t = 0; t <= retries; ++t) {
-      st = episode_layout_rng(rng, L, G.scratch, kRoadAttempts, G.rec);
-      if (st == ROAD_OK) break;
+      st = g.draw(G.res, budget, G.rec);
+      if (st == ROAD_OK || st == ROAD_PENDING) break;
     }
     rng.store();
   }
   st = __shfl(st, 0);
   __syncthreads();
   for (int i = lane; i < OPP_WORDS; i += 64) gmt[i] = G.mt[i];
-  if (st == ROAD_OK) {
+  if (lane < 16) reinterpret_cast<uint32_t*>(ghdr)[lane] = reinterpret_cast<const uint32_t*>(&G.res)[lane];
+  if (st == ROAD_PENDING) {  // keep the draw for the next call (published by the caller's claim release)
+    for (int i = lane; i < sbytes / 4; i += 64) reinterpret_cast<uint32_t*>(gscr)[i] = reinterpret_cast<const uint32_t*>(G.scratch)[i];
+    for (int i = 1 + lane; i < lw; i += 64) slot[i] = G.rec[i];
+  } else if (st == ROAD_OK) {
     for (int i = 1 + lane; i < lw; i += 64) slot[i] = G.rec[i];
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -1401,7 +1434,7 @@ __global__ __launch_bounds__(64) void td_reset_kernel(StepArgs a) {
     const uint32_t tail = a.lay_tail[b];
     uint32_t* slot = a.nxt + ((size_t)b * NSLOT + head % NSLOT) * a.slot_words;
     if (tail == head) {  // nothing staged: draw now
-      const int st = wave_layout(sh.gen, a, b, 0, slot, head);
+      const int st = wave_layout(sh.gen, a, b, 0, slot, head, 0x7fffffff);
       __syncthreads();
       if (st != ROAD_OK) {
         if (threadIdx.x == 0) a.reset_fail[b] = (uint8_t)st;
@@ -1460,9 +1493,11 @@ __global__ __launch_bounds__(64) void td_refill_kernel(StepArgs a) {
       const uint32_t h = ld_relaxed(a.lay_head + bb);
       while (t - h < (uint32_t)NSLOT) {
         uint32_t* slot = a.nxt + ((size_t)bb * NSLOT + t % NSLOT) * a.slot_words;
-        const int st = wave_layout(G, a, bb, kLayoutRetries, slot, t);
+        // an empty ring is urgent (the board needs this layout at its next episode end):
+        // its draw runs to the end; otherwise at most kRefillWalks walks this launch
+        const int st = wave_layout(G, a, bb, kLayoutRetries, slot, t, t == h ? 0x7fffffff : kRefillWalks);
         __syncthreads();
-        if (st != ROAD_OK) break;  // 65 failing draws in a row: the next refill tries again
+        if (st != ROAD_OK) break;  // out of walks (continued next launch), or 65 failing draws in a row
         ++t;
       }
       if (lane == 0) st_relaxed(a.lay_tail + bb, t);
