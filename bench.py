@@ -180,8 +180,12 @@ def main():
     B = args.boards or B_default
     K, W = args.steps, args.warmup
     seeds = shard.shard_seeds(args.seed, rank, B)
+    # info tensors (win, allow-next, fail codes, real actions, episode totals) are written
+    # every step -- except in multi-action mode, where the reference itself cannot build
+    # its info dict (TDDefense.py:87, TDMulti.py:134-135 raise) and SURVEY 8(d) config 3
+    # is the board-level step
     eng = TDEngine(L, B, mode, multi, 1, device=dev, np_seeds=seeds, py_seeds=seeds, autoreset=bool(args.autoreset),
-                   info=True)
+                   info=not multi)
     obs, _ = eng.reset_all()  # failing road draws (the reference raises/hangs) are redrawn
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
 
