@@ -31,6 +31,13 @@ def _register_all():
 _register_all()
 
 
+def make_vec(env_id, num_envs, **kwargs):
+    """AsyncVectorEnv stand-in (train/main.py:329-347): ``num_envs`` boards of ``env_id``
+    in one batched engine, numpy in / out (gym_TD.vector.VectorEnv)."""
+    from .vector import VectorEnv
+    return VectorEnv(env_id, num_envs, **kwargs)
+
+
 def make(env_id, **kwargs):
     """gym.make stand-in for images without gym: ``make('TD-def-small-v0')``."""
     from . import envs

@@ -444,3 +444,70 @@ def test_many_towers_vs_oracle():
         assert (eng.flags() == 0).all()
     finally:
         eng.close()
+
+
+def _norm_info(info):
+    def n(v):
+        if isinstance(v, dict):
+            return {k: n(x) for k, x in v.items()}
+        if isinstance(v, (list, tuple)):
+            return [n(x) for x in v]
+        if isinstance(v, np.ndarray):
+            return v.astype(np.int64).tolist()
+        if isinstance(v, (np.integer,)):
+            return int(v)
+        if isinstance(v, np.bool_):
+            return bool(v)
+        return v
+    return n({k: info[k] for k in ("RealAction", "Win", "AllowNextMove", "FailCode")})
+
+
+@pytest.mark.parametrize("env_id,difficulty", [("TD-def-small-v0", 1), ("TD-atk-small-v0", 2), ("TD-2p-small-v0", 1)])
+def test_async_vector_env_surface(env_id, difficulty):
+    """gym_TD.vector.VectorEnv answers train/main.py's AsyncVectorEnv calls: numpy
+    obs / rewards / dones and one info dict per env, equal to N oracle envs with
+    auto-reset (failing layout draws skipped on both sides)."""
+    from gym_TD.vector import VectorEnv
+    kind = env_id.split("-")[1]
+    L, N, steps = 10, 12, 150
+    ov = dict(base_LP=1, defender_init_cost=0, defender_cost_rate=0.05)
+    S = None
+    for s0 in range(2000, 2400, 16):
+        try:
+            orc = [O.Env(L, G.MODES[kind], difficulty, s0 + i, s0 + i, O.Config(**ov), O.Hyper(), road_attempts=1000)
+                   for i in range(N)]
+            S = s0
+            break
+        except O.RoadGenError:
+            continue
+    assert S is not None
+    with reference_settings(ov, False):
+        ve = VectorEnv(env_id, N, difficulty=difficulty, seed=S)
+    try:
+        assert len(ve.env_fns) == N
+        obs = ve.reset()
+        assert isinstance(obs, np.ndarray) and obs.shape == (N, 45, L, L)
+        for i, o in enumerate(orc):
+            assert np.array_equal(obs[i], o._board.get_states())
+        rng = np.random.RandomState(5)
+        for k in range(steps):
+            da = [policies.discrete_def(rng, L, o._board.map[0], 0.3) for o in orc] if kind != "atk" else None
+            aa = [policies.atk(rng) for _ in orc] if kind != "def" else None
+            if kind == "def":
+                act = np.array(da, dtype=np.int64)
+            elif kind == "atk":
+                act = np.stack(aa)
+            else:
+                act = {"Defender": np.array(da, dtype=np.int64), "Attacker": np.stack(aa)}
+            obs, rew, done, infos = ve.step(act)
+            assert isinstance(infos, tuple) and len(infos) == N
+            for i, o in enumerate(orc):
+                wo, wr, wd, winfo = o.step(None if da is None else da[i], None if aa is None else aa[i])
+                assert canon.fhex(rew[i]) == canon.fhex(wr), (k, i)
+                assert bool(done[i]) == wd, (k, i)
+                assert _norm_info(infos[i]) == _norm_info(winfo), (k, i, infos[i], winfo)
+                if wd:
+                    wo, _ = _oracle_reset_skipping(o)
+                assert np.array_equal(obs[i], wo), (k, i)
+    finally:
+        ve.close()
