@@ -249,6 +249,8 @@ def main():
     flags = eng.flags()
     t = shard.max_over_ranks(torch.tensor([elapsed, avg_kernel_s], dtype=torch.float64, device=coll))
     per_rank = shard.gather_stats(eng.episode_stats(clear=True).to(coll))
+    # the per-board payload (16 B per board: last episode's return, length, win)
+    recs = shard.gather_episode_records(*[t.to(coll) for t in eng.episode_records()])
     elapsed, avg_kernel_s = float(t[0]), float(t[1])
 
     if rank == 0:
@@ -286,7 +288,9 @@ def main():
             "board_flags": {name: int(((flags & bit) != 0).sum()) for name, bit in FLAG_BITS if ((flags & bit) != 0).any()},
             "episodes": {"finished": int(per_rank[:, 0].sum()),
                          "mean_return": float(per_rank[:, 1].sum() / max(float(per_rank[:, 0].sum()), 1.0)),
-                         "per_rank": [int(v) for v in per_rank[:, 0].tolist()]},
+                         "per_rank": [int(v) for v in per_rank[:, 0].tolist()],
+                         "boards_with_a_finished_episode": int((recs[2] >= 0).sum()),
+                         "last_episode_win_rate": float((recs[2] == 1).sum()) / max(int((recs[2] >= 0).sum()), 1)},
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(L, mode, multi, args.cpu_seconds, host_cores(), args.workload)

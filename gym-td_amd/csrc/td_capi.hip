@@ -71,6 +71,7 @@ struct td_handle {
   int stage_cap = 0;
   uint64_t* d_stamps = nullptr;  // TD_STAMPS diagnostic builds only (not owned)
   double* d_epstats = nullptr;   // [2] finished episodes, sum of their returns
+  td_episode_record* d_lastep = nullptr;  // [B] each board's last finished episode
   // Layout refills run on kSideStreams side streams in turn; the step stream never
   // waits for them (the rings give every board NSLOT episodes of slack, and
   // per-board claims keep concurrent refills apart).
@@ -322,6 +323,12 @@ td_handle* td_create(const td_config* cfg, int map_size, int n_boards, int mode,
   rc |= dalloc(&h->d_fail, B);
   rc |= dalloc(&h->d_stage, (size_t)h->stage_cap * h->lw);
   rc |= dalloc(&h->d_epstats, 2);
+  rc |= dalloc(&h->d_lastep, B);
+  if (!rc) {  // win = -1: no finished episode yet
+    std::vector<td_episode_record> init((size_t)B, td_episode_record{0.0, 0, -1});
+    if (hipMemcpy(h->d_lastep, init.data(), B * sizeof(td_episode_record), hipMemcpyHostToDevice) != hipSuccess)
+      rc = fail("episode records init");
+  }
   if (!rc && hipMemcpy(h->d_cfg, &h->dcfg, sizeof(TdDevCfg), hipMemcpyHostToDevice) != hipSuccess) rc = fail("cfg upload");
   for (int q = 0; q < kSideStreams && !rc; ++q)
     if (hipStreamCreateWithFlags(&h->side[q], hipStreamNonBlocking) != hipSuccess) rc = fail("side stream");
@@ -339,7 +346,7 @@ void td_destroy(td_handle* h) {
   (void)hipDeviceSynchronize();
   void* dptrs[] = {h->d_cfg, h->d_hdr, h->d_en_lp, h->d_en_mg, h->d_en_inf, h->d_tw_cd, h->d_tw_inf,
                    h->d_cells, h->d_opp, h->d_hot, h->d_np, h->d_nxt, h->d_scratch, h->d_lay_head, h->d_lay_tail,
-                   h->d_lay_claim, h->d_ovr_idx, h->d_mask, h->d_fail, h->d_stage, h->d_epstats};
+                   h->d_lay_claim, h->d_ovr_idx, h->d_mask, h->d_fail, h->d_stage, h->d_epstats, h->d_lastep};
   for (void* p : dptrs)
     if (p) (void)hipFree(p);
   if (h->ev_main) (void)hipEventDestroy(h->ev_main);
@@ -499,6 +506,7 @@ int td_step(td_handle* h, const td_step_io* io, void* stream) {
   a.win = io->win; a.allow_next = io->allow_next; a.ep_return = io->ep_return; a.ep_len = io->ep_len;
   a.stamps = h->d_stamps;
   a.ep_stats = h->d_epstats;
+  a.last_ep = h->d_lastep;
   // the refill goes first: it waits for the previous step only, so a board whose ring
   // is dry in this step can wait for it (td_step.hip step_board) without a cycle
   if (h->autoreset && (h->steps % refill_every(h->B)) == 0 && start_refill(h, s)) return -1;
@@ -512,6 +520,13 @@ int td_episode_stats(td_handle* h, double* dev_out, int clear, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   HIP_OK(hipMemcpyAsync(dev_out, h->d_epstats, 2 * sizeof(double), hipMemcpyDeviceToDevice, s));
   if (clear) HIP_OK(hipMemsetAsync(h->d_epstats, 0, 2 * sizeof(double), s));
+  return 0;
+}
+
+int td_episode_records(td_handle* h, td_episode_record* dev_out, void* stream) {
+  if (!h || !dev_out) return fail("td_episode_records: NULL argument");
+  HIP_OK(hipMemcpyAsync(dev_out, h->d_lastep, (size_t)h->B * sizeof(td_episode_record), hipMemcpyDeviceToDevice,
+                        (hipStream_t)stream));
   return 0;
 }
 

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include "td_common.h"
+#include "../../include/tdstep.h"
 
 namespace td {
 
@@ -53,6 +54,7 @@ struct StepArgs {
   double* ep_return;
   int32_t* ep_len;
   double* ep_stats;  // [2]: finished episodes, sum of their returns (accumulated by the step kernel)
+  td_episode_record* last_ep;  // [B]: each board's last finished episode (written on done)
   const uint8_t* reset_mask;  // reset kernel only (nullptr = all boards)
 };
 

@@ -1299,6 +1299,13 @@ __device__ void step_board(Smem<NC>& S, const Ctx& x, const StepArgs& a, int b, 
     if (a.real_def && !a.multi) a.real_def[b] = real_def;
     if (a.ep_return) a.ep_return[b] = ep_ret;
     if (a.ep_len) a.ep_len[b] = ep_steps;
+    if (done && a.last_ep) {  // the board's last finished episode (td_episode_records)
+      td_episode_record r;
+      r.ret = ep_ret;
+      r.length = ep_steps;
+      r.win = win;
+      a.last_ep[b] = r;
+    }
     if (done && a.ep_stats) {  // device-side episode accounting (SURVEY §8(b) td_episode_stats)
       atomicAdd(&a.ep_stats[0], 1.0);
       atomicAdd(&a.ep_stats[1], ep_ret);

@@ -234,6 +234,15 @@ class TDEngine(object):
                                              self._stream()))
         return out
 
+    def episode_records(self):
+        """Each board's last finished episode (td_episode_records): (return f64 [B],
+        length int32 [B], win int32 [B], -1 before the board's first finished episode),
+        device tensors -- the per-board payload gathered across ranks."""
+        raw = torch.empty((self.B, 16), dtype=torch.uint8, device=self.device)
+        _lib.check(_lib.lib.td_episode_records(self._h, _lib.ctypes.c_void_p(raw.data_ptr()), self._stream()))
+        ints = raw[:, 8:].contiguous().view(torch.int32)
+        return raw[:, :8].contiguous().view(torch.float64).reshape(self.B), ints[:, 0], ints[:, 1]
+
     def flags(self):
         f = np.zeros(self.B, dtype=np.int32)
         _lib.check(_lib.lib.td_get_flags(self._h, _lib.ptr(f, _lib.ctypes.c_int32)))

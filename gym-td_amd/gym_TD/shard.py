@@ -46,3 +46,31 @@ def gather_stats(stats, dst=0):
     out = [torch.zeros_like(stats) for _ in range(world)] if rank == dst else None
     dist.gather(stats, out, dst=dst)
     return torch.stack(out) if rank == dst else None
+
+
+def pack_episode_records(ret, length, win):
+    """(return f64, length i32, win i32) per board -> [B, 16] uint8 (td_episode_record)."""
+    B = ret.shape[0]
+    raw = torch.empty((B, 16), dtype=torch.uint8, device=ret.device)
+    raw[:, :8] = ret.to(torch.float64).contiguous().reshape(B, 1).view(torch.uint8)
+    raw[:, 8:12] = length.to(torch.int32).contiguous().reshape(B, 1).view(torch.uint8)
+    raw[:, 12:] = win.to(torch.int32).contiguous().reshape(B, 1).view(torch.uint8)
+    return raw
+
+
+def unpack_episode_records(raw):
+    ints = raw[:, 8:].contiguous().view(torch.int32)
+    return raw[:, :8].contiguous().view(torch.float64).reshape(-1), ints[:, 0], ints[:, 1]
+
+
+def gather_episode_records(ret, length, win, dst=0):
+    """Gather every rank's per-board last-episode records on ``dst`` -- 16 B per board
+    (return f64, length i32, win i32), the per-board payload of SURVEY.md 8(e), once per
+    reporting interval -- as [world * B] tensors in global board order.  None elsewhere."""
+    raw = pack_episode_records(ret, length, win)
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return unpack_episode_records(raw)
+    rank, world = dist.get_rank(), dist.get_world_size()
+    out = [torch.zeros_like(raw) for _ in range(world)] if rank == dst else None
+    dist.gather(raw, out, dst=dst)
+    return unpack_episode_records(torch.cat(out)) if rank == dst else None

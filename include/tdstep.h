@@ -143,6 +143,18 @@ int td_step(td_handle* h, const td_step_io* io, void* stream);
  * multi-GPU driver gathers over RCCL. */
 int td_episode_stats(td_handle* h, double* dev_out, int clear, void* stream);
 
+/* Each board's last finished episode, the per-episode record a trainer collects
+ * (train/main.py:155-166: total reward, length, win): dev_out = B records of 16 bytes,
+ * { f64 return; i32 length; i32 win (1, 0, or -1 before the first finished episode) },
+ * device memory, asynchronous on `stream`.  SURVEY.md §8(e): the per-board payload the
+ * multi-GPU driver gathers over RCCL once per reporting interval. */
+typedef struct td_episode_record {
+  double ret;
+  int32_t length;
+  int32_t win;
+} td_episode_record;
+int td_episode_records(td_handle* h, td_episode_record* dev_out, void* stream);
+
 /* Layout records. */
 int td_layout_words(int map_size);
 int td_layout_from_roads(int map_size, int num_roads, const int32_t* cells, const int32_t* offsets, uint32_t* rec);

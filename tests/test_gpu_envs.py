@@ -159,6 +159,7 @@ def test_vecenv_autoreset_vs_oracle():
         for b, o in enumerate(orc):
             assert np.array_equal(obs[b], o._board.get_states())
         rets = np.zeros(B)
+        last = (np.zeros(B), np.zeros(B, np.int32), np.full(B, -1, np.int32))  # td_episode_records
         rng = np.random.RandomState(9)
         resets = skipped = 0
         for k in range(steps):
@@ -167,12 +168,13 @@ def test_vecenv_autoreset_vs_oracle():
             ob, rw, dn = obs_t.cpu().numpy(), rew_t.cpu().numpy(), done_t.cpu().numpy()
             er, el = infos["episode_return"].cpu().numpy(), infos["episode_length"].cpu().numpy()
             for b, o in enumerate(orc):
-                wo, wr, wd, _ = o.step(int(acts[b]))
+                wo, wr, wd, winfo = o.step(int(acts[b]))
                 rets[b] += wr
                 assert canon.fhex(rw[b]) == canon.fhex(wr), (k, b)
                 assert bool(dn[b]) == wd, (k, b)
                 if wd:
                     assert canon.fhex(er[b]) == canon.fhex(rets[b]) and int(el[b]) == o._board.steps, (k, b)
+                    last[0][b], last[1][b], last[2][b] = rets[b], o._board.steps, int(winfo["Win"])
                     rets[b] = 0.0
                     wo, s = _oracle_reset_skipping(o)
                     skipped += s
@@ -180,6 +182,10 @@ def test_vecenv_autoreset_vs_oracle():
                 assert np.array_equal(ob[b], wo), (k, b, np.argwhere(ob[b] != wo)[:5].tolist())
         assert resets > 3 * B  # several episodes per board
         assert skipped > 0, "no failing layout draw was exercised; widen the run"
+        r_ret, r_len, r_win = eng.episode_records()
+        assert [canon.fhex(v) for v in r_ret.cpu().numpy()] == [canon.fhex(v) for v in last[0]]
+        assert r_len.cpu().numpy().tolist() == last[1].tolist()
+        assert r_win.cpu().numpy().tolist() == last[2].tolist()
         assert (eng.flags() == 0).all()
     finally:
         ve.close()

@@ -32,20 +32,31 @@ def _run_boards(seeds):
         acts = [r.randint(0, 6 * L * L + 1) for r in rngs]
         done = np.zeros(len(envs), bool)
         ep = np.zeros(len(envs))
+        ln = np.zeros(len(envs), np.int32)
+        win = np.full(len(envs), -1, np.int32)
         for i, (e, a) in enumerate(zip(envs, acts)):
-            _, r, d, _ = e.step(int(a))
+            _, r, d, info = e.step(int(a))
             ret[i] += r
             if d:
-                done[i], ep[i] = True, ret[i]
+                done[i], ep[i], ln[i], win[i] = True, ret[i], e._board.steps, int(info["Win"])
                 ret[i] = 0.0
                 e.reset()
-        out.append((done, ep))
+        out.append((done, ep, ln, win))
     return out
+
+
+def _last_records(trace):
+    """Each board's last finished episode (td_episode_records' payload)."""
+    n = len(trace[0][0])
+    ret, ln, win = np.zeros(n), np.zeros(n, np.int32), np.full(n, -1, np.int32)
+    for done, ep, l, w in trace:
+        ret[done], ln[done], win[done] = ep[done], l[done], w[done]
+    return torch.from_numpy(ret), torch.from_numpy(ln), torch.from_numpy(win)
 
 
 def _stats(trace):
     tot = torch.zeros(2, dtype=torch.float64)
-    for done, ep in trace:
+    for done, ep, _, _ in trace:
         tot += shard.episode_stats(torch.from_numpy(done), torch.from_numpy(ep))
     return tot
 
@@ -55,11 +66,13 @@ def _worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         seeds = shard.shard_seeds(2000, rank, BOARDS_PER_RANK)
-        stats = _stats(_run_boards(seeds))
+        trace = _run_boards(seeds)
+        stats = _stats(trace)
         t = shard.max_over_ranks(torch.tensor([float(rank + 1)], dtype=torch.float64))
         got = shard.gather_stats(stats)
+        recs = shard.gather_episode_records(*_last_records(trace))
         if rank == 0:
-            q.put((got.numpy().tolist(), float(t[0])))
+            q.put((got.numpy().tolist(), float(t[0]), [r.numpy().tolist() for r in recs]))
     finally:
         dist.destroy_process_group()
 
@@ -86,13 +99,16 @@ def test_gloo_two_ranks_match_one_process():
     for p in procs:
         p.start()
     try:
-        per_rank, tmax = q.get(timeout=300)
+        per_rank, tmax, recs = q.get(timeout=300)
     finally:
         for p in procs:
             p.join(timeout=60)
     assert all(p.exitcode == 0 for p in procs)
     assert tmax == float(world)
-    one = _stats(_run_boards(shard.shard_seeds(2000, 0, world * BOARDS_PER_RANK)))
+    trace = _run_boards(shard.shard_seeds(2000, 0, world * BOARDS_PER_RANK))
+    one = _stats(trace)
+    want = [r.numpy().tolist() for r in _last_records(trace)]
+    assert recs == want  # per-board records, 16 B each, in global board order
     per_rank = np.asarray(per_rank)
     assert per_rank.shape == (world, 2)
     assert per_rank[:, 0].sum() == float(one[0]) > 0
