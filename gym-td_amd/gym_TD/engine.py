@@ -37,10 +37,13 @@ class TDEngine(object):
     autoreset: a board that finishes starts its next episode inside the same
           step and the returned obs is the new episode's first obs (gym 0.21
           AsyncVectorEnv semantics); reward/done/info describe the finished step.
+    host_io: step inputs and outputs live in pinned host memory that the kernels
+          read and write directly (zero-copy).  For the single-env classes: one
+          launch and one stream synchronisation per step, no per-tensor copies.
     """
 
     def __init__(self, map_size, n_boards, mode="def", multi_action=None, difficulty=1, device=None,
-                 np_seeds=None, py_seeds=None, autoreset=True, info=True, cfg=None, hp=None):
+                 np_seeds=None, py_seeds=None, autoreset=True, info=True, cfg=None, hp=None, host_io=False):
         hp = hp or P.hyper_parameters
         if multi_action is None:
             multi_action = bool(hp.allow_multiple_actions)
@@ -59,25 +62,32 @@ class TDEngine(object):
         self.lw = _lib.lib.td_layout_words(self.L)
         self.autoreset = bool(autoreset)
         _lib.check(_lib.lib.td_set_autoreset(h, int(self.autoreset)))
-        B, L, dev = self.B, self.L, self.device
-        self.obs = torch.zeros((B, _lib.NCH, L, L), dtype=torch.float32, device=dev)
-        self.reward = torch.zeros(B, dtype=torch.float64, device=dev)
-        self.done = torch.zeros(B, dtype=torch.uint8, device=dev)
+        B, L = self.B, self.L
+        self.host_io = bool(host_io)
+        dev = torch.device("cpu") if self.host_io else self.device
+        zeros = (lambda shape, dtype: torch.zeros(shape, dtype=dtype).pin_memory()) if self.host_io else \
+            (lambda shape, dtype: torch.zeros(shape, dtype=dtype, device=dev))
+        self.obs = zeros((B, _lib.NCH, L, L), torch.float32)
+        self.reward = zeros(B, torch.float64)
+        self.done = zeros(B, torch.uint8)
         self.info_enabled = bool(info)
         self.win = self.allow_next = self.ep_return = self.ep_len = None
         self.real_def = self.fail_def = self.real_atk = self.fail_atk = None
         if info:
-            self.win = torch.zeros(B, dtype=torch.int8, device=dev)
-            self.allow_next = torch.zeros(B, dtype=torch.uint8, device=dev)
-            self.ep_return = torch.zeros(B, dtype=torch.float64, device=dev)
-            self.ep_len = torch.zeros(B, dtype=torch.int32, device=dev)
+            self.win = zeros(B, torch.int8)
+            self.allow_next = zeros(B, torch.uint8)
+            self.ep_return = zeros(B, torch.float64)
+            self.ep_len = zeros(B, torch.int32)
             if mode != "atk":
                 shape = (B, 6, L, L) if self.multi else (B,)
-                self.real_def = torch.zeros(shape, dtype=torch.int64, device=dev)
-                self.fail_def = torch.zeros(B, dtype=torch.int32, device=dev)
+                self.real_def = zeros(shape, torch.int64)
+                self.fail_def = zeros(B, torch.int32)
             if mode != "def":
-                self.real_atk = torch.zeros((B, 3, 8), dtype=torch.int64, device=dev)
-                self.fail_atk = torch.zeros((B, 3), dtype=torch.int32, device=dev)
+                self.real_atk = zeros((B, 3, 8), torch.int64)
+                self.fail_atk = zeros((B, 3), torch.int32)
+        if self.host_io:  # action staging, read by the kernel from pinned host memory
+            self._def_in = zeros((B, 6, L, L) if self.multi else (B,), torch.int64) if mode != "atk" else None
+            self._atk_in = zeros((B, 3, 8), torch.int64) if mode != "def" else None
         self._io = _lib.TdStepIO()
         for name in ("obs", "reward", "done", "real_def", "real_atk", "fail_def", "fail_atk", "win",
                      "allow_next", "ep_return", "ep_len"):
@@ -192,6 +202,15 @@ class TDEngine(object):
         (clone them to keep a history)."""
         io = self._io
         keep = []
+        if self.host_io:
+            if self.mode != "atk":
+                self._def_in.numpy()[...] = np.asarray(def_act, dtype=np.int64).reshape(self._def_in.shape)
+                io.def_act = self._def_in.data_ptr()
+            if self.mode != "def":
+                self._atk_in.numpy()[...] = np.asarray(atk_act, dtype=np.int64).reshape(self._atk_in.shape)
+                io.atk_act = self._atk_in.data_ptr()
+            _lib.check(_lib.lib.td_step(self._h, io, self._stream()))
+            return self.obs, self.reward, self.done
         if self.mode != "atk":
             d = _as_dev(def_act, torch.int64, self.device)
             exp = (self.B, 6, self.L, self.L) if self.multi else (self.B,)

@@ -108,7 +108,7 @@ class _TDBasic(object):
         self.difficulty = difficulty
         self._multi = bool(P.hyper_parameters.allow_multiple_actions)
         self._engine = TDEngine(self.map_size, 1, self._mode, self._multi, difficulty if self._mode != "2p" else 1,
-                                device=device, autoreset=False, info=True)
+                                device=device, autoreset=False, info=True, host_io=True)
         if opponent_seed is not None:
             self._engine.seed(py_seeds=[opponent_seed])
         else:
@@ -134,7 +134,7 @@ class _TDBasic(object):
         st = self._engine.export_state(0, 1)
         self.num_roads = int(st["hdr"]["num_roads"][0])
         self.attacker_cd = self.defender_cd = 0
-        self._obs = obs[0].cpu().numpy()
+        self._obs = obs[0].numpy().copy()
         return self._obs.copy()
 
     @property
@@ -144,11 +144,12 @@ class _TDBasic(object):
     def _run(self, def_act=None, atk_act=None):
         e = self._engine
         e.step(def_act, atk_act)
-        self._obs = e.obs[0].cpu().numpy()
-        reward = float(e.reward[0].item())
-        done = bool(e.done[0].item())
-        win = int(e.win[0].item())
-        an = int(e.allow_next[0].item())
+        torch.cuda.current_stream(e.device).synchronize()  # the kernel wrote the pinned outputs
+        self._obs = e.obs[0].numpy().copy()
+        reward = float(e.reward[0])
+        done = bool(e.done[0])
+        win = int(e.win[0])
+        an = int(e.allow_next[0])
         self.attacker_cd = 0 if (an & 1) else 2  # only "<= 1" is observable from the step
         self.defender_cd = 0 if (an & 2) else 2
         return self._obs.copy(), reward, done, (None if win < 0 else bool(win)), an
@@ -190,9 +191,9 @@ class TDDefense(_TDBasic):
         obs, reward, done, win, an = self._run(def_act=a)
         e = self._engine
         if self._multi:
-            real, fc = e.real_def[0].cpu().numpy(), None  # the reference raises here (TDDefense.py:87)
+            real, fc = e.real_def[0].numpy().copy(), None  # the reference raises here (TDDefense.py:87)
         else:
-            real, fc = int(e.real_def[0].item()), int(e.fail_def[0].item())
+            real, fc = int(e.real_def[0]), int(e.fail_def[0])
         return obs, reward, done, {"RealAction": real, "Win": win, "AllowNextMove": bool(an & 2), "FailCode": fc}
 
 
@@ -213,9 +214,9 @@ class TDAttack(_TDBasic):
         a = np.asarray(action, dtype=np.int64).reshape(1, 3, 8)
         obs, reward, done, win, an = self._run(atk_act=a)
         e = self._engine
-        fa = e.fail_atk[0].cpu().numpy()
+        fa = e.fail_atk[0].numpy()
         fc = [int(v) for v in fa if v >= 0]
-        return obs, reward, done, {"RealAction": e.real_atk[0].cpu().numpy(), "Win": win,
+        return obs, reward, done, {"RealAction": e.real_atk[0].numpy().copy(), "Win": win,
                                    "AllowNextMove": bool(an & 1), "FailCode": fc}
 
 
@@ -248,17 +249,17 @@ class TDMulti(_TDBasic):
         a = np.asarray(action["Attacker"], dtype=np.int64).reshape(1, 3, 8)
         obs, reward, done, win, an = self._run(def_act=d, atk_act=a)
         e = self._engine
-        real = {"Attacker": e.real_atk[0].cpu().numpy()}
+        real = {"Attacker": e.real_atk[0].numpy().copy()}
         if self._multi:
-            real["Defender"] = e.real_def[0].cpu().numpy()
+            real["Defender"] = e.real_def[0].numpy().copy()
             fc = None  # the reference raises here (TDMulti.py:134-135)
         else:
-            rd = int(e.real_def[0].item())
+            rd = int(e.real_def[0])
             real["Defender"] = rd
             if rd != L * L * 6:
                 real = rd  # TDMulti.py:257 replaces the whole dict
-            fa = e.fail_atk[0].cpu().numpy()
-            fc = {"Attacker": [int(v) for v in fa if v >= 0], "Defender": int(e.fail_def[0].item())}
+            fa = e.fail_atk[0].numpy()
+            fc = {"Attacker": [int(v) for v in fa if v >= 0], "Defender": int(e.fail_def[0])}
         if win is not None:
             win = {"Defender": win, "Attacker": not win}
         return obs, reward, done, {"RealAction": real, "Win": win,
