@@ -279,11 +279,11 @@ class TDVecEnv(object):
     """
 
     def __init__(self, map_size, num_envs, mode="def", difficulty=1, multi_action=None, seed=0, global_offset=0,
-                 device=None, info=True, autoreset=True):
+                 device=None, info=True, autoreset=True, host_io=False):
         self.map_size, self.num_envs, self.mode = int(map_size), int(num_envs), mode
         seeds = np.arange(num_envs, dtype=np.int64) + int(seed) + int(global_offset)
         self.engine = TDEngine(map_size, num_envs, mode, multi_action, difficulty, device=device,
-                               np_seeds=seeds, py_seeds=seeds, autoreset=autoreset, info=info)
+                               np_seeds=seeds, py_seeds=seeds, autoreset=autoreset, info=info, host_io=host_io)
         L = self.map_size
         self.observation_space = Box(low=0., high=1., shape=(45, L, L), dtype=np.float32)
         dspace = (Box(low=0., high=2., shape=(6, L, L), dtype=np.int64) if self.engine.multi

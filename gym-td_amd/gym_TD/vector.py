@@ -9,8 +9,9 @@ one ``TDEngine`` on the GPU: one kernel launch per step instead of N worker
 processes, auto-reset as AsyncVectorEnv does it (a finished env's returned obs is
 its next episode's first obs; reward / done / info describe the finished step).
 
-Numpy in, numpy out (copied from the device every step); a trainer that keeps its
-rollout on the GPU uses ``gym_TD.envs.TDVecEnv`` (torch tensors) instead.
+Numpy in, numpy out: the engine's inputs and outputs live in pinned host memory
+that the kernels read and write directly (``TDEngine(host_io=True)``); a trainer
+that keeps its rollout on the GPU uses ``gym_TD.envs.TDVecEnv`` (device tensors).
 """
 import numpy as np
 import torch
@@ -50,8 +51,9 @@ class VectorEnv(object):
         self._multi = bool(P.hyper_parameters.allow_multiple_actions)
         self._seed = 0 if seed is None else int(seed)
         self._difficulty = difficulty
+        # host_io: the kernels write the numpy outputs straight into pinned host memory
         self.vec = _envs.TDVecEnv(self.map_size, self.num_envs, self.kind, difficulty=difficulty, seed=self._seed,
-                                  device=device, info=True)
+                                  device=device, info=True, host_io=True)
         self.observation_space = self.vec.observation_space
         self.single_action_space = self.vec.action_space
         self.action_space = self.vec.action_space
@@ -71,36 +73,32 @@ class VectorEnv(object):
         raise NotImplementedError("seed the VectorEnv through its constructor (seed + env index)")
 
     def reset(self):
-        return self.vec.reset().cpu().numpy()
+        return self.vec.reset().numpy().copy()
 
     def _actions(self, actions):
-        dev = self.vec.engine.device
         if self.kind == "2p":
             if isinstance(actions, dict):
                 d, a = actions["Defender"], actions["Attacker"]
             else:  # a sequence of per-env dicts
                 d = np.stack([np.asarray(x["Defender"]) for x in actions])
                 a = np.stack([np.asarray(x["Attacker"]) for x in actions])
-            return (torch.as_tensor(np.asarray(d), dtype=torch.int64, device=dev),
-                    torch.as_tensor(np.asarray(a), dtype=torch.int64, device=dev))
-        return torch.as_tensor(np.asarray(actions), dtype=torch.int64, device=dev)
+            return np.asarray(d, dtype=np.int64), np.asarray(a, dtype=np.int64)
+        return np.asarray(actions, dtype=np.int64)
 
     def step(self, actions):
         obs, rew, done, inf = self.vec.step(self._actions(actions))
-        obs = obs.cpu().numpy()
-        rew = rew.cpu().numpy()
-        done = done.cpu().numpy().astype(bool)
-        return obs, rew, done, self._infos(inf)
+        torch.cuda.current_stream(self.vec.engine.device).synchronize()  # outputs are in pinned host memory
+        return obs.numpy().copy(), rew.numpy().copy(), done.numpy().astype(bool), self._infos(inf)
 
     def _infos(self, inf):
         """Per-env info dicts with the single envs' keys (TDDefense.py:87, TDAttack.py:56, TDMulti.py:130-138)."""
         L, N, kind = self.map_size, self.num_envs, self.kind
-        win = inf["Win"].cpu().numpy()
-        an = inf["AllowNextMove"].cpu().numpy()
-        rd = inf["RealAction"].cpu().numpy() if "RealAction" in inf else None
-        fd = inf["FailCode"].cpu().numpy() if "FailCode" in inf else None
-        ra = inf["RealActionAttacker"].cpu().numpy() if "RealActionAttacker" in inf else None
-        fa = inf["FailCodeAttacker"].cpu().numpy() if "FailCodeAttacker" in inf else None
+        win = inf["Win"].numpy()
+        an = inf["AllowNextMove"].numpy()
+        rd = inf["RealAction"].numpy().copy() if "RealAction" in inf else None
+        fd = inf["FailCode"].numpy() if "FailCode" in inf else None
+        ra = inf["RealActionAttacker"].numpy().copy() if "RealActionAttacker" in inf else None
+        fa = inf["FailCodeAttacker"].numpy() if "FailCodeAttacker" in inf else None
         out = []
         for i in range(N):
             w = None if win[i] < 0 else bool(win[i])
