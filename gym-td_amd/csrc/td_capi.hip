@@ -523,6 +523,23 @@ int td_episode_stats(td_handle* h, double* dev_out, int clear, void* stream) {
   return 0;
 }
 
+int td_opponent(td_handle* h, int side, int level, const uint8_t* host_mask, void* stream) {
+  if (!h) return fail("NULL handle");
+  if (side == 0 && (level < 0 || level > 1)) return fail("td_opponent: random_enemy_lv%d does not exist", level);
+  if (side == 1 && (level < 0 || level > 2)) return fail("td_opponent: random_tower_lv%d does not exist", level);
+  if (side != 0 && side != 1) return fail("td_opponent: side must be 0 (enemy) or 1 (tower)");
+  hipStream_t s = (hipStream_t)stream;
+  std::vector<uint8_t> mask((size_t)h->B, 1);
+  if (host_mask) std::memcpy(mask.data(), host_mask, (size_t)h->B);
+  HIP_OK(hipDeviceSynchronize());
+  HIP_OK(hipMemcpy(h->d_mask, mask.data(), (size_t)h->B, hipMemcpyHostToDevice));
+  StepArgs a = base_args(h);
+  a.reset_mask = h->d_mask;
+  HIP_OK(launch_opponent(a, side, level, s));
+  HIP_OK(hipStreamSynchronize(s));
+  return 0;
+}
+
 int td_episode_records(td_handle* h, td_episode_record* dev_out, void* stream) {
   if (!h || !dev_out) return fail("td_episode_records: NULL argument");
   HIP_OK(hipMemcpyAsync(dev_out, h->d_lastep, (size_t)h->B * sizeof(td_episode_record), hipMemcpyDeviceToDevice,

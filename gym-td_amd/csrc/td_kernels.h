@@ -61,6 +61,9 @@ struct StepArgs {
 hipError_t launch_step(const StepArgs& a, hipStream_t s, bool reset);
 // Draw staged layouts for every board whose ring has a free slot (side stream).
 hipError_t launch_refill(const StepArgs& a, hipStream_t s);
+// The built-in opponent (side 0: random_enemy_lv<level>, 1: random_tower_lv<level>)
+// on the boards in a.reset_mask (nullptr = all).
+hipError_t launch_opponent(const StepArgs& a, int side, int level, hipStream_t s);
 
 constexpr int NSLOT = 4;  // staged layouts per board: four episodes of slack for the refill
 __host__ __device__ inline uint32_t slot_tag(uint32_t n) { return 0x80000000u | (n & 0x7fffffffu); }

@@ -1332,6 +1332,61 @@ __global__ __launch_bounds__(64) void td_step_kernel(StepArgs a) {
   step_board<NC, LT, MODE>(S, x, a, b, P);
 }
 
+// The built-in opponents called on their own, between steps (TDGymBasic.py:81-292,
+// called directly by demo.py:78-79): random_enemy_lv{0,1} (side 0) or
+// random_tower_lv{0,1,2} (side 1) for every masked board, on the board's opponent
+// stream, with the reference's cool-down check and update.  No observation.
+template <int LT>
+__global__ __launch_bounds__(64) void td_opponent_kernel(StepArgs a, int side, int level) {
+  constexpr int NC = LT ? LT * LT : MAX_KERNEL_L * MAX_KERNEL_L;
+  __shared__ Smem<NC> S;
+  const int b = blockIdx.x;
+  if (b >= a.B) return;
+  if (a.reset_mask && !a.reset_mask[b]) return;
+  stage_cfg(S, a.cfg);
+  const int L = LT ? LT : a.L;
+  const Ctx x{S.cfg, L, L * L, (int)threadIdx.x};
+  Prefetch P;
+  prefetch_issue(P, a, b, x.lane, x.NCr, false);
+  U u;
+  load_board(S, u, x, a, b, P);
+  if (u.num_roads < 1 || u.num_roads > 3) return;  // never reset: nothing to act on
+  uint32_t* const hot = a.opp_hot + (size_t)b * HOT_WORDS;
+  WaveMt R{a.opp_mt + (size_t)b * OPP_WORDS, lane_word(P.w, PF_HOT + 0), lane_word(P.w, PF_HOT + 1)};
+  R.cn = lane_word(P.w, PF_HOT + 2);
+  R.cbase = R.pos;
+  R.cache = __shfl(P.w, PF_HOT + 4 + (x.lane & 7));
+  if (side == 0) opponent_enemy(S, u, x, R, level);
+  else opponent_tower(S, u, x, R, level);
+  __syncthreads();
+  R.prefetch(x.lane);  // the next step expects the hot record primed
+  const size_t eb = (size_t)b * ECAP;
+  for (int i = x.lane; i < u.n; i += 64) {
+    a.en_lp[eb + i] = S.eLP[i];
+    a.en_mg[eb + i] = S.eMg[i];
+    a.en_inf[eb + i] = S.eInf[i];
+  }
+  store_cells(S, u, x, a, b);
+  store_board(S, u, x, a, b);
+  if (x.lane == 0) { hot[0] = R.pos; hot[1] = R.tw; hot[2] = R.cn; }
+  if (x.lane < 8) hot[4 + x.lane] = R.cache;
+}
+
+template <int LT>
+static hipError_t launch_opponent2(const StepArgs& a, int side, int level, hipStream_t s) {
+  hipLaunchKernelGGL(td_opponent_kernel<LT>, dim3(a.B), dim3(64), 0, s, a, side, level);
+  return hipGetLastError();
+}
+
+hipError_t launch_opponent(const StepArgs& a, int side, int level, hipStream_t s) {
+  switch (a.L) {
+    case 10: return launch_opponent2<10>(a, side, level, s);
+    case 20: return launch_opponent2<20>(a, side, level, s);
+    case 30: return launch_opponent2<30>(a, side, level, s);
+    default: return launch_opponent2<0>(a, side, level, s);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // episode layouts on the device
 // ---------------------------------------------------------------------------

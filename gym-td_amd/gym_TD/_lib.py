@@ -78,6 +78,7 @@ def _load():
         "td_get_flags": (ctypes.c_int, [c_vp, c_i32p]),
         "td_episode_stats": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int, c_vp]),
         "td_episode_records": (ctypes.c_int, [c_vp, c_vp, c_vp]),
+        "td_opponent": (ctypes.c_int, [c_vp, ctypes.c_int, ctypes.c_int, c_u8p, c_vp]),
         "td_py_seed": (None, [c_u32p, ctypes.c_uint32]),
         "td_np_seed": (None, [c_u32p, ctypes.c_uint32]),
         "td_mt_next": (ctypes.c_uint32, [c_u32p]),

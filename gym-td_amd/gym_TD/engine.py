@@ -262,6 +262,15 @@ class TDEngine(object):
         ints = raw[:, 8:].contiguous().view(torch.int32)
         return raw[:, :8].contiguous().view(torch.float64).reshape(self.B), ints[:, 0], ints[:, 1]
 
+    def opponent(self, side, level, mask=None):
+        """Run the built-in opponent on its own (TDGymBasic.py:81-292): side 'enemy'
+        (random_enemy_lv<level>) or 'tower' (random_tower_lv<level>), boards in mask."""
+        m = None
+        if mask is not None:
+            m = np.ascontiguousarray(np.asarray(mask, dtype=np.uint8).reshape(self.B))
+        _lib.check(_lib.lib.td_opponent(self._h, {"enemy": 0, "tower": 1}[side], int(level),
+                                        _lib.ptr(m, _lib.ctypes.c_uint8) if m is not None else None, self._stream()))
+
     def flags(self):
         f = np.zeros(self.B, dtype=np.int32)
         _lib.check(_lib.lib.td_get_flags(self._h, _lib.ptr(f, _lib.ctypes.c_int32)))

@@ -160,11 +160,23 @@ class _TDBasic(object):
     def close(self):
         self._engine.close()
 
-    def _opponent_only(self, *a, **k):
-        raise NotImplementedError("built-in opponents run inside the device step; they cannot be called directly")
+    # The built-in opponents called directly (TDGymBasic.py:81-292; demo.py:78-79 drives a
+    # TD-2p env this way): they act on the board now, with the reference's cool-down
+    # check and update, on this env's opponent stream; the next step() shows the result.
+    def random_enemy_lv0(self):
+        self._engine.opponent("enemy", 0)
 
-    random_enemy_lv0 = random_enemy_lv1 = _opponent_only
-    random_tower_lv0 = random_tower_lv1 = random_tower_lv2 = _opponent_only
+    def random_enemy_lv1(self):
+        self._engine.opponent("enemy", 1)
+
+    def random_tower_lv0(self):
+        self._engine.opponent("tower", 0)
+
+    def random_tower_lv1(self):
+        self._engine.opponent("tower", 1)
+
+    def random_tower_lv2(self):
+        self._engine.opponent("tower", 2)
 
 
 class TDDefense(_TDBasic):

@@ -155,6 +155,13 @@ typedef struct td_episode_record {
 } td_episode_record;
 int td_episode_records(td_handle* h, td_episode_record* dev_out, void* stream);
 
+/* The built-in opponent acting on its own between steps, as TDGymBasic's methods do when
+ * called directly (TDGymBasic.py:81-108 random_enemy_lv0/1, :111-292 random_tower_lv0/1/2;
+ * demo.py:78-79): side 0 = random_enemy_lv<level>, side 1 = random_tower_lv<level>, for the
+ * boards in host_mask (NULL = all), on each board's opponent stream, with the reference's
+ * cool-down check and update.  Synchronous. */
+int td_opponent(td_handle* h, int side, int level, const uint8_t* host_mask, void* stream);
+
 /* Layout records. */
 int td_layout_words(int map_size);
 int td_layout_from_roads(int map_size, int num_roads, const int32_t* cells, const int32_t* offsets, uint32_t* rec);

@@ -517,3 +517,38 @@ def test_async_vector_env_surface(env_id, difficulty):
                 assert np.array_equal(obs[i], wo), (k, i)
     finally:
         ve.close()
+
+
+@pytest.mark.parametrize("env_cls,mode,calls", [
+    ("TDMulti", "2p", ("random_tower_lv1", "random_enemy_lv1")),   # demo.py:72-80 play_2p
+    ("TDMulti", "2p", ("random_tower_lv2", "random_enemy_lv0")),
+    ("TDDefense", "def", ("random_tower_lv0",)),
+    ("TDAttack", "atk", ("random_enemy_lv1",)),
+])
+def test_opponent_methods_called_directly(env_cls, mode, calls):
+    """TDGymBasic's built-in opponents called by the caller between steps (demo.py:78-79),
+    then step(empty_action()): bit-exact with the oracle env making the same calls."""
+    L, seed, opp = 10, 31, 77
+    cls = getattr(E, env_cls)
+    kw = dict(seed=seed, opponent_seed=opp)
+    if mode != "2p":
+        kw["difficulty"] = 1
+    env = cls(L, **kw)
+    orc = O.Env(L, G.MODES[mode], 1, seed, opp, O.Config(), O.Hyper(), road_attempts=10000)
+    try:
+        for k in range(200):
+            for name in calls:
+                getattr(env, name)()
+                getattr(orc, name)()
+            obs, r, d, _ = env.step(env.empty_action())
+            e = orc.empty_def() if mode != "atk" else None
+            a = orc.empty_atk() if mode != "def" else None
+            wo, wr, wd, _ = orc.step(e, a)
+            assert canon.fhex(r) == canon.fhex(wr), (k, r, wr)
+            assert canon.state_digest(env._engine.board_state(0)) == canon.state_digest(canon.oracle_state(orc)), k
+            assert np.array_equal(obs, wo), (k, np.argwhere(obs != wo)[:5].tolist())
+            assert d == wd, k
+            if d:
+                break
+    finally:
+        env.close()
