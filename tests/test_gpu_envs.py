@@ -552,3 +552,40 @@ def test_opponent_methods_called_directly(env_cls, mode, calls):
                 break
     finally:
         env.close()
+
+
+def test_board_view_and_errors():
+    """env._board mirrors TDBoard's attributes (TDBoard.py:25-79) after play, and the
+    surface raises where the reference raises (invalid action: AssertionError,
+    TDDefense.py:36) or where an option is not provided."""
+    L, seed, opp = 10, 31, 77
+    env = E.TDDefense(L, seed=seed, opponent_seed=opp)
+    orc = O.Env(L, O.MODE_DEF, 1, seed, opp, O.Config(), O.Hyper(), road_attempts=10000)
+    try:
+        rng = np.random.RandomState(2)
+        for k in range(120):
+            a = policies.discrete_def(rng, L, orc._board.map[0], 0.6)
+            env.step(a)
+            orc.step(a)
+        v, w = env._board, orc._board
+        assert np.array_equal(v.map, w.map)
+        assert v.start == [list(s) for s in w.start] and v.end == list(w.end)
+        assert (v.cost_def, v.cost_atk, v.base_LP, v.steps) == (w.cost_def, w.cost_atk, w.base_LP, w.steps)
+        assert v.progress == w.progress
+        assert [(e.type, e.lv, e.loc, e.LP, e.margin, e.slowdown, e.dist) for e in v.enemies] == \
+            [(e.type, e.lv, list(e.loc), e.LP, e.margin, e.slowdown, e.dist) for e in w.enemies]
+        assert [(t.type, t.lv, t.loc, t.cd, t.intv, t.cost, t.atk, t.rge) for t in v.towers] == \
+            [(t.type, t.lv, list(t.loc), t.cd, t.intv, t.cost, t.atk, t.rge) for t in w.towers]
+        assert len(w.towers) > 0
+        assert np.array_equal(v.get_states(), w.get_states())
+        with pytest.raises(AssertionError):
+            env.step(6 * L * L + 1)
+        with pytest.raises(Exception):
+            env._engine.opponent("tower", 3)
+    finally:
+        env.close()
+    with pytest.raises(NotImplementedError):
+        E.TDDefense(L, seed=seed, random_agent=False)
+    from gym_TD.vector import VectorEnv
+    with pytest.raises(NotImplementedError):
+        VectorEnv("TD-def-small-v0", 4, seed=0, fixed_seed=True)
