@@ -816,6 +816,17 @@ __device__ __forceinline__ void obs_store(f32x4* p, f32x4 v) { *p = v; }
 #else
 __device__ __forceinline__ void obs_store(f32x4* p, f32x4 v) { __builtin_nontemporal_store(v, p); }
 #endif
+// The two lines a board shares with its neighbours (written half by this wave, half
+// by a wave on another XCD) are stored write-through (sc1) instead: two non-temporal
+// partial writes of one line cost ~7 % of the whole stream (scripts/storepol.hip:
+// 234 us with nt partial lines, 218 us with sc1 ones = the whole-lines-only bound).
+__device__ __forceinline__ void obs_store_shared(__amdgpu_buffer_rsrc_t r, int off, f32x4 v) {
+#ifdef TD_OBS_SHARED_NT  // A/B diagnostic builds only
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, 2);
+#else
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, 16);  // aux 16 = sc1
+#endif
+}
 
 // The (45, L, L) float32 observation of one board.  The wave writes the batch's
 // observation stream in 128-B-aligned 1-KB windows: store k covers the 16-B units
@@ -834,6 +845,9 @@ __device__ __forceinline__ void write_obs(const Smem<NC>& S, const Ctx& x, float
     const int Q = ncr / 4, n4 = NCH * Q;
     f32x4* o4 = reinterpret_cast<f32x4*>(out);
     const int mis = (int)((reinterpret_cast<uintptr_t>(o4) >> 4) & 7u);  // units of the line before the board
+    // units [0, head) and [tail, n4) lie in lines shared with the neighbouring boards
+    const int head = mis ? 8 - mis : 0, tail = ((n4 + mis) & ~7) - mis;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(o4, 0, n4 * 16, 0x00020000);
     const uint4* cell4 = reinterpret_cast<const uint4*>(S.cell);
     for (int i = x.lane - mis; i < n4; i += 64) {
       if (i < 0) continue;
@@ -862,7 +876,8 @@ __device__ __forceinline__ void write_obs(const Smem<NC>& S, const Ctx& x, float
       } else {
         v = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
       }
-      obs_store(o4 + i, v);
+      if (i < head || i >= tail) obs_store_shared(rs, i * 16, v);
+      else obs_store(o4 + i, v);
     }
   } else {
     const int nf = NCH * ncr;
