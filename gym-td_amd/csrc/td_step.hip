@@ -22,6 +22,7 @@
 #include "td_layout.h"
 #include "td_rng.h"
 
+#include <type_traits>
 #include <utility>
 
 namespace td {
@@ -91,6 +92,27 @@ __device__ __forceinline__ void release_board(uint32_t* claim, int lane) {
 // ---------------------------------------------------------------------------
 // per-board LDS image
 // ---------------------------------------------------------------------------
+// Per-board state and output stores.  TD_SST selects the cache policy (A/B builds):
+// 0 plain, 1 non-temporal, 2 write-through (sc1).  Plain is the product: these arrays
+// hold a few bytes per board, so a line is shared by boards on several XCDs and the
+// XCD L2s merge the plain stores; 65,536 boards at L = 10 measured 224 us plain,
+// 227 us sc1 and 287 us non-temporal (partial-line writes to HBM).
+#ifndef TD_SST
+#define TD_SST 0
+#endif
+template <class T>
+__device__ __forceinline__ void sst(T* p, T v) {
+  if constexpr (TD_SST == 1) {
+    __builtin_nontemporal_store(v, p);
+  } else if constexpr (TD_SST == 2) {
+    using W = std::conditional_t<sizeof(T) == 8, uint64_t,
+              std::conditional_t<sizeof(T) == 4, uint32_t, std::conditional_t<sizeof(T) == 2, uint16_t, uint8_t>>>;
+    __hip_atomic_store(reinterpret_cast<W*>(p), __builtin_bit_cast(W, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    *p = v;
+  }
+}
+
 template <int NC>
 struct alignas(16) Smem {
   uint32_t cell[NC];      // cell words (td_layout.h)
@@ -662,9 +684,9 @@ __device__ double board_step(Smem<NC>& S, U& u, const Ctx& x, const StepArgs& a,
   // the enemy list is final for this step: write it back now (its LDS is reused by the stats)
   const size_t eb = (size_t)b * ECAP;
   for (int i = lane; i < n2; i += 64) {
-    a.en_lp[eb + i] = S.eLP[i];
-    a.en_mg[eb + i] = S.eMg[i];
-    a.en_inf[eb + i] = S.eInf[i];
+    sst(&a.en_lp[eb + i], S.eLP[i]);
+    sst(&a.en_mg[eb + i], S.eMg[i]);
+    sst(&a.en_inf[eb + i], S.eInf[i]);
   }
   return reward;
 }
@@ -996,7 +1018,7 @@ template <int NC>
 __device__ __forceinline__ void store_cells(const Smem<NC>& S, const U& u, const Ctx& x, const StepArgs& a, int b) {
   const size_t cb = (size_t)b * x.NCr;
   if (u.cells_dirty)
-    for (int i = x.lane; i < x.NCr; i += 64) a.cells[cb + i] = S.cell[i];
+    for (int i = x.lane; i < x.NCr; i += 64) sst(&a.cells[cb + i], S.cell[i]);
 }
 
 template <int NC>
@@ -1013,7 +1035,7 @@ __device__ void store_board(const Smem<NC>& S, const U& u, const Ctx& x, const S
   }
   const size_t tb = (size_t)b * TCAP;
   // cells were written back by store_cells, enemies at the end of board_step
-  if (x.lane < u.nt) { a.tw_cd[tb + x.lane] = S.tCd[x.lane]; a.tw_inf[tb + x.lane] = S.tInf[x.lane]; }
+  if (x.lane < u.nt) { sst(&a.tw_cd[tb + x.lane], S.tCd[x.lane]); sst(&a.tw_inf[tb + x.lane], S.tInf[x.lane]); }
 }
 
 // ---------------------------------------------------------------------------
@@ -1303,17 +1325,17 @@ __device__ void step_board(Smem<NC>& S, const Ctx& x, const StepArgs& a, int b, 
   if (x.lane == 0) {
     if (was_reset)  // the record has been read into LDS: its slot may be redrawn
       st_relaxed(a.lay_head + b, lay_head + 1u);
-    hot[0] = R.pos;
-    hot[1] = R.tw;
-    hot[2] = R.cn;
-    a.reward[b] = reward;
-    a.done[b] = done ? 1 : 0;
-    if (a.win) a.win[b] = win;
-    if (a.allow_next) a.allow_next[b] = allow;
-    if (a.fail_def) a.fail_def[b] = fail_def;
-    if (a.real_def && !a.multi) a.real_def[b] = real_def;
-    if (a.ep_return) a.ep_return[b] = ep_ret;
-    if (a.ep_len) a.ep_len[b] = ep_steps;
+    sst(&hot[0], R.pos);
+    sst(&hot[1], R.tw);
+    sst(&hot[2], R.cn);
+    sst(&a.reward[b], reward);
+    sst(&a.done[b], (uint8_t)(done ? 1 : 0));
+    if (a.win) sst(&a.win[b], win);
+    if (a.allow_next) sst(&a.allow_next[b], allow);
+    if (a.fail_def) sst(&a.fail_def[b], (int32_t)fail_def);
+    if (a.real_def && !a.multi) sst(&a.real_def[b], real_def);
+    if (a.ep_return) sst(&a.ep_return[b], ep_ret);
+    if (a.ep_len) sst(&a.ep_len[b], (int32_t)ep_steps);
     if (done && a.last_ep) {  // the board's last finished episode (td_episode_records)
       td_episode_record r;
       r.ret = ep_ret;
@@ -1326,7 +1348,7 @@ __device__ void step_board(Smem<NC>& S, const Ctx& x, const StepArgs& a, int b, 
       atomicAdd(&a.ep_stats[1], ep_ret);
     }
   }
-  if (MODE != MODE_2P && x.lane < 8) hot[4 + x.lane] = R.cache;
+  if (MODE != MODE_2P && x.lane < 8) sst(&hot[4 + x.lane], R.cache);
   STAMP(8);
 }
 
@@ -1377,9 +1399,9 @@ __global__ __launch_bounds__(64) void td_opponent_kernel(StepArgs a, int side, i
   R.prefetch(x.lane);  // the next step expects the hot record primed
   const size_t eb = (size_t)b * ECAP;
   for (int i = x.lane; i < u.n; i += 64) {
-    a.en_lp[eb + i] = S.eLP[i];
-    a.en_mg[eb + i] = S.eMg[i];
-    a.en_inf[eb + i] = S.eInf[i];
+    sst(&a.en_lp[eb + i], S.eLP[i]);
+    sst(&a.en_mg[eb + i], S.eMg[i]);
+    sst(&a.en_inf[eb + i], S.eInf[i]);
   }
   store_cells(S, u, x, a, b);
   store_board(S, u, x, a, b);
