@@ -1,5 +1,6 @@
 """Diagnostic: per-phase wave cycles of the step kernel (TD_STAMPS build) and
-timings, at a chosen batch.  Usage: TDSTEP_LIB=.../libtdstep_stamps.so python probe_phases.py B L burnin"""
+timings, at a chosen batch.
+Usage: TDSTEP_LIB=.../libtdstep_stamps.so python probe_phases.py B L burnin [mode multi]"""
 import os, sys, time
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "gym-td_amd"))
 import numpy as np, torch
@@ -9,13 +10,28 @@ from gym_TD.engine import TDEngine
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
 L = int(sys.argv[2]) if len(sys.argv) > 2 else 10
 burn = int(sys.argv[3]) if len(sys.argv) > 3 else 600
+mode = sys.argv[4] if len(sys.argv) > 4 else "def"
+multi = len(sys.argv) > 5 and sys.argv[5] == "1"
 seeds = np.arange(B) + 11
-eng = TDEngine(L, B, "def", False, 1, np_seeds=seeds, py_seeds=seeds, autoreset=True)
+eng = TDEngine(L, B, mode, multi, 1, np_seeds=seeds, py_seeds=seeds, autoreset=True, info=not multi)
 eng.reset_all()
 g = torch.Generator(device="cuda").manual_seed(0)
-acts = torch.randint(0, 6 * L * L + 1, (burn + 20, B), device="cuda", generator=g)
+if multi:  # a few pre-drawn flag batches, cycled (bench.py's 2p-middle-multi shape)
+    pool = [(torch.randint(0, 3, (B, 6, L, L), device="cuda", generator=g),
+             torch.randint(0, 5, (B, 3, 8), device="cuda", generator=g)) for _ in range(4)]
+    act = lambda k: pool[k % 4]
+else:
+    acts = torch.randint(0, 6 * L * L + 1, (burn + 20, B), device="cuda", generator=g)
+    act = lambda k: (acts[k], None)
+
+
+def step(k):
+    d, a = act(k)
+    eng.step(def_act=d, atk_act=a if mode != "def" else None)
+
+
 for k in range(burn):
-    eng.step(def_act=acts[k])
+    step(k)
 torch.cuda.synchronize()
 stamps = torch.zeros((B, 16), dtype=torch.int64, device="cuda")
 fn = getattr(_lib.lib, "td_debug_stamps", None)
@@ -27,7 +43,7 @@ names = ["load", "actions", "sort", "towers", "march+costs", "stats+scalars", "o
 acc = np.zeros(len(names))
 t0 = time.time()
 for k in range(burn, burn + 20):
-    eng.step(def_act=acts[k])
+    step(k)
     torch.cuda.synchronize()
     if fn is not None:
         s = stamps.cpu().numpy().astype(np.float64)
