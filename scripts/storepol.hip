@@ -89,6 +89,40 @@ __global__ __launch_bounds__(256) void fixup(f32x4* out, const f32x4* scr, int B
   __builtin_nontemporal_store(scr[i], out + (lo & ~7l) + k);
 }
 
+// The 2p-middle-multi memory skeleton: per board read 19,200 B of int64 flags
+// (non-temporal 16-B loads, K per lane in flight), then write the 72,000-B (45, 20, 20)
+// observation in 128-B-aligned 1-KB windows (shared lines sc1).  LDS bytes per
+// workgroup as the step kernel (occupancy), or none.
+constexpr int OBS2 = 4500, ACT2 = 1200;  // 16-B units per board
+template <int K, int LDS>
+__global__ __launch_bounds__(64) void skel2p(f32x4* out, const f32x4* act, int B, int rd) {
+  __shared__ float pad[LDS / 4 + 1];
+  const int b = blockIdx.x, lane = threadIdx.x;
+  if (b >= B) return;
+  float acc = 0.f;
+  if (rd) {
+    const f32x4* a = act + (size_t)b * ACT2;
+    for (int base = 0; base < ACT2; base += 64 * K) {
+      f32x4 v[K];
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const int e = base + 64 * k + lane;
+        v[k] = e < ACT2 ? __builtin_nontemporal_load(a + e) : f32x4{0, 0, 0, 0};
+      }
+#pragma unroll
+      for (int k = 0; k < K; ++k) acc += v[k].x + v[k].w;
+    }
+  }
+  if (LDS) { pad[lane] = acc; __syncthreads(); acc = pad[(lane + 1) & 63]; }
+  const long lo = (long)b * OBS2, hi = lo + OBS2, a0 = lo & ~7l;
+  const long f0 = (lo + 7) & ~7l, f1 = hi & ~7l;
+  for (long g = a0 + lane; g < hi; g += 64) {
+    const f32x4 v = f32x4{acc, 1.f, 2.f, (float)g};
+    if (g >= f0 && g < f1) st<1>(out + g, v);
+    else if (g >= lo) st<6>(out + g, v);
+  }
+}
+
 int main(int argc, char** argv) {
   const int B = argc > 1 ? atoi(argv[1]) : 65536;
   const size_t bytes = (size_t)B * BOARD_F4 * 16;
@@ -150,5 +184,37 @@ int main(int argc, char** argv) {
     run("pad_sc0_nt", [&] { hipLaunchKernelGGL(padded<3>, g, t, 0, 0, out, B); });
   }
   CK(hipFree(out));
+  {
+    const int B2 = 16384;
+    f32x4 *o2, *a2;
+    CK(hipMalloc(&o2, (size_t)B2 * OBS2 * 16));
+    CK(hipMalloc(&a2, (size_t)B2 * ACT2 * 16 * 4));  // 4 action batches, cycled (> MALL)
+    CK(hipMemset(a2, 0, (size_t)B2 * ACT2 * 16 * 4));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    auto run2 = [&](const char* name, auto launch) {
+      for (int i = 0; i < 4; ++i) launch(i);
+      CK(hipDeviceSynchronize());
+      CK(hipEventRecord(e0));
+      const int reps = 20;
+      for (int i = 0; i < reps; ++i) launch(i);
+      CK(hipEventRecord(e1));
+      CK(hipEventSynchronize(e1));
+      float ms = 0;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      const double us = ms * 1000.0 / reps;
+      printf("%-14s %8.1f us  %6.2f TB/s (read+write)\n", name, us,
+             (double)B2 * (OBS2 + ACT2) * 16 / (us * 1e-6) / 1e12);
+    };
+    const dim3 g2(B2), t2(64);
+    for (int rep = 0; rep < 2; ++rep) {
+      run2("2p_write_only", [&](int i) { hipLaunchKernelGGL((skel2p<8, 7760>), g2, t2, 0, 0, o2, a2 + (size_t)(i & 3) * B2 * ACT2, B2, 0); });
+      run2("2p_k8_lds", [&](int i) { hipLaunchKernelGGL((skel2p<8, 7760>), g2, t2, 0, 0, o2, a2 + (size_t)(i & 3) * B2 * ACT2, B2, 1); });
+      run2("2p_k19_lds", [&](int i) { hipLaunchKernelGGL((skel2p<19, 7760>), g2, t2, 0, 0, o2, a2 + (size_t)(i & 3) * B2 * ACT2, B2, 1); });
+      run2("2p_k8_nolds", [&](int i) { hipLaunchKernelGGL((skel2p<8, 0>), g2, t2, 0, 0, o2, a2 + (size_t)(i & 3) * B2 * ACT2, B2, 1); });
+      run2("2p_k19_nolds", [&](int i) { hipLaunchKernelGGL((skel2p<19, 0>), g2, t2, 0, 0, o2, a2 + (size_t)(i & 3) * B2 * ACT2, B2, 1); });
+    }
+  }
   return 0;
 }
