@@ -10,7 +10,7 @@ for r in $(seq 1 $R); do
     python - "$n" "$r" <<'PY'
 import json, sys
 d = json.loads(open("gpurun_out/ab/%s.%s.json" % (sys.argv[1], sys.argv[2])).read().strip().splitlines()[-1])
-print("%-10s r%s %8.1fM env-steps/s  kernel %6.1f us" % (sys.argv[1], sys.argv[2], d["value"] / 1e6, d["roofline"]["avg_kernel_us"]), flush=True)
+print("%-10s r%s %8.1fM env-steps/s  step %6.1f us  kernel %6.1f us" % (sys.argv[1], sys.argv[2], d["value"] / 1e6, d["ms_per_step"] * 1e3, d["roofline"]["avg_kernel_us"]), flush=True)
 PY
   done
 done
