@@ -191,15 +191,17 @@ def test_vecenv_autoreset_vs_oracle():
         ve.close()
 
 
-@pytest.mark.parametrize("mode,multi", [("def", False), ("2p", True)])
-def test_vecenv_sharding_invariance(mode, multi):
+@pytest.mark.parametrize("mode,multi,shards", [("def", False, 2), ("2p", True, 2), ("def", False, 8)])
+def test_vecenv_sharding_invariance(mode, multi, shards):
     """Board i of the global batch follows the same trajectory whether it is
-    stepped in one TDVecEnv of 64 boards or in the second of two shards of 32
-    (trajectories do not depend on the GPU count)."""
+    stepped in one TDVecEnv of 64 boards or in its shard of 64 / shards boards, as
+    rank r of a `shards`-GPU run owns it (trajectories at 1 and 8
+    GPUs are bit-identical)."""
     L, B, steps = 10, 64, 200
+    n = B // shards
     with reference_settings({"base_LP": 2}, multi):
         whole = E.TDVecEnv(L, B, mode, seed=777)
-        parts = [E.TDVecEnv(L, B // 2, mode, seed=777, global_offset=r * (B // 2)) for r in range(2)]
+        parts = [E.TDVecEnv(L, n, mode, seed=777, global_offset=r * n) for r in range(shards)]
     try:
         ow = whole.reset()
         op = torch.cat([p.reset() for p in parts])
@@ -214,7 +216,7 @@ def test_vecenv_sharding_invariance(mode, multi):
             a = torch.randint(0, 5, (B, 3, 8), device="cuda", generator=g, dtype=torch.int64)
             act = (lambda lo, hi: d[lo:hi]) if mode == "def" else (lambda lo, hi: (d[lo:hi], a[lo:hi]))
             ow, rw, dw, iw = whole.step(act(0, B))
-            res = [p.step(act(r * (B // 2), (r + 1) * (B // 2))) for r, p in enumerate(parts)]
+            res = [p.step(act(r * n, (r + 1) * n)) for r, p in enumerate(parts)]
             assert torch.equal(ow, torch.cat([r[0] for r in res])), k
             assert torch.equal(rw, torch.cat([r[1] for r in res])), k
             assert torch.equal(dw, torch.cat([r[2] for r in res])), k
