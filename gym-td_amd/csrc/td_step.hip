@@ -115,6 +115,7 @@ __device__ __forceinline__ void sst(T* p, T v) {
 
 template <int NC>
 struct alignas(16) Smem {
+  static_assert(NC % 4 == 0, "cell and tower maps are moved in 16-B / 4-B units");
   uint32_t cell[NC];      // cell words (td_layout.h)
   uint8_t twr[NC];        // tower at cell: 0 none, else 0x80 | lv << 2 | type
   uint8_t grp[4][NC];     // enemy group (head enemy index) per (type, cell), 0xFF none
@@ -919,7 +920,8 @@ __device__ __forceinline__ void write_obs(const Smem<NC>& S, const Ctx& x, float
 // opponent stream's hot record.
 struct Prefetch {
   double lp, mg, tcd;
-  uint32_t inf, tinf, c0, c1, w;
+  uint4 c4;  // cells 4 lane .. 4 lane + 3 (board of L*L % 4 == 0), else cells lane and lane + 64 in .x / .y
+  uint32_t inf, tinf, w;
 };
 #ifndef TD_PF_TW
 #define TD_PF_TW 16
@@ -940,8 +942,12 @@ __device__ __forceinline__ void prefetch_issue(Prefetch& P, const StepArgs& a, i
     P.tcd = a.tw_cd[tb + lane];
     P.tinf = a.tw_inf[tb + lane];
   }
-  P.c0 = lane < ncr ? a.cells[cb + lane] : 0u;
-  P.c1 = lane + 64 < ncr ? a.cells[cb + lane + 64] : 0u;
+  if ((ncr & 3) == 0) {
+    P.c4 = lane < (ncr >> 2) ? reinterpret_cast<const uint4*>(a.cells + cb)[lane] : uint4{0u, 0u, 0u, 0u};
+  } else {
+    P.c4.x = lane < ncr ? a.cells[cb + lane] : 0u;
+    P.c4.y = lane + 64 < ncr ? a.cells[cb + lane + 64] : 0u;
+  }
   const uint32_t* src;
   if (lane < PF_ACT) src = reinterpret_cast<const uint32_t*>(a.hdr + b) + lane;
   else if (lane < PF_HOT) src = want_act ? reinterpret_cast<const uint32_t*>(a.def_act + b) + (lane - PF_ACT) : nullptr;
@@ -960,10 +966,33 @@ __device__ __forceinline__ double lane_f64(uint32_t v, int l) {
 template <int NC>
 __device__ void load_board(Smem<NC>& S, U& u, const Ctx& x, const StepArgs& a, int b, const Prefetch& P) {
   const size_t eb = (size_t)b * ECAP, cb = (size_t)b * x.NCr;
-  if (x.lane < x.NCr) S.cell[x.lane] = P.c0;
-  if (x.lane + 64 < x.NCr) S.cell[x.lane + 64] = P.c1;
-  for (int i = 128 + x.lane; i < x.NCr; i += 64) S.cell[i] = a.cells[cb + i];
-  for (int i = x.lane; i < x.NCr; i += 64) S.twr[i] = 0;
+  if ((x.NCr & 3) == 0) {
+    // 16-B cell loads: the first 256 cells came with the prefetch, the rest (L > 16)
+    // are all issued before any is stored to LDS
+    const int n4 = x.NCr >> 2;
+    const uint4* g4 = reinterpret_cast<const uint4*>(a.cells + cb);
+    uint4* s4 = reinterpret_cast<uint4*>(S.cell);
+    constexpr int NR = (NC / 4 + 63) / 64 - 1;  // further 16-B loads per lane: 0 (L <= 16) .. 3 (NC = 1024)
+    uint4 r[NR > 0 ? NR : 1];
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+      const int i = 64 * (k + 1) + x.lane;
+      if (i < n4) r[k] = g4[i];
+    }
+    if (x.lane < n4) s4[x.lane] = P.c4;
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+      const int i = 64 * (k + 1) + x.lane;
+      if (i < n4) s4[i] = r[k];
+    }
+    uint32_t* t4 = reinterpret_cast<uint32_t*>(S.twr);  // NC % 4 == 0
+    for (int i = x.lane; i < n4; i += 64) t4[i] = 0u;
+  } else {
+    if (x.lane < x.NCr) S.cell[x.lane] = P.c4.x;
+    if (x.lane + 64 < x.NCr) S.cell[x.lane + 64] = P.c4.y;
+    for (int i = 128 + x.lane; i < x.NCr; i += 64) S.cell[i] = a.cells[cb + i];
+    for (int i = x.lane; i < x.NCr; i += 64) S.twr[i] = 0;
+  }
   // TdHdr words (td_common.h): 0-5 cost_def, cost_atk, ep_return; 6 steps, 7 base_LP,
   // 8 atk_cd, 9 def_cd, 10 n_en, 11 n_tw, 12 num_roads, 13 end_cell, 14-16 start_cell,
   // 17 maxdist, 18 flags, 19 episodes
