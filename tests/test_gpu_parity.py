@@ -198,9 +198,12 @@ def test_autoreset_matches_explicit_reset():
         eb.close()
 
 
-@pytest.mark.parametrize("L,B,mode,multi", [(10, 65536, "def", False), (20, 16384, "2p", True)])
+@pytest.mark.parametrize("L,B,mode,multi", [(10, 4096, "def", False), (10, 65536, "def", False),
+                                            (20, 16384, "2p", True), (30, 16384, "def", False)])
 def test_full_size_properties(L, B, mode, multi):
-    """BASELINE-sized batches: invariants over every board, bit-exact spot checks vs the oracle."""
+    """BASELINE.json configs[1]-[4] sizes per GPU (4,096 and 65,536 x 10x10 TD-def,
+    16,384 x 20x20 TD-2p multi-action, 16,384 x 30x30 TD-def = one GPU's share of
+    configs[4]): invariants over every board, bit-exact spot checks vs the oracle."""
     seeds = np.arange(B, dtype=np.int64) + 7000
     eng = TDEngine(L, B, mode, multi, 1, np_seeds=seeds, py_seeds=seeds, autoreset=True)
     try:
