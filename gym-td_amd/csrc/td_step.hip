@@ -71,7 +71,11 @@ __device__ __forceinline__ void st_relaxed(uint32_t* p, uint32_t v) {
 // A board's layout stream (np_mt) and its ring tail are written only by the refill
 // wave holding the board's claim word (several refills may be in flight on side
 // streams).  Take it with an agent-scope CAS + acquire; give it back after the
-// wave's stores have drained, behind an agent-scope release.
+// wave's stores have drained.  Everything the claim protects is stored write-through
+// (sc1, st_relaxed), so no release fence is needed (MI355X_MICROARCH.md, publish
+// recipe R1): a release fence writes back the XCD's whole L2, full of the step
+// kernel's dirty observation lines, and ~490 of them per refill launch cost the
+// 20x20 multi-action step 3.6 % (335.5 -> 323.7 us per step without them).
 __device__ __forceinline__ bool claim_board(uint32_t* claim, int lane) {
   uint32_t got = 0;
   if (lane == 0) got = atomicCAS(claim, 0u, 1u) == 0u ? 1u : 0u;
@@ -82,11 +86,7 @@ __device__ __forceinline__ bool claim_board(uint32_t* claim, int lane) {
 __device__ __forceinline__ void release_board(uint32_t* claim, int lane) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (lane == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    st_relaxed(claim, 0u);
-  }
+  if (lane == 0) st_relaxed(claim, 0u);
 }
 
 // ---------------------------------------------------------------------------
@@ -1517,20 +1517,19 @@ __device__ int wave_layout(LayoutSmem<NC>& G, const StepArgs& a, int b, int retr
   }
   st = __shfl(st, 0);
   __syncthreads();
-  for (int i = lane; i < OPP_WORDS; i += 64) gmt[i] = G.mt[i];
-  if (lane < 16) reinterpret_cast<uint32_t*>(ghdr)[lane] = reinterpret_cast<const uint32_t*>(&G.res)[lane];
+  // every store below is write-through (st_relaxed = sc1): the claim release and the
+  // tag store publish them without a release fence (see claim_board)
+  for (int i = lane; i < OPP_WORDS; i += 64) st_relaxed(gmt + i, G.mt[i]);
+  if (lane < 16) st_relaxed(reinterpret_cast<uint32_t*>(ghdr) + lane, reinterpret_cast<const uint32_t*>(&G.res)[lane]);
   if (st == ROAD_PENDING) {  // keep the draw for the next call (published by the caller's claim release)
-    for (int i = lane; i < sbytes / 4; i += 64) reinterpret_cast<uint32_t*>(gscr)[i] = reinterpret_cast<const uint32_t*>(G.scratch)[i];
-    for (int i = 1 + lane; i < lw; i += 64) slot[i] = G.rec[i];
+    for (int i = lane; i < sbytes / 4; i += 64)
+      st_relaxed(reinterpret_cast<uint32_t*>(gscr) + i, reinterpret_cast<const uint32_t*>(G.scratch)[i]);
+    for (int i = 1 + lane; i < lw; i += 64) st_relaxed(slot + i, G.rec[i]);
   } else if (st == ROAD_OK) {
-    for (int i = 1 + lane; i < lw; i += 64) slot[i] = G.rec[i];
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    for (int i = 1 + lane; i < lw; i += 64) st_relaxed(slot + i, G.rec[i]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every lane's record stores have landed
     __syncthreads();
-    if (lane == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      st_relaxed(slot, slot_tag(n));
-    }
+    if (lane == 0) st_relaxed(slot, slot_tag(n));
   }
   return st;
 }
