@@ -89,9 +89,6 @@ __device__ __forceinline__ void release_board(uint32_t* claim, int lane) {
   if (lane == 0) st_relaxed(claim, 0u);
 }
 
-// ---------------------------------------------------------------------------
-// per-board LDS image
-// ---------------------------------------------------------------------------
 // Per-board state and output stores.  TD_SST selects the cache policy (A/B builds):
 // 0 plain, 1 non-temporal, 2 write-through (sc1).  Plain is the product: these arrays
 // hold a few bytes per board, so a line is shared by boards on several XCDs and the
@@ -113,6 +110,9 @@ __device__ __forceinline__ void sst(T* p, T v) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// per-board LDS image
+// ---------------------------------------------------------------------------
 template <int NC>
 struct alignas(16) Smem {
   static_assert(NC % 4 == 0, "cell and tower maps are moved in 16-B / 4-B units");
