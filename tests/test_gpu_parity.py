@@ -240,3 +240,42 @@ def test_full_size_properties(L, B, mode, multi):
         assert (fl[~good] == 8).all()  # TD_FLAG_NO_LAYOUT
     finally:
         eng.close()
+
+
+def test_reference_kat_on_device():
+    """The reference's own known-answer test (TDBoard.py:674-751) through the C-ABI:
+    the seed-1024 two-road 10x10 layout (roads drawn by the restatement of
+    create_road_v2, handed over with td_layout_from_roads) resets four TD-atk boards
+    to the KAT's full initial observation, byte for byte; then every one-enemy
+    cluster (types 0-3 on roads 0 and 1) fails at zero attacker cost
+    (TDBoard.py:749-751): FailCode COST_SHORTAGE and no enemy on the board."""
+    from gym_TD import fail_code
+    from gym_TD import _lib
+    z = np.load(G.GOLDEN + "/kat_seed1024.npz")
+    L, B = 10, 4
+    rng = np.random.RandomState()
+    rng.seed(1024)
+    roads = O.create_road(rng, L, 2)
+    cells = np.asarray([p[0] * L + p[1] for r in roads for p in r], dtype=np.int32)
+    off = np.cumsum([0] + [len(r) for r in roads]).astype(np.int32)
+    rec = np.zeros(8 + L * L, np.uint32)
+    assert _lib.lib.td_layout_from_roads(L, 2, _lib.ptr(cells, _lib.ctypes.c_int32),
+                                         _lib.ptr(off, _lib.ctypes.c_int32), _lib.ptr(rec, _lib.ctypes.c_uint32)) == 0
+    seeds = np.arange(B) + 1024
+    eng = TDEngine(L, B, "atk", False, 1, np_seeds=seeds, py_seeds=seeds, autoreset=False)
+    try:
+        obs = eng.reset_layouts(np.stack([rec] * B), np.arange(B))
+        for b in range(B):
+            assert np.array_equal(obs[b].cpu().numpy(), z["obs"]), b
+            m, start, end = eng.map_planes(b)
+            assert np.array_equal(m, z["map"]) and start == z["start"].tolist() and end == z["end"].tolist()
+        act = np.full((B, 3, 8), 4, dtype=np.int64)  # 4 = no enemy in that slot
+        act[:, 0, 0] = np.arange(B)                    # board t: one enemy of type t on road 0 ...
+        act[:, 1, 0] = np.arange(B)                    # ... and on road 1
+        eng.step(atk_act=torch.from_numpy(act).cuda())
+        fa = eng.fail_atk.cpu().numpy()
+        assert (fa[:, :2] == fail_code.COST_SHORTAGE).all(), fa
+        for b in range(B):
+            assert eng.board_state(b)["enemies"] == []
+    finally:
+        eng.close()
