@@ -1,4 +1,4 @@
-"""The N > 1 path on CPU (gloo, world size 2): board sharding and the episode-stats
+"""The N > 1 path on CPU (gloo, world sizes 2 and 4): board sharding and the episode-stats
 gather that bench.py runs over RCCL on GPUs.
 
 Each rank steps its own contiguous block of boards (here with the oracle, the
@@ -18,7 +18,7 @@ import torch.multiprocessing as tmp
 from gym_TD import shard
 from oracle import td_oracle as O
 
-L, BOARDS_PER_RANK, STEPS = 10, 3, 80  # seeds 2000..2005: every first layout draw succeeds
+L, BOARDS_PER_RANK, STEPS = 10, 3, 80  # seeds 2000..2005 and 2008..2019: every layout draw of these runs succeeds
 
 
 def _run_boards(seeds):
@@ -61,11 +61,11 @@ def _stats(trace):
     return tot
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, base):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        seeds = shard.shard_seeds(2000, rank, BOARDS_PER_RANK)
+        seeds = shard.shard_seeds(base, rank, BOARDS_PER_RANK)
         trace = _run_boards(seeds)
         stats = _stats(trace)
         t = shard.max_over_ranks(torch.tensor([float(rank + 1)], dtype=torch.float64))
@@ -90,12 +90,12 @@ def test_shard_partition():
         assert shard.shard_range(world - 1, 16) == (16 * (world - 1), 16 * world)
 
 
-def test_gloo_two_ranks_match_one_process():
-    world = 2
+@pytest.mark.parametrize("world,base", [(2, 2000), (4, 2008)])
+def test_gloo_ranks_match_one_process(world, base):
     ctx = tmp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, base)) for r in range(world)]
     for p in procs:
         p.start()
     try:
@@ -105,7 +105,7 @@ def test_gloo_two_ranks_match_one_process():
             p.join(timeout=60)
     assert all(p.exitcode == 0 for p in procs)
     assert tmax == float(world)
-    trace = _run_boards(shard.shard_seeds(2000, 0, world * BOARDS_PER_RANK))
+    trace = _run_boards(shard.shard_seeds(base, 0, world * BOARDS_PER_RANK))
     one = _stats(trace)
     want = [r.numpy().tolist() for r in _last_records(trace)]
     assert recs == want  # per-board records, 16 B each, in global board order
