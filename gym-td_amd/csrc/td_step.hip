@@ -371,7 +371,7 @@ __device__ void defender_scan(Smem<NC>& S, U& u, const Ctx& x, const int64_t* A,
   for (int i = x.lane; i < (2 * NC) / 4; i += 64) fw[i] = 0u;  // grp[0] and grp[1]
   __syncthreads();
   bool bad = false;
-  if ((ncr & 1) == 0) {  // 16-B units of two cells of one plane
+  if ((ncr & 1) == 0 && (reinterpret_cast<uintptr_t>(A) & 15u) == 0) {  // 16-B units of two cells of one plane
     typedef long long i64x2 __attribute__((ext_vector_type(2)));
     const i64x2* A2 = reinterpret_cast<const i64x2*>(A);
     const int n2 = n / 2;
@@ -446,7 +446,7 @@ __device__ void defender_scan(Smem<NC>& S, U& u, const Ctx& x, const int64_t* A,
   }
   __syncthreads();
   if (R) {
-    if ((ncr & 1) == 0) {
+    if ((ncr & 1) == 0 && (reinterpret_cast<uintptr_t>(R) & 15u) == 0) {
       typedef long long i64x2 __attribute__((ext_vector_type(2)));
       i64x2* R2 = reinterpret_cast<i64x2*>(R);
       const int n2 = n / 2, mis = (int)((reinterpret_cast<uintptr_t>(R2) >> 4) & 7u);
@@ -864,7 +864,7 @@ __device__ __forceinline__ void obs_store_shared(__amdgpu_buffer_rsrc_t r, int o
 template <int NC, int LT>
 __device__ __forceinline__ void write_obs(const Smem<NC>& S, const Ctx& x, float* out, bool any_enemy) {
   const int ncr = LT ? LT * LT : x.NCr;
-  if ((ncr & 3) == 0) {
+  if ((ncr & 3) == 0 && (reinterpret_cast<uintptr_t>(out) & 15u) == 0) {  // else: caller buffer not 16-B aligned
     const int Q = ncr / 4, n4 = NCH * Q;
     f32x4* o4 = reinterpret_cast<f32x4*>(out);
     const int mis = (int)((reinterpret_cast<uintptr_t>(o4) >> 4) & 7u);  // units of the line before the board

@@ -133,7 +133,10 @@ int td_last_reset_failures(td_handle* h, int32_t* boards, int cap);
 /* Reset from explicit layout records (td_layout_words(L) uint32 each, host memory). */
 int td_reset_layouts(td_handle* h, const uint32_t* recs, const int32_t* boards, int n, float* obs, void* stream);
 
-/* One env step for all boards (asynchronous on `stream`). */
+/* One env step for all boards (asynchronous on `stream`).  Buffers need only their
+ * element type's alignment; a 16-B-aligned obs (and, multi-action, 16-B-aligned flag
+ * and real-action arrays) takes the line-aligned 16-B store path, any other the
+ * per-element one (same bytes, slower). */
 int td_step(td_handle* h, const td_step_io* io, void* stream);
 
 /* Episodes finished by td_step since the last clear (SURVEY.md §8(b) td_episode_stats):

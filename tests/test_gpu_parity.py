@@ -279,3 +279,42 @@ def test_reference_kat_on_device():
             assert eng.board_state(b)["enemies"] == []
     finally:
         eng.close()
+
+
+@pytest.mark.parametrize("multi", [False, True])
+def test_unaligned_caller_buffers(multi):
+    """td_step takes caller-owned pointers: an observation buffer that is only 4-B
+    aligned (a float view one element into a larger tensor) and multi-action flags
+    only 8-B aligned give the same bytes as 16-B-aligned buffers (the kernels store
+    16-B units and read 16-B flag pairs)."""
+    L, B = 10, 48
+    seeds = np.arange(B) + 3100
+    a = TDEngine(L, B, "def", multi, 1, np_seeds=seeds, py_seeds=seeds, autoreset=True)
+    b = TDEngine(L, B, "def", multi, 1, np_seeds=seeds, py_seeds=seeds, autoreset=True)
+    try:
+        a.reset_all()
+        b.reset_all()
+        n = B * 45 * L * L
+        big = torch.full((n + 1,), -1.0, device="cuda")
+        b.obs = big[1:].view(B, 45, L, L)
+        assert b.obs.data_ptr() % 16 == 4
+        b._io.obs = b.obs.data_ptr()
+        g = torch.Generator(device="cuda").manual_seed(9)
+        for k in range(120):
+            if multi:
+                d = torch.randint(0, 3, (B, 6, L, L), device="cuda", generator=g, dtype=torch.int64)
+                dbig = torch.empty(d.numel() + 1, dtype=torch.int64, device="cuda")
+                dbig[1:] = d.reshape(-1)
+                du = dbig[1:].view(B, 6, L, L)
+                assert du.data_ptr() % 16 == 8
+            else:
+                d = torch.randint(0, 6 * L * L + 1, (B,), device="cuda", generator=g, dtype=torch.int64)
+                du = d
+            a.step(def_act=d)
+            b.step(def_act=du)
+            assert torch.equal(a.obs, b.obs), k
+            assert torch.equal(a.reward, b.reward) and torch.equal(a.done, b.done), k
+        assert float(big[0]) == -1.0  # nothing written before the buffer
+    finally:
+        a.close()
+        b.close()
