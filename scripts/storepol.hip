@@ -123,6 +123,25 @@ __global__ __launch_bounds__(64) void skel2p(f32x4* out, const f32x4* act, int B
   }
 }
 
+// 30x30 observation stream (162,000 B per board, one wave per board, 1-KB windows,
+// shared lines sc1) at the step kernel's LDS footprint (13 workgroups per CU) or none
+constexpr int OBS3 = 10125;  // 16-B units per board
+template <int LDS>
+__global__ __launch_bounds__(64) void large(f32x4* out, int B) {
+  __shared__ float pad[LDS / 4 + 1];
+  const int b = blockIdx.x, lane = threadIdx.x;
+  if (b >= B) return;
+  float acc = 0.f;
+  if (LDS) { pad[lane] = (float)b; __syncthreads(); acc = pad[(lane + 1) & 63]; }
+  const long lo = (long)b * OBS3, hi = lo + OBS3, a0 = lo & ~7l;
+  const long f0 = (lo + 7) & ~7l, f1 = hi & ~7l;
+  for (long g = a0 + lane; g < hi; g += 64) {
+    const f32x4 v = f32x4{acc, 1.f, 2.f, (float)g};
+    if (g >= f0 && g < f1) st<1>(out + g, v);
+    else if (g >= lo) st<6>(out + g, v);
+  }
+}
+
 int main(int argc, char** argv) {
   const int B = argc > 1 ? atoi(argv[1]) : 65536;
   const size_t bytes = (size_t)B * BOARD_F4 * 16;
@@ -215,6 +234,33 @@ int main(int argc, char** argv) {
       run2("2p_k8_nolds", [&](int i) { hipLaunchKernelGGL((skel2p<8, 0>), g2, t2, 0, 0, o2, a2 + (size_t)(i & 3) * B2 * ACT2, B2, 1); });
       run2("2p_k19_nolds", [&](int i) { hipLaunchKernelGGL((skel2p<19, 0>), g2, t2, 0, 0, o2, a2 + (size_t)(i & 3) * B2 * ACT2, B2, 1); });
     }
+  }
+  {
+    const int B3 = 16384;
+    f32x4* o3;
+    CK(hipMalloc(&o3, (size_t)B3 * OBS3 * 16 + 4096));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    auto run3 = [&](const char* name, auto launch) {
+      for (int i = 0; i < 3; ++i) launch();
+      CK(hipDeviceSynchronize());
+      CK(hipEventRecord(e0));
+      const int reps = 10;
+      for (int i = 0; i < reps; ++i) launch();
+      CK(hipEventRecord(e1));
+      CK(hipEventSynchronize(e1));
+      float ms = 0;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      const double us = ms * 1000.0 / reps;
+      printf("%-14s %8.1f us  %6.2f TB/s\n", name, us, (double)B3 * OBS3 * 16 / (us * 1e-6) / 1e12);
+    };
+    for (int rep = 0; rep < 2; ++rep) {
+      run3("30x30_lds12k", [&] { hipLaunchKernelGGL((large<12272>), dim3(B3), dim3(64), 0, 0, o3, B3); });
+      run3("30x30_lds6k", [&] { hipLaunchKernelGGL((large<6000>), dim3(B3), dim3(64), 0, 0, o3, B3); });
+      run3("30x30_nolds", [&] { hipLaunchKernelGGL((large<0>), dim3(B3), dim3(64), 0, 0, o3, B3); });
+    }
+    CK(hipFree(o3));
   }
   return 0;
 }
