@@ -5,6 +5,8 @@ The batched counterpart of TDGymBasic + TDDefense / TDAttack / TDMulti
 outputs are torch tensors on the engine's device; every step is one kernel
 launch on torch's current stream.
 """
+import types
+
 import numpy as np
 import torch
 
@@ -89,10 +91,18 @@ class TDEngine(object):
             self._def_in = zeros((B, 6, L, L) if self.multi else (B,), torch.int64) if mode != "atk" else None
             self._atk_in = zeros((B, 3, 8), torch.int64) if mode != "def" else None
         self._io = _lib.TdStepIO()
+        # host_io: numpy views of the pinned buffers, made once (a torch -> numpy
+        # conversion or a scalar read through torch costs microseconds per step)
+        self.np = types.SimpleNamespace()
         for name in ("obs", "reward", "done", "real_def", "real_atk", "fail_def", "fail_atk", "win",
                      "allow_next", "ep_return", "ep_len"):
             t = getattr(self, name)
             setattr(self._io, name, t.data_ptr() if t is not None else None)
+            if self.host_io:
+                setattr(self.np, name, t.numpy() if t is not None else None)
+        if self.host_io:
+            self._def_np = self._def_in.numpy() if self._def_in is not None else None
+            self._atk_np = self._atk_in.numpy() if self._atk_in is not None else None
         if np_seeds is not None or py_seeds is not None:
             self.seed(np_seeds, py_seeds)
         P._live.add(self)
@@ -204,10 +214,10 @@ class TDEngine(object):
         keep = []
         if self.host_io:
             if self.mode != "atk":
-                self._def_in.numpy()[...] = np.asarray(def_act, dtype=np.int64).reshape(self._def_in.shape)
+                self._def_np[...] = np.asarray(def_act, dtype=np.int64).reshape(self._def_np.shape)
                 io.def_act = self._def_in.data_ptr()
             if self.mode != "def":
-                self._atk_in.numpy()[...] = np.asarray(atk_act, dtype=np.int64).reshape(self._atk_in.shape)
+                self._atk_np[...] = np.asarray(atk_act, dtype=np.int64).reshape(self._atk_np.shape)
                 io.atk_act = self._atk_in.data_ptr()
             _lib.check(_lib.lib.td_step(self._h, io, self._stream()))
             return self.obs, self.reward, self.done

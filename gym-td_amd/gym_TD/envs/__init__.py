@@ -145,11 +145,12 @@ class _TDBasic(object):
         e = self._engine
         e.step(def_act, atk_act)
         torch.cuda.current_stream(e.device).synchronize()  # the kernel wrote the pinned outputs
-        self._obs = e.obs[0].numpy().copy()
-        reward = float(e.reward[0])
-        done = bool(e.done[0])
-        win = int(e.win[0])
-        an = int(e.allow_next[0])
+        n = e.np  # numpy views of the pinned outputs
+        self._obs = n.obs[0].copy()
+        reward = float(n.reward[0])
+        done = bool(n.done[0])
+        win = int(n.win[0])
+        an = int(n.allow_next[0])
         self.attacker_cd = 0 if (an & 1) else 2  # only "<= 1" is observable from the step
         self.defender_cd = 0 if (an & 2) else 2
         return self._obs.copy(), reward, done, (None if win < 0 else bool(win)), an
@@ -203,9 +204,9 @@ class TDDefense(_TDBasic):
         obs, reward, done, win, an = self._run(def_act=a)
         e = self._engine
         if self._multi:
-            real, fc = e.real_def[0].numpy().copy(), None  # the reference raises here (TDDefense.py:87)
+            real, fc = e.np.real_def[0].copy(), None  # the reference raises here (TDDefense.py:87)
         else:
-            real, fc = int(e.real_def[0]), int(e.fail_def[0])
+            real, fc = int(e.np.real_def[0]), int(e.np.fail_def[0])
         return obs, reward, done, {"RealAction": real, "Win": win, "AllowNextMove": bool(an & 2), "FailCode": fc}
 
 
@@ -226,9 +227,9 @@ class TDAttack(_TDBasic):
         a = np.asarray(action, dtype=np.int64).reshape(1, 3, 8)
         obs, reward, done, win, an = self._run(atk_act=a)
         e = self._engine
-        fa = e.fail_atk[0].numpy()
+        fa = e.np.fail_atk[0]
         fc = [int(v) for v in fa if v >= 0]
-        return obs, reward, done, {"RealAction": e.real_atk[0].numpy().copy(), "Win": win,
+        return obs, reward, done, {"RealAction": e.np.real_atk[0].copy(), "Win": win,
                                    "AllowNextMove": bool(an & 1), "FailCode": fc}
 
 
@@ -261,17 +262,18 @@ class TDMulti(_TDBasic):
         a = np.asarray(action["Attacker"], dtype=np.int64).reshape(1, 3, 8)
         obs, reward, done, win, an = self._run(def_act=d, atk_act=a)
         e = self._engine
-        real = {"Attacker": e.real_atk[0].numpy().copy()}
+        n = e.np
+        real = {"Attacker": n.real_atk[0].copy()}
         if self._multi:
-            real["Defender"] = e.real_def[0].numpy().copy()
+            real["Defender"] = n.real_def[0].copy()
             fc = None  # the reference raises here (TDMulti.py:134-135)
         else:
-            rd = int(e.real_def[0])
+            rd = int(n.real_def[0])
             real["Defender"] = rd
             if rd != L * L * 6:
-                real = rd  # TDMulti.py:257 replaces the whole dict
-            fa = e.fail_atk[0].numpy()
-            fc = {"Attacker": [int(v) for v in fa if v >= 0], "Defender": int(e.fail_def[0])}
+                real = rd  # TDMulti.py:114 replaces the whole dict
+            fa = n.fail_atk[0]
+            fc = {"Attacker": [int(v) for v in fa if v >= 0], "Defender": int(n.fail_def[0])}
         if win is not None:
             win = {"Defender": win, "Attacker": not win}
         return obs, reward, done, {"RealAction": real, "Win": win,
