@@ -56,6 +56,7 @@ constexpr int kSideStreams = 2;  // refill streams: one stuck on a long draw doe
 
 struct td_handle {
   int L = 0, NC = 0, B = 0, mode = 0, multi = 0, difficulty = 1, device = 0, autoreset = 1;
+  int opp_np = 0;  // random_agent=False
   int lw = 0;  // layout record words
   size_t scratch_stride = 0;
   TdDevCfg dcfg;
@@ -153,6 +154,7 @@ StepArgs base_args(td_handle* h) {
   std::memset(&a, 0, sizeof a);
   a.B = h->B; a.L = h->L; a.mode = h->mode; a.multi = h->multi; a.difficulty = h->difficulty;
   a.autoreset = h->autoreset;
+  a.opp_np = h->opp_np;
   a.hdr = h->d_hdr; a.en_lp = h->d_en_lp; a.en_mg = h->d_en_mg; a.en_inf = h->d_en_inf;
   a.tw_cd = h->d_tw_cd; a.tw_inf = h->d_tw_inf; a.cells = h->d_cells; a.opp_mt = h->d_opp; a.opp_hot = h->d_hot;
   a.np_mt = h->d_np; a.nxt = h->d_nxt; a.scratch = h->d_scratch; a.scratch_stride = h->scratch_stride;
@@ -366,7 +368,19 @@ int td_set_config(td_handle* h, const td_config* cfg) {
 
 int td_set_autoreset(td_handle* h, int on) {
   if (!h) return fail("NULL handle");
+  if (on && h->opp_np)
+    return fail("auto-reset needs random_agent=True: with random_agent=False the opponents draw from the "
+                "layout stream, which auto-reset draws ahead of play");
   h->autoreset = on ? 1 : 0;
+  return 0;
+}
+
+int td_set_random_agent(td_handle* h, int random_agent) {
+  if (!h) return fail("NULL handle");
+  if (!random_agent && h->autoreset)
+    return fail("random_agent=False needs auto-reset off (td_set_autoreset(h, 0) first): the opponents then "
+                "draw from the layout stream, which auto-reset draws ahead of play");
+  h->opp_np = random_agent ? 0 : 1;
   return 0;
 }
 

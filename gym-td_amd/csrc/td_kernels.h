@@ -13,6 +13,7 @@ constexpr int HOT_WORDS = 12;
 
 struct StepArgs {
   int B, L, mode, multi, difficulty, autoreset;
+  int opp_np;           // random_agent=False: the built-in opponents draw from np_mt (auto-reset off)
   TdHdr* hdr;
   double* en_lp;
   double* en_mg;

@@ -250,10 +250,37 @@ struct WaveMt {
     return r;
   }
   __device__ __forceinline__ int64_t randint(int64_t a, int64_t b) { return a + randbelow(b - a + 1); }
+  // numpy legacy RandomState.randint(lo, hi) (hi exclusive): masked rejection on 32-bit
+  // outputs, no draw when hi - lo == 1; also shuffle's random_interval(i) = np_randint(0, i + 1)
+  __device__ __forceinline__ int64_t np_randint(int64_t lo, int64_t hi) {
+    if (hi <= lo + 1) return lo;
+    const uint32_t rng = (uint32_t)(hi - lo - 1);
+    uint32_t mask = rng;
+    mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4; mask |= mask >> 8; mask |= mask >> 16;
+    uint32_t v = next() & mask;
+    while (v > rng) v = next() & mask;
+    return lo + (int64_t)v;
+  }
   __device__ __forceinline__ double random() {
     uint32_t x = next() >> 5, y = next() >> 6;
     return (x * 67108864.0 + y) * (1.0 / 9007199254740992.0);
   }
+};
+
+// The built-in opponents' random source (TDGymBasic.py:81-292).  random_agent=True: the
+// board's CPython stream.  random_agent=False: the board's numpy layout stream (the one
+// reset() draws roads from), except the destruct branch's tower index, which the
+// reference still draws from CPython random (:191, :287).  Each method is one call site
+// shape of the reference: ri(lo, hi) = random.randint(lo, hi) | np_random.randint(lo, hi + 1).
+struct OppRng {
+  WaveMt& py;
+  WaveMt* np;  // nullptr: random_agent=True
+  __device__ __forceinline__ int64_t ri(int64_t lo, int64_t hi) { return np ? np->np_randint(lo, hi + 1) : py.randint(lo, hi); }
+  __device__ __forceinline__ double rnd() { return np ? np->random() : py.random(); }
+  // random.shuffle's randbelow(i + 1) | np shuffle's random_interval(i)
+  __device__ __forceinline__ int64_t shuffle_j(int64_t i) { return np ? np->np_randint(0, i + 1) : py.randbelow(i + 1); }
+  // random_enemy_lv0's cluster slot: random.randint(0, types) (:85) | np_random.randint(0, types) (:88)
+  __device__ __forceinline__ int64_t slot(int64_t types) { return np ? np->np_randint(0, types) : py.randint(0, types); }
 };
 
 // ---------------------------------------------------------------------------
@@ -1071,17 +1098,17 @@ __device__ void store_board(const Smem<NC>& S, const U& u, const Ctx& x, const S
 // built-in opponents
 // ---------------------------------------------------------------------------
 template <int NC>
-__device__ void opponent_enemy(Smem<NC>& S, U& u, const Ctx& x, WaveMt& R, int difficulty) {
-  // random_enemy_lv0 / lv1 with random_agent=True (TDGymBasic.py:81-108)
+__device__ void opponent_enemy(Smem<NC>& S, U& u, const Ctx& x, OppRng& R, int difficulty) {
+  // random_enemy_lv0 / lv1 (TDGymBasic.py:81-108)
   if (u.atk_cd != 0) return;
   uint32_t types = 0;
   int road;
   if (difficulty == 0) {
-    for (int k = 0; k < 8; ++k) types |= (uint32_t)R.randint(0, 4) << (4 * k);
-    road = (int)R.randint(0, u.num_roads - 1);
+    for (int k = 0; k < 8; ++k) types |= (uint32_t)R.slot(4) << (4 * k);
+    road = (int)R.ri(0, u.num_roads - 1);
   } else {
-    const uint32_t t = (uint32_t)R.randint(0, 3);
-    road = (int)R.randint(0, u.num_roads - 1);
+    const uint32_t t = (uint32_t)R.ri(0, 3);
+    road = (int)R.ri(0, u.num_roads - 1);
     types = t * 0x11111111u;
   }
   summon_cluster(S, u, x, types, road, nullptr);
@@ -1090,18 +1117,18 @@ __device__ void opponent_enemy(Smem<NC>& S, U& u, const Ctx& x, WaveMt& R, int d
 }
 
 template <int NC>
-__device__ void opponent_tower_lv0(Smem<NC>& S, U& u, const Ctx& x, WaveMt& R) {
-  // random_tower_lv0 with random_agent=True (TDGymBasic.py:111-122)
+__device__ void opponent_tower_lv0(Smem<NC>& S, U& u, const Ctx& x, OppRng& R) {
+  // random_tower_lv0 (TDGymBasic.py:111-122)
   if (u.def_cd != 0) return;
-  int r = (int)R.randint(0, x.L - 1);
-  int c = (int)R.randint(0, x.L - 1);
-  int t = (int)R.randint(0, 3);
+  int r = (int)R.ri(0, x.L - 1);
+  int c = (int)R.ri(0, x.L - 1);
+  int t = (int)R.ri(0, 3);
   if (tower_build(S, u, x, t, r * x.L + c) == FC_OK) u.def_cd = x.C.def_interval;
 }
 
-// random_tower_lv1 / lv2 with random_agent=True (TDGymBasic.py:124-292).
+// random_tower_lv1 / lv2 (TDGymBasic.py:124-292).
 template <int NC>
-__device__ void build_near_road(Smem<NC>& S, U& u, const Ctx& x, WaveMt& R, int t, bool draw_type) {
+__device__ void build_near_road(Smem<NC>& S, U& u, const Ctx& x, OppRng& R, int t, bool draw_type) {
   // road cells in row-major order, then random.shuffle (Fisher-Yates on randbelow)
   // The list lives in the sort-key scratch as cell indices (<= L*L <= 4096 > 4*ECAP,
   // so it is kept in the group map instead: grp has 4*NC bytes -> store u16 cells).
@@ -1117,13 +1144,13 @@ __device__ void build_near_road(Smem<NC>& S, U& u, const Ctx& x, WaveMt& R, int 
   }
   __syncthreads();
   for (int i = nroad - 1; i >= 1; --i) {
-    int j = (int)R.randbelow(i + 1);
+    int j = (int)R.shuffle_j(i);
     if (x.lane == 0) { uint16_t tmp = cells[i]; cells[i] = cells[j]; cells[j] = tmp; }
     __syncthreads();
   }
-  if (draw_type) t = (int)R.randint(0, 3);
+  if (draw_type) t = (int)R.ri(0, 3);
   for (int i = 0; i < nroad; ++i) {
-    int k = (int)R.randint(0, 24);
+    int k = (int)R.ri(0, 24);
     int dr = k / 5 - 2, dc = k % 5 - 2;
     int cc = cells[i];
     int r = cc / x.L + dr, c = cc % x.L + dc;
@@ -1135,25 +1162,25 @@ __device__ void build_near_road(Smem<NC>& S, U& u, const Ctx& x, WaveMt& R, int 
 }
 
 template <int NC>
-__device__ void upgrade_or_destruct(Smem<NC>& S, U& u, const Ctx& x, WaveMt& R, int act) {
+__device__ void upgrade_or_destruct(Smem<NC>& S, U& u, const Ctx& x, OppRng& R, int act) {
   if (u.nt == 0) return;
   if (act == 1) {
-    int id = (int)R.randint(0, u.nt - 1);
+    int id = (int)R.ri(0, u.nt - 1);
     int cell = (int)(S.tInf[id] & 0xfffu);
     if (tower_lvup(S, u, x, cell) == FC_OK) u.def_cd = x.C.def_interval;
   } else {
-    if (R.random() > 0.01) return;
-    int id = (int)R.randint(0, u.nt - 1);
+    if (R.rnd() > 0.01) return;
+    int id = (int)R.py.randint(0, u.nt - 1);  // CPython random whatever random_agent is (:187, :191)
     int cell = (int)(S.tInf[id] & 0xfffu);
     if (tower_destruct(S, u, x, cell) == FC_OK) u.def_cd = x.C.def_interval;
   }
 }
 
 template <int NC>
-__device__ void opponent_tower(Smem<NC>& S, U& u, const Ctx& x, WaveMt& R, int difficulty) {
+__device__ void opponent_tower(Smem<NC>& S, U& u, const Ctx& x, OppRng& R, int difficulty) {
   if (difficulty == 0) { opponent_tower_lv0(S, u, x, R); return; }
   if (u.def_cd != 0) return;
-  int act = (int)R.randint(0, 2);
+  int act = (int)R.ri(0, 2);
   if (act != 0) { upgrade_or_destruct(S, u, x, R, act); return; }
   if (difficulty == 1) { build_near_road(S, u, x, R, 0, true); return; }
   // lv2: tower type from the enemy type mix (TDGymBasic.py:217-240)
@@ -1164,7 +1191,7 @@ __device__ void opponent_tower(Smem<NC>& S, U& u, const Ctx& x, WaveMt& R, int d
   // float32 array / int64 scalar promotes to float64 (NEP 50), so the ratio is an f64 quotient
   int types[4], nt = 0;
   for (int t = 0; t < 4; ++t) if (cnt[t]) types[nt++] = t;
-  double p = R.random();
+  double p = R.rnd();
   int chosen = -1;
   for (int i = 0; i < 4; ++i) {
     if (i >= nt) { u.flags |= FLAG_BAD_ACTION; break; }  // the reference raises IndexError here
@@ -1175,7 +1202,7 @@ __device__ void opponent_tower(Smem<NC>& S, U& u, const Ctx& x, WaveMt& R, int d
   if (chosen < 0) return;
   const int remap[4] = {2, 0, 1, 0};
   int t = remap[chosen];
-  if (R.random() < 0.2) t = 3;
+  if (R.rnd() < 0.2) t = 3;
   build_near_road(S, u, x, R, t, false);
 }
 
@@ -1278,15 +1305,21 @@ __device__ void step_board(Smem<NC>& S, const Ctx& x, const StepArgs& a, int b, 
     }
   }
   // ---- attacker
+  // random_agent=False: the opponents draw from the numpy layout stream (OppRng)
+  uint32_t* const npw = a.np_mt + (size_t)b * OPP_WORDS;
+  WaveMt N{npw, 0u, 0u};
+  if (MODE != MODE_2P && a.opp_np) { N.pos = npw[MT_N]; N.tw = npw[MT_N + 1]; N.cbase = N.pos; }
+  OppRng G{R, (MODE != MODE_2P && a.opp_np) ? &N : nullptr};
   if (MODE == MODE_DEF) {
-    opponent_enemy(S, u, x, R, a.difficulty);
+    opponent_enemy(S, u, x, G, a.difficulty);
   } else {
     attacker_actions<NC, MODE>(S, u, x, a, b);
     // info of the attacker now: its LDS arrays share space with the observation tables
     if (a.fail_atk && x.lane < 3) a.fail_atk[(size_t)b * 3 + x.lane] = S.fail_atk[x.lane];
     if (a.real_atk && x.lane < 24) a.real_atk[(size_t)b * 24 + x.lane] = S.real_atk[x.lane];
-    if (MODE == MODE_ATK) opponent_tower(S, u, x, R, a.difficulty);
+    if (MODE == MODE_ATK) opponent_tower(S, u, x, G, a.difficulty);
   }
+  if (MODE != MODE_2P && a.opp_np && x.lane == 0) { npw[MT_N] = N.pos; npw[MT_N + 1] = N.tw; }
   // pre-draw the next step's words: loads issued now, consumed at the end of the step
   if (MODE != MODE_2P) R.prefetch_issue(x.lane);
   __syncthreads();
@@ -1422,9 +1455,14 @@ __global__ __launch_bounds__(64) void td_opponent_kernel(StepArgs a, int side, i
   R.cn = lane_word(P.w, PF_HOT + 2);
   R.cbase = R.pos;
   R.cache = __shfl(P.w, PF_HOT + 4 + (x.lane & 7));
-  if (side == 0) opponent_enemy(S, u, x, R, level);
-  else opponent_tower(S, u, x, R, level);
+  uint32_t* const npw = a.np_mt + (size_t)b * OPP_WORDS;
+  WaveMt N{npw, 0u, 0u};
+  if (a.opp_np) { N.pos = npw[MT_N]; N.tw = npw[MT_N + 1]; N.cbase = N.pos; }
+  OppRng G{R, a.opp_np ? &N : nullptr};
+  if (side == 0) opponent_enemy(S, u, x, G, level);
+  else opponent_tower(S, u, x, G, level);
   __syncthreads();
+  if (a.opp_np && x.lane == 0) { npw[MT_N] = N.pos; npw[MT_N + 1] = N.tw; }
   R.prefetch(x.lane);  // the next step expects the hot record primed
   const size_t eb = (size_t)b * ECAP;
   for (int i = x.lane; i < u.n; i += 64) {

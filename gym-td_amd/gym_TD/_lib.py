@@ -60,6 +60,7 @@ def _load():
         "td_destroy": (None, [c_vp]),
         "td_set_config": (ctypes.c_int, [c_vp, ctypes.POINTER(TdConfig)]),
         "td_set_autoreset": (ctypes.c_int, [c_vp, ctypes.c_int]),
+        "td_set_random_agent": (ctypes.c_int, [c_vp, ctypes.c_int]),
         "td_seed": (ctypes.c_int, [c_vp, c_u32p, c_u32p]),
         "td_set_py_state": (ctypes.c_int, [c_vp, ctypes.c_int, c_u32p]),
         "td_get_py_state": (ctypes.c_int, [c_vp, ctypes.c_int, c_u32p]),

@@ -45,7 +45,8 @@ class TDEngine(object):
     """
 
     def __init__(self, map_size, n_boards, mode="def", multi_action=None, difficulty=1, device=None,
-                 np_seeds=None, py_seeds=None, autoreset=True, info=True, cfg=None, hp=None, host_io=False):
+                 np_seeds=None, py_seeds=None, autoreset=True, info=True, cfg=None, hp=None, host_io=False,
+                 random_agent=True):
         hp = hp or P.hyper_parameters
         if multi_action is None:
             multi_action = bool(hp.allow_multiple_actions)
@@ -64,6 +65,9 @@ class TDEngine(object):
         self.lw = _lib.lib.td_layout_words(self.L)
         self.autoreset = bool(autoreset)
         _lib.check(_lib.lib.td_set_autoreset(h, int(self.autoreset)))
+        self.random_agent = bool(random_agent)
+        if not self.random_agent:  # opponents on the layout stream (needs auto-reset off)
+            _lib.check(_lib.lib.td_set_random_agent(h, 0))
         B, L = self.B, self.L
         self.host_io = bool(host_io)
         dev = torch.device("cpu") if self.host_io else self.device

@@ -93,22 +93,23 @@ class _TDBasic(object):
     global ``random`` (TDGymBasic.py:84-86,98-100).  Here each env owns a copy of
     that stream: the global ``random`` state at construction, or
     ``random.Random(opponent_seed)`` when ``opponent_seed`` is given.
-    ``random_agent=False`` (opponent on ``np_random``) is not implemented.
+    ``random_agent=False``: the opponent draws from the env's ``np_random``, the
+    stream reset() draws layouts from (TDGymBasic.py:87-89,101-103,118-120,139-191,
+    213-287), checked against the oracle's restatement (not pinned by reference runs).
     """
     metadata = {"render.modes": ["human", "rgb_array"], "video.frames_per_second": 50}
     _mode = "def"
 
     def __init__(self, map_size, seed=None, fixed_seed=False, random_agent=True, difficulty=1,
                  opponent_seed=None, device=None):
-        if not random_agent:
-            raise NotImplementedError("random_agent=False (np_random-driven opponent) is not implemented")
         self.map_size = int(map_size)
         self.observation_space = Box(low=0., high=1., shape=(45, self.map_size, self.map_size), dtype=np.float32)
         self.fixed_seed, self.input_seed, self.random_agent = fixed_seed, seed, random_agent
         self.difficulty = difficulty
         self._multi = bool(P.hyper_parameters.allow_multiple_actions)
         self._engine = TDEngine(self.map_size, 1, self._mode, self._multi, difficulty if self._mode != "2p" else 1,
-                                device=device, autoreset=False, info=True, host_io=True)
+                                device=device, autoreset=False, info=True, host_io=True,
+                                random_agent=random_agent)
         if opponent_seed is not None:
             self._engine.seed(py_seeds=[opponent_seed])
         else:

@@ -109,6 +109,12 @@ td_handle* td_create(const td_config* cfg, int map_size, int n_boards, int mode,
 void td_destroy(td_handle* h);
 int td_set_config(td_handle* h, const td_config* cfg);
 int td_set_autoreset(td_handle* h, int on);
+/* TDGymBasic(random_agent=...) (TDGymBasic.py:18-26): with random_agent = 0 the built-in
+ * opponents draw from each board's numpy layout stream (np_random, :87-89,101-103,
+ * 118-120,139-160,176-177,188-190,213-256) instead of its CPython stream; the destruct
+ * branch's tower index stays on CPython random (:191, :287).  Requires auto-reset off
+ * (the layout stream is then shared by play and reset(), in order). */
+int td_set_random_agent(td_handle* h, int random_agent);
 
 /* Board b's layout stream = numpy.random.RandomState(np_seeds[b]) and its built-in
  * opponent stream = random.Random(py_seeds[b]).  Host arrays of n_boards entries. */

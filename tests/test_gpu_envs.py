@@ -586,8 +586,62 @@ def test_board_view_and_errors():
             env._engine.opponent("tower", 3)
     finally:
         env.close()
-    with pytest.raises(NotImplementedError):
-        E.TDDefense(L, seed=seed, random_agent=False)
     from gym_TD.vector import VectorEnv
     with pytest.raises(NotImplementedError):
         VectorEnv("TD-def-small-v0", 4, seed=0, fixed_seed=True)
+
+
+@pytest.mark.parametrize("cls,mode,L,difficulty,steps", [
+    ("TDDefense", "def", 10, 0, 1300), ("TDDefense", "def", 10, 1, 1300),
+    ("TDAttack", "atk", 10, 0, 300), ("TDAttack", "atk", 10, 1, 400), ("TDAttack", "atk", 20, 2, 300)])
+def test_random_agent_false_vs_oracle(cls, mode, L, difficulty, steps):
+    """random_agent=False (TDGymBasic.py:87-289): the built-in opponents draw from the
+    env's numpy layout stream, interleaved with reset()'s layout draws, except the
+    destruct branch's tower index (CPython random, :191, :287).  Checked bit-exactly
+    against the oracle's restatement of that branch over episodes and resets (the
+    reference itself was not run for this mode: parity unpinned)."""
+    rng = np.random.RandomState(L + difficulty)
+    seed, opp = 300 + 17 * difficulty + L, 900 + difficulty
+    while True:
+        try:
+            orc = O.Env(L, G.MODES[mode], difficulty, seed, opp, O.Config(), O.Hyper(), random_agent=False,
+                        road_attempts=ROAD_ATTEMPTS)
+            break
+        except O.RoadGenError:
+            seed += 1
+    env = getattr(E, cls)(L, difficulty=difficulty, seed=seed, opponent_seed=opp, random_agent=False)
+    try:
+        assert np.array_equal(env._obs, orc._board.get_states())
+        resets, ended, road_fail = 0, False, False
+        for k in range(steps):
+            if mode == "def":
+                a = policies.discrete_def(rng, L, orc._board.map[0], 0.6)
+                wo, wr, wd, wi = orc.step(a, None)
+            else:
+                a = policies.atk(rng)
+                wo, wr, wd, wi = orc.step(None, a)
+            o, r, d, info = env.step(a)
+            assert canon.fhex(r) == canon.fhex(wr), k
+            assert np.array_equal(o, wo), k
+            assert d == bool(wd), k
+            if d:
+                ended = True
+                try:
+                    wo = orc.reset()
+                except O.RoadGenError:
+                    with pytest.raises(RuntimeError):
+                        env.reset()
+                    road_fail = True
+                    break
+                assert np.array_equal(env.reset(), wo), k
+                resets += 1
+        if not road_fail:
+            assert env._engine.get_np_state(0)[:625].tolist() == list(orc.np_random.get_state()[1]) + \
+                [orc.np_random.get_state()[2]]
+        # TD-def episodes run to max_episode_steps (1200) against a random defender
+        assert ended or mode == "atk"
+    finally:
+        env.close()
+    # auto-reset draws layouts ahead of play: refused with random_agent=False
+    with pytest.raises(Exception):
+        TDEngine(L, 2, mode, False, difficulty, autoreset=True, random_agent=False)
