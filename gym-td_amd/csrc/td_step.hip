@@ -267,21 +267,50 @@ struct WaveMt {
   }
 };
 
-// The built-in opponents' random source (TDGymBasic.py:81-292).  random_agent=True: the
-// board's CPython stream.  random_agent=False: the board's numpy layout stream (the one
-// reset() draws roads from), except the destruct branch's tower index, which the
-// reference still draws from CPython random (:191, :287).  Each method is one call site
-// shape of the reference: ri(lo, hi) = random.randint(lo, hi) | np_random.randint(lo, hi + 1).
+// The built-in opponents' random source (TDGymBasic.py:81-292).  random_agent=True
+// (NP = false): the board's CPython stream.  random_agent=False (NP = true): the
+// board's numpy layout stream (the one reset() draws roads from), except the destruct
+// branch's tower index, which the reference still draws from CPython random (:191,
+// :287).  Each method is one call site shape of the reference: ri(lo, hi) =
+// random.randint(lo, hi) | np_random.randint(lo, hi + 1).  NP is a template argument,
+// not a nullable pointer: a pointer chosen between two locals at run time would keep
+// both streams in scratch memory.
+template <bool NP>
 struct OppRng {
   WaveMt& py;
-  WaveMt* np;  // nullptr: random_agent=True
-  __device__ __forceinline__ int64_t ri(int64_t lo, int64_t hi) { return np ? np->np_randint(lo, hi + 1) : py.randint(lo, hi); }
-  __device__ __forceinline__ double rnd() { return np ? np->random() : py.random(); }
+  WaveMt& np;  // == py when !NP
+  __device__ __forceinline__ int64_t ri(int64_t lo, int64_t hi) {
+    if constexpr (NP) return np.np_randint(lo, hi + 1); else return py.randint(lo, hi);
+  }
+  __device__ __forceinline__ double rnd() {
+    if constexpr (NP) return np.random(); else return py.random();
+  }
   // random.shuffle's randbelow(i + 1) | np shuffle's random_interval(i)
-  __device__ __forceinline__ int64_t shuffle_j(int64_t i) { return np ? np->np_randint(0, i + 1) : py.randbelow(i + 1); }
+  __device__ __forceinline__ int64_t shuffle_j(int64_t i) {
+    if constexpr (NP) return np.np_randint(0, i + 1); else return py.randbelow(i + 1);
+  }
   // random_enemy_lv0's cluster slot: random.randint(0, types) (:85) | np_random.randint(0, types) (:88)
-  __device__ __forceinline__ int64_t slot(int64_t types) { return np ? np->np_randint(0, types) : py.randint(0, types); }
+  __device__ __forceinline__ int64_t slot(int64_t types) {
+    if constexpr (NP) return np.np_randint(0, types); else return py.randint(0, types);
+  }
 };
+
+// Runs f(OppRng<...>&) on the stream random_agent selects.  random_agent=False: board
+// b's numpy layout stream, loaded from and stored back to its MT record (np_mt).
+template <class F>
+__device__ __forceinline__ void with_opp_rng(const StepArgs& a, int b, int lane, WaveMt& R, F&& f) {
+  if (a.opp_np) {
+    uint32_t* const npw = a.np_mt + (size_t)b * OPP_WORDS;
+    WaveMt N{npw, npw[MT_N], npw[MT_N + 1]};
+    N.cbase = N.pos;
+    OppRng<true> G{R, N};
+    f(G);
+    if (lane == 0) { npw[MT_N] = N.pos; npw[MT_N + 1] = N.tw; }
+  } else {
+    OppRng<false> G{R, R};
+    f(G);
+  }
+}
 
 // ---------------------------------------------------------------------------
 // defender operations (TDBoard.py:226-293), wave-uniform
@@ -1097,8 +1126,8 @@ __device__ void store_board(const Smem<NC>& S, const U& u, const Ctx& x, const S
 // ---------------------------------------------------------------------------
 // built-in opponents
 // ---------------------------------------------------------------------------
-template <int NC>
-__device__ void opponent_enemy(Smem<NC>& S, U& u, const Ctx& x, OppRng& R, int difficulty) {
+template <int NC, class Rng>
+__device__ void opponent_enemy(Smem<NC>& S, U& u, const Ctx& x, Rng& R, int difficulty) {
   // random_enemy_lv0 / lv1 (TDGymBasic.py:81-108)
   if (u.atk_cd != 0) return;
   uint32_t types = 0;
@@ -1116,8 +1145,8 @@ __device__ void opponent_enemy(Smem<NC>& S, U& u, const Ctx& x, OppRng& R, int d
   u.atk_cd = x.C.atk_interval;  // the (ok, real) tuple is always truthy
 }
 
-template <int NC>
-__device__ void opponent_tower_lv0(Smem<NC>& S, U& u, const Ctx& x, OppRng& R) {
+template <int NC, class Rng>
+__device__ void opponent_tower_lv0(Smem<NC>& S, U& u, const Ctx& x, Rng& R) {
   // random_tower_lv0 (TDGymBasic.py:111-122)
   if (u.def_cd != 0) return;
   int r = (int)R.ri(0, x.L - 1);
@@ -1127,8 +1156,8 @@ __device__ void opponent_tower_lv0(Smem<NC>& S, U& u, const Ctx& x, OppRng& R) {
 }
 
 // random_tower_lv1 / lv2 (TDGymBasic.py:124-292).
-template <int NC>
-__device__ void build_near_road(Smem<NC>& S, U& u, const Ctx& x, OppRng& R, int t, bool draw_type) {
+template <int NC, class Rng>
+__device__ void build_near_road(Smem<NC>& S, U& u, const Ctx& x, Rng& R, int t, bool draw_type) {
   // road cells in row-major order, then random.shuffle (Fisher-Yates on randbelow)
   // The list lives in the sort-key scratch as cell indices (<= L*L <= 4096 > 4*ECAP,
   // so it is kept in the group map instead: grp has 4*NC bytes -> store u16 cells).
@@ -1161,8 +1190,8 @@ __device__ void build_near_road(Smem<NC>& S, U& u, const Ctx& x, OppRng& R, int 
   }
 }
 
-template <int NC>
-__device__ void upgrade_or_destruct(Smem<NC>& S, U& u, const Ctx& x, OppRng& R, int act) {
+template <int NC, class Rng>
+__device__ void upgrade_or_destruct(Smem<NC>& S, U& u, const Ctx& x, Rng& R, int act) {
   if (u.nt == 0) return;
   if (act == 1) {
     int id = (int)R.ri(0, u.nt - 1);
@@ -1176,8 +1205,8 @@ __device__ void upgrade_or_destruct(Smem<NC>& S, U& u, const Ctx& x, OppRng& R, 
   }
 }
 
-template <int NC>
-__device__ void opponent_tower(Smem<NC>& S, U& u, const Ctx& x, OppRng& R, int difficulty) {
+template <int NC, class Rng>
+__device__ void opponent_tower(Smem<NC>& S, U& u, const Ctx& x, Rng& R, int difficulty) {
   if (difficulty == 0) { opponent_tower_lv0(S, u, x, R); return; }
   if (u.def_cd != 0) return;
   int act = (int)R.ri(0, 2);
@@ -1305,21 +1334,16 @@ __device__ void step_board(Smem<NC>& S, const Ctx& x, const StepArgs& a, int b, 
     }
   }
   // ---- attacker
-  // random_agent=False: the opponents draw from the numpy layout stream (OppRng)
-  uint32_t* const npw = a.np_mt + (size_t)b * OPP_WORDS;
-  WaveMt N{npw, 0u, 0u};
-  if (MODE != MODE_2P && a.opp_np) { N.pos = npw[MT_N]; N.tw = npw[MT_N + 1]; N.cbase = N.pos; }
-  OppRng G{R, (MODE != MODE_2P && a.opp_np) ? &N : nullptr};
   if (MODE == MODE_DEF) {
-    opponent_enemy(S, u, x, G, a.difficulty);
+    with_opp_rng(a, b, x.lane, R, [&](auto& G) { opponent_enemy(S, u, x, G, a.difficulty); });
   } else {
     attacker_actions<NC, MODE>(S, u, x, a, b);
     // info of the attacker now: its LDS arrays share space with the observation tables
     if (a.fail_atk && x.lane < 3) a.fail_atk[(size_t)b * 3 + x.lane] = S.fail_atk[x.lane];
     if (a.real_atk && x.lane < 24) a.real_atk[(size_t)b * 24 + x.lane] = S.real_atk[x.lane];
-    if (MODE == MODE_ATK) opponent_tower(S, u, x, G, a.difficulty);
+    if (MODE == MODE_ATK)
+      with_opp_rng(a, b, x.lane, R, [&](auto& G) { opponent_tower(S, u, x, G, a.difficulty); });
   }
-  if (MODE != MODE_2P && a.opp_np && x.lane == 0) { npw[MT_N] = N.pos; npw[MT_N + 1] = N.tw; }
   // pre-draw the next step's words: loads issued now, consumed at the end of the step
   if (MODE != MODE_2P) R.prefetch_issue(x.lane);
   __syncthreads();
@@ -1455,14 +1479,11 @@ __global__ __launch_bounds__(64) void td_opponent_kernel(StepArgs a, int side, i
   R.cn = lane_word(P.w, PF_HOT + 2);
   R.cbase = R.pos;
   R.cache = __shfl(P.w, PF_HOT + 4 + (x.lane & 7));
-  uint32_t* const npw = a.np_mt + (size_t)b * OPP_WORDS;
-  WaveMt N{npw, 0u, 0u};
-  if (a.opp_np) { N.pos = npw[MT_N]; N.tw = npw[MT_N + 1]; N.cbase = N.pos; }
-  OppRng G{R, a.opp_np ? &N : nullptr};
-  if (side == 0) opponent_enemy(S, u, x, G, level);
-  else opponent_tower(S, u, x, G, level);
+  with_opp_rng(a, b, x.lane, R, [&](auto& G) {
+    if (side == 0) opponent_enemy(S, u, x, G, level);
+    else opponent_tower(S, u, x, G, level);
+  });
   __syncthreads();
-  if (a.opp_np && x.lane == 0) { npw[MT_N] = N.pos; npw[MT_N + 1] = N.tw; }
   R.prefetch(x.lane);  // the next step expects the hot record primed
   const size_t eb = (size_t)b * ECAP;
   for (int i = x.lane; i < u.n; i += 64) {
