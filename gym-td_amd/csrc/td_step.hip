@@ -1127,7 +1127,7 @@ __device__ void store_board(const Smem<NC>& S, const U& u, const Ctx& x, const S
 // built-in opponents
 // ---------------------------------------------------------------------------
 template <int NC, class Rng>
-__device__ void opponent_enemy(Smem<NC>& S, U& u, const Ctx& x, Rng& R, int difficulty) {
+__device__ __forceinline__ void opponent_enemy(Smem<NC>& S, U& u, const Ctx& x, Rng& R, int difficulty) {
   // random_enemy_lv0 / lv1 (TDGymBasic.py:81-108)
   if (u.atk_cd != 0) return;
   uint32_t types = 0;
@@ -1146,7 +1146,7 @@ __device__ void opponent_enemy(Smem<NC>& S, U& u, const Ctx& x, Rng& R, int diff
 }
 
 template <int NC, class Rng>
-__device__ void opponent_tower_lv0(Smem<NC>& S, U& u, const Ctx& x, Rng& R) {
+__device__ __forceinline__ void opponent_tower_lv0(Smem<NC>& S, U& u, const Ctx& x, Rng& R) {
   // random_tower_lv0 (TDGymBasic.py:111-122)
   if (u.def_cd != 0) return;
   int r = (int)R.ri(0, x.L - 1);
@@ -1157,7 +1157,7 @@ __device__ void opponent_tower_lv0(Smem<NC>& S, U& u, const Ctx& x, Rng& R) {
 
 // random_tower_lv1 / lv2 (TDGymBasic.py:124-292).
 template <int NC, class Rng>
-__device__ void build_near_road(Smem<NC>& S, U& u, const Ctx& x, Rng& R, int t, bool draw_type) {
+__device__ __forceinline__ void build_near_road(Smem<NC>& S, U& u, const Ctx& x, Rng& R, int t, bool draw_type) {
   // road cells in row-major order, then random.shuffle (Fisher-Yates on randbelow)
   // The list lives in the sort-key scratch as cell indices (<= L*L <= 4096 > 4*ECAP,
   // so it is kept in the group map instead: grp has 4*NC bytes -> store u16 cells).
@@ -1191,7 +1191,7 @@ __device__ void build_near_road(Smem<NC>& S, U& u, const Ctx& x, Rng& R, int t, 
 }
 
 template <int NC, class Rng>
-__device__ void upgrade_or_destruct(Smem<NC>& S, U& u, const Ctx& x, Rng& R, int act) {
+__device__ __forceinline__ void upgrade_or_destruct(Smem<NC>& S, U& u, const Ctx& x, Rng& R, int act) {
   if (u.nt == 0) return;
   if (act == 1) {
     int id = (int)R.ri(0, u.nt - 1);
@@ -1206,7 +1206,7 @@ __device__ void upgrade_or_destruct(Smem<NC>& S, U& u, const Ctx& x, Rng& R, int
 }
 
 template <int NC, class Rng>
-__device__ void opponent_tower(Smem<NC>& S, U& u, const Ctx& x, Rng& R, int difficulty) {
+__device__ __forceinline__ void opponent_tower(Smem<NC>& S, U& u, const Ctx& x, Rng& R, int difficulty) {
   if (difficulty == 0) { opponent_tower_lv0(S, u, x, R); return; }
   if (u.def_cd != 0) return;
   int act = (int)R.ri(0, 2);
@@ -1279,7 +1279,10 @@ __device__ void attacker_actions(Smem<NC>& S, U& u, const Ctx& x, const StepArgs
 }
 
 
-template <int NC, int LT, int MODE>
+// SCAN: the multi-action defender scan is compiled in (launched only when a.multi).
+// Its 16-B staging buffers raise the 30x30 kernel from 55 to 148 VGPRs, and the
+// discrete kernel should not pay for them in occupancy.
+template <int NC, int LT, int MODE, bool SCAN>
 __device__ void step_board(Smem<NC>& S, const Ctx& x, const StepArgs& a, int b, const Prefetch& P) {
   const TdDevCfg& C = x.C;
   uint32_t* const opp = a.opp_mt + (size_t)b * OPP_WORDS;
@@ -1318,7 +1321,7 @@ __device__ void step_board(Smem<NC>& S, const Ctx& x, const StepArgs& a, int b, 
 
   // ---- defender
   if (MODE != MODE_ATK) {
-    if (a.multi) {
+    if (SCAN) {
       defender_scan(S, u, x, a.def_act + (size_t)b * 6 * x.NCr,
                     a.real_def ? a.real_def + (size_t)b * 6 * x.NCr : nullptr, u.def_cd == 0);
     } else {
@@ -1441,7 +1444,7 @@ __device__ void step_board(Smem<NC>& S, const Ctx& x, const StepArgs& a, int b, 
 // One workgroup (one wave) per board.  (A persistent variant that prefetched the
 // next board while stepping the current one measured slower: its static board
 // assignment leaves a one-board tail, and the step is bound by HBM writes.)
-template <int LT, int MODE>
+template <int LT, int MODE, bool SCAN>
 __global__ __launch_bounds__(64) void td_step_kernel(StepArgs a) {
   constexpr int NC = LT ? LT * LT : MAX_KERNEL_L * MAX_KERNEL_L;
   __shared__ Smem<NC> S;
@@ -1452,7 +1455,7 @@ __global__ __launch_bounds__(64) void td_step_kernel(StepArgs a) {
   const Ctx x{S.cfg, L, L * L, (int)threadIdx.x};
   Prefetch P;
   prefetch_issue(P, a, b, x.lane, x.NCr, MODE != MODE_ATK && !a.multi);
-  step_board<NC, LT, MODE>(S, x, a, b, P);
+  step_board<NC, LT, MODE, SCAN>(S, x, a, b, P);
 }
 
 // The built-in opponents called on their own, between steps (TDGymBasic.py:81-292,
@@ -1695,9 +1698,11 @@ __global__ __launch_bounds__(64) void td_refill_kernel(StepArgs a) {
 template <int LT>
 static hipError_t launch2(const StepArgs& a, hipStream_t s, bool reset) {
   if (reset) hipLaunchKernelGGL(td_reset_kernel<LT>, dim3(a.B), dim3(64), 0, s, a);
-  else if (a.mode == MODE_DEF) hipLaunchKernelGGL((td_step_kernel<LT, MODE_DEF>), dim3(a.B), dim3(64), 0, s, a);
-  else if (a.mode == MODE_ATK) hipLaunchKernelGGL((td_step_kernel<LT, MODE_ATK>), dim3(a.B), dim3(64), 0, s, a);
-  else hipLaunchKernelGGL((td_step_kernel<LT, MODE_2P>), dim3(a.B), dim3(64), 0, s, a);
+  else if (a.mode == MODE_DEF && a.multi) hipLaunchKernelGGL((td_step_kernel<LT, MODE_DEF, true>), dim3(a.B), dim3(64), 0, s, a);
+  else if (a.mode == MODE_DEF) hipLaunchKernelGGL((td_step_kernel<LT, MODE_DEF, false>), dim3(a.B), dim3(64), 0, s, a);
+  else if (a.mode == MODE_ATK) hipLaunchKernelGGL((td_step_kernel<LT, MODE_ATK, false>), dim3(a.B), dim3(64), 0, s, a);
+  else if (a.multi) hipLaunchKernelGGL((td_step_kernel<LT, MODE_2P, true>), dim3(a.B), dim3(64), 0, s, a);
+  else hipLaunchKernelGGL((td_step_kernel<LT, MODE_2P, false>), dim3(a.B), dim3(64), 0, s, a);
   return hipGetLastError();
 }
 
