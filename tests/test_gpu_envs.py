@@ -24,14 +24,15 @@ from test_gpu_parity import reference_settings  # noqa: E402
 ROAD_ATTEMPTS = 1000  # td_kernels.h kRoadAttempts: the device's bound of each create_road_v2 loop
 
 
-def _first_ok_seeds(L, n, start, mode, multi, difficulty, cfg=None):
+def _first_ok_seeds(L, n, start, mode, multi, difficulty, cfg=None, random_agent=True):
     """Seeds whose first layout draw succeeds, with their oracle envs."""
     hp = O.Hyper(allow_multiple_actions=multi)
     seeds, envs = [], []
     s = start
     while len(seeds) < n:
         try:
-            envs.append(O.Env(L, G.MODES[mode], difficulty, s, s, cfg or O.Config(), hp, road_attempts=ROAD_ATTEMPTS))
+            envs.append(O.Env(L, G.MODES[mode], difficulty, s, s, cfg or O.Config(), hp, random_agent=random_agent,
+                              road_attempts=ROAD_ATTEMPTS))
             seeds.append(s)
         except O.RoadGenError:
             pass
@@ -43,26 +44,33 @@ def _fc_list(row):
     return [int(v) for v in row if v >= 0]
 
 
-@pytest.mark.parametrize("L,B,mode,multi,difficulty,steps", [
-    (10, 24, "atk", False, 0, 150),
-    (10, 24, "atk", False, 1, 150),
-    (10, 24, "atk", False, 2, 150),
-    (20, 12, "atk", False, 2, 100),
-    (10, 24, "2p", False, 1, 150),
-    (10, 16, "2p", True, 1, 120),
-    (10, 16, "def", True, 1, 120),
-    (10, 24, "def", False, 0, 150),
+@pytest.mark.parametrize("L,B,mode,multi,difficulty,steps,random_agent", [
+    (10, 24, "atk", False, 0, 150, True),
+    (10, 24, "atk", False, 1, 150, True),
+    (10, 24, "atk", False, 2, 150, True),
+    (20, 12, "atk", False, 2, 100, True),
+    (10, 24, "2p", False, 1, 150, True),
+    (10, 16, "2p", True, 1, 120, True),
+    (10, 16, "def", True, 1, 120, True),
+    (10, 24, "def", False, 0, 150, True),
     # sizes off the specialised kernels (generic L <= 32 build; odd L*L: scalar observation path)
-    (8, 16, "def", False, 1, 120),
-    (12, 12, "atk", False, 1, 100),
-    (15, 8, "2p", True, 1, 80),
-    (16, 8, "def", False, 1, 100),
+    (8, 16, "def", False, 1, 120, True),
+    (12, 12, "atk", False, 1, 100, True),
+    (15, 8, "2p", True, 1, 80, True),
+    (16, 8, "def", False, 1, 100, True),
+    # random_agent=False: the opponents on each board's numpy layout stream (OppRng<true>)
+    (10, 16, "def", True, 1, 120, False),
+    (10, 24, "def", False, 0, 150, False),
+    (10, 24, "atk", False, 1, 150, False),
+    (20, 12, "atk", False, 2, 100, False),
+    (30, 6, "def", False, 1, 80, False),
 ])
-def test_batched_modes_vs_oracle(L, B, mode, multi, difficulty, steps):
+def test_batched_modes_vs_oracle(L, B, mode, multi, difficulty, steps, random_agent):
     """B boards of one mode in one launch vs B oracle envs: reward bits, done,
     state digest, observation bytes and the info tensors of every board."""
-    seeds, orc = _first_ok_seeds(L, B, 3000 + 97 * difficulty, mode, multi, difficulty)
-    eng = TDEngine(L, B, mode, multi, difficulty, np_seeds=seeds, py_seeds=seeds, autoreset=False)
+    seeds, orc = _first_ok_seeds(L, B, 3000 + 97 * difficulty, mode, multi, difficulty, random_agent=random_agent)
+    eng = TDEngine(L, B, mode, multi, difficulty, np_seeds=seeds, py_seeds=seeds, autoreset=False,
+                   random_agent=random_agent)
     try:
         _, failed = eng.reset()
         assert not failed
