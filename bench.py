@@ -4,29 +4,34 @@
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
-Workload (BASELINE.json configs[1]/[3] shape, per GPU): TD-def-small (10x10),
-``--boards`` boards per GPU (default 65,536 = the metric's batch), built-in lv1
-opponent, uniform random defender actions over [0, 601) drawn on the device
-before the timed region, auto-reset on.  ``--workload`` selects the other
-SURVEY.md 8(d) shapes for their own measurement lines (not the metric):
-``2p-middle-multi`` (16,384 x TD-2p 20x20, multi-action defender flags uniform in
-{0,1,2}, attacker clusters uniform in {0..4}) and ``def-large`` (16,384 x TD-def
-30x30, the per-GPU share of configs[4]).  Boards are seeded base + global index
-(trajectories do not depend on the GPU count) and burned in ``--burnin`` steps
-untimed.  The burn-in staggers the episodes: at burn-in step k the boards whose
-global index is k modulo the episode limit (1,200 steps) are reset explicitly, so
-after a full burn-in the boards' episode phases are spread uniformly and the
-timed steps see the steady state of a long rollout -- about B / 1,200 auto-resets
-(layout draws included) per step and every tower count of an episode -- instead
-of the synchronised start of a fresh batch, where every board would reset in
-the same step.
-Scaling is weak: every rank owns its own boards; the only collective is the
-timing all-reduce and the episode-stat gather after the timed region.
+Workload: TD-def-small (10x10), built-in lv1 opponent, uniform random defender
+actions over [0, 601) drawn on the device before the timed region, auto-reset on.
+Scaling is STRONG by default, as BASELINE.json's metric and configs[3] state it:
+the global batch (default 65,536 boards = "batch=65k") is split over the N ranks,
+65,536 / N boards per GPU (8,192 at N = 8), contiguous global board blocks per
+rank.  ``--boards-per-gpu B`` instead runs B boards on every rank (weak scaling)
+and labels its line as such.  ``--workload`` selects the other SURVEY.md 8(d)
+shapes for their own lines (not the metric): ``2p-middle-multi`` (configs[2]:
+16,384 x TD-2p 20x20, multi-action defender flags uniform in {0,1,2}, attacker
+clusters uniform in {0..4}) and ``def-large`` (configs[4]: 131,072 x TD-def 30x30
+over the node).  Boards are seeded base + global index (trajectories do not
+depend on the GPU count) and burned in ``--burnin`` steps untimed.  The burn-in
+staggers the episodes: at burn-in step k the boards whose global index is k
+modulo the episode limit (1,200 steps) are reset explicitly, so after a full
+burn-in the boards' episode phases are spread uniformly and the timed steps see
+the steady state of a long rollout -- about B / 1,200 auto-resets (layout draws
+included) per step and every tower count of an episode -- instead of the
+synchronised start of a fresh batch, where every board would reset in the same
+step.  There is no collective on the data path: the only ones are the timing
+MAX and the episode-stat gather after the timed region (RCCL on GPUs).
 
-One JSON line on rank 0: metric/value/unit, ``roofline`` for the step kernel
-(HIP events on the launch stream, algorithmic bytes per launch) and
-``cpu_baseline`` (the C restatement oracle/td_cpu.c on this host's cores, rank 0,
-N=1; ``cpu_baseline_python`` times the Python restatement the same way).
+One JSON line on rank 0: metric/value/unit (the metric string, ``global_batch``,
+``boards_per_gpu`` and ``scaling`` follow what actually ran), ``roofline`` for
+the step kernel (HIP events on the launch stream, algorithmic bytes per launch;
+``traffic`` is the PMC-measured HBM bytes per launch of the same kernel build at
+the same boards per GPU, with its source, or null) and ``cpu_baseline`` (the C
+restatement oracle/td_cpu.c on this host's cores, rank 0, N=1;
+``cpu_baseline_python`` times the Python restatement the same way).
 """
 import argparse
 import json
@@ -46,13 +51,14 @@ import torch.distributed as dist  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 
 
-# name -> (map size, mode, multi-action, default boards per GPU, metric)
+# name -> (map size, mode, multi-action, default GLOBAL batch (split over the ranks), BASELINE config)
 WORKLOADS = {
-    "def-small": (10, "def", False, 65536, "env-steps/sec (whole node), 10x10 board, batch=65k, at 1/2/4/8 MI355X"),
-    "2p-middle-multi": (20, "2p", True, 16384, "env-steps/sec (whole node), TD-2p-middle 20x20 multi-action, "
-                                                "16k boards per GPU"),
-    "def-large": (30, "def", False, 16384, "env-steps/sec (whole node), TD-def-large 30x30, 16k boards per GPU"),
+    "def-small": (10, "def", False, 65536, "configs[1]/[3]"),
+    "2p-middle-multi": (20, "2p", True, 16384, "configs[2]"),
+    "def-large": (30, "def", False, 131072, "configs[4]"),
 }
+# BASELINE.json's metric, quoted verbatim when the run is exactly its configuration
+BASELINE_METRIC = "env-steps/sec (whole node), 10\u00d710 board, batch=65k, at 1/2/4/8 MI355X"
 ENV_ID = {"def-small": "TD-def-small-v0", "2p-middle-multi": "TD-2p-middle-v0 (allow_multiple_actions)",
           "def-large": "TD-def-large-v0"}
 DATA = {("def", False): "synthetic: uniform random defender actions, built-in lv1 opponent, seeded boards",
@@ -69,6 +75,58 @@ def algorithmic_bytes(L, mode="def", multi=False):
     act = (6 * L * L * 8 if multi else 8) if mode != "atk" else 0
     act += 3 * 8 * 8 if mode != "def" else 0
     return obs + act + 8 + 1
+
+
+def partition(workload, world, global_batch=None, boards_per_gpu=None):
+    """Boards per rank and the scaling mode of a run.
+
+    Strong scaling (default): the global batch -- BASELINE's 65,536 boards for the
+    metric -- is split evenly over the ranks.  Weak scaling: ``boards_per_gpu`` on
+    every rank.  Returns (boards per rank, global batch, "strong" | "weak")."""
+    if boards_per_gpu is not None:
+        if boards_per_gpu < 1:
+            raise ValueError("--boards-per-gpu must be >= 1")
+        return int(boards_per_gpu), int(boards_per_gpu) * world, "weak"
+    g = int(global_batch or WORKLOADS[workload][3])
+    if g < world or g % world:
+        raise ValueError("global batch %d does not split evenly over %d ranks" % (g, world))
+    return g // world, g, "strong"
+
+
+def metric_label(workload, global_batch, scaling):
+    """The metric string of what ran: BASELINE.json's own metric only for its config."""
+    L = WORKLOADS[workload][0]
+    if workload == "def-small" and global_batch == 65536 and scaling == "strong":
+        return BASELINE_METRIC
+    kind = {"def-small": "TD-def", "def-large": "TD-def", "2p-middle-multi": "TD-2p multi-action"}[workload]
+    return "env-steps/sec (whole node), %s %dx%d board, batch=%d (%s scaling)" % (kind, L, L, global_batch, scaling)
+
+
+def kernel_source_hash():
+    """sha256 (16 hex) of the step kernel's sources: a PMC traffic record is quoted
+    only for the build it was measured on."""
+    import hashlib
+    h = hashlib.sha256()
+    d = os.path.join(HERE, "gym-td_amd", "csrc")
+    for f in sorted(os.listdir(d)):
+        if f.endswith((".hip", ".h")):
+            h.update(open(os.path.join(d, f), "rb").read())
+    return h.hexdigest()[:16]
+
+
+def measured_traffic(workload, boards):
+    """(bytes per launch, source) from profiles/pmc_traffic.json when that file holds a
+    PMC measurement of this workload at these boards per GPU on this kernel build."""
+    tp = os.path.join(HERE, "profiles", "pmc_traffic.json")
+    try:
+        rec = json.load(open(tp)).get("%s_B%d" % (workload, boards))
+    except Exception:  # noqa: BLE001
+        return None, None
+    if not rec or rec.get("kernel_src") != kernel_source_hash():
+        return None, None
+    return rec["hbm_bytes_per_launch"], "profiles/pmc_traffic.json[%s_B%d] (%s, rocprofv3 --pmc FETCH_SIZE / " \
+        "WRITE_SIZE passes of bench.py at the same boards per GPU, kernel sources %s)" % (
+            workload, boards, rec.get("round", "?"), rec["kernel_src"])
 
 
 # --------------------------------------------------------------------------- CPU baseline
@@ -145,7 +203,10 @@ def main():
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--workload", default="def-small", choices=sorted(WORKLOADS))
-    ap.add_argument("--boards", type=int, default=None, help="boards per GPU (default: the workload's)")
+    ap.add_argument("--global-batch", type=int, default=None,
+                    help="boards over all ranks, split evenly (strong scaling; default: the workload's)")
+    ap.add_argument("--boards-per-gpu", "--boards", dest="boards_per_gpu", type=int, default=None,
+                    help="boards on every rank (weak scaling, its own labelled line)")
     ap.add_argument("--burnin", type=int, default=1200)
     ap.add_argument("--stagger", type=int, default=1, help="stagger episode phases during burn-in (see docstring)")
     ap.add_argument("--seed", type=int, default=0)
@@ -176,8 +237,9 @@ def main():
     from gym_TD import shard
     from gym_TD import params as P
 
-    L, mode, multi, B_default, metric = WORKLOADS[args.workload]
-    B = args.boards or B_default
+    L, mode, multi, _, base_cfg = WORKLOADS[args.workload]
+    B, global_batch, scaling = partition(args.workload, world, args.global_batch, args.boards_per_gpu)
+    metric = metric_label(args.workload, global_batch, scaling)
     K, W = args.steps, args.warmup
     seeds = shard.shard_seeds(args.seed, rank, B)
     # info tensors (win, allow-next, fail codes, real actions, episode totals) are written
@@ -258,29 +320,21 @@ def main():
         value = total_steps / elapsed
         bpe = algorithmic_bytes(L, mode, multi)
         achieved = B * bpe / avg_kernel_s / 1e9
-        traffic = None
-        tp = os.path.join(HERE, "profiles", "pmc_traffic.json")
-        if os.path.exists(tp):
-            try:
-                tj = json.load(open(tp))
-                key = "%s_B%d" % (args.workload, B)
-                if key in tj:
-                    traffic = tj[key]["hbm_bytes_per_launch"]
-            except Exception:  # noqa: BLE001
-                traffic = None
+        traffic, traffic_src = measured_traffic(args.workload, B)
         out = {
             "metric": metric,
             "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": K, "warmup": W,
-            "ms_per_step": elapsed / K * 1e3, "higher_is_better": True, "scaling": "weak",
+            "ms_per_step": elapsed / K * 1e3, "higher_is_better": True, "scaling": scaling,
             "vs_baseline": None, "dtype": "f64",
             "data": DATA[mode, multi],
-            "config": {"workload": "%s (%dx%d), %d boards per GPU, auto-reset, burn-in %d steps%s"
-                                   % (ENV_ID[args.workload], L, L, B, args.burnin,
-                                      ", episode phases staggered" if args.stagger else ""), "global_batch": world * B,
-                       "boards_per_gpu": B,
-                       "map_size": L, "parallelism": "boards sharded per GPU (dp%d)" % world},
+            "config": {"workload": "%s (%dx%d), %d boards over %d GPU(s) = %d per GPU (%s scaling; BASELINE %s), "
+                                   "auto-reset, burn-in %d steps%s"
+                                   % (ENV_ID[args.workload], L, L, global_batch, world, B, scaling, base_cfg,
+                                      args.burnin, ", episode phases staggered" if args.stagger else ""),
+                       "global_batch": global_batch, "boards_per_gpu": B,
+                       "map_size": L, "parallelism": "boards sharded per GPU (dp%d), no data-path collective" % world},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": "td_step_kernel<%d, %s>" % (L, mode.upper()), "avg_kernel_us": avg_kernel_s * 1e6,
                          "kernel_samples": len(kern_ms) * world,
                          "algorithmic_bytes_per_launch": B * bpe},

@@ -57,7 +57,10 @@ def main():
     json.dump(summary, open(os.path.join(out, "%s_pmc.json" % tag), "w"), indent=1)
     tp = os.path.join(out, "pmc_traffic.json")
     tj = json.load(open(tp)) if os.path.exists(tp) else {}
-    tj["%s_B%d" % (wl, B)] = {"hbm_bytes_per_launch": fetch + write, "read": fetch, "write": write, "round": rnd}
+    sys.path.insert(0, HERE)
+    import bench  # noqa: E402  (the kernel-source hash bench.py checks before quoting this record)
+    tj["%s_B%d" % (wl, B)] = {"hbm_bytes_per_launch": fetch + write, "read": fetch, "write": write, "round": rnd,
+                              "kernel_src": bench.kernel_source_hash()}
     json.dump(tj, open(tp, "w"), indent=1)
     print(json.dumps({k: summary[k] for k in ("hbm_read_bytes_per_launch", "hbm_write_bytes_per_launch", "per_board")}))
 
