@@ -57,6 +57,7 @@ constexpr int kSideStreams = 2;  // refill streams: one stuck on a long draw doe
 struct td_handle {
   int L = 0, NC = 0, B = 0, mode = 0, multi = 0, difficulty = 1, device = 0, autoreset = 1;
   int opp_np = 0;  // random_agent=False
+  int small = 0, obs_wt = 0;  // small-batch step kernel, write-through observation stores (td_kernels.h)
   int lw = 0;  // layout record words
   size_t scratch_stride = 0;
   TdDevCfg dcfg;
@@ -155,6 +156,8 @@ StepArgs base_args(td_handle* h) {
   a.B = h->B; a.L = h->L; a.mode = h->mode; a.multi = h->multi; a.difficulty = h->difficulty;
   a.autoreset = h->autoreset;
   a.opp_np = h->opp_np;
+  a.small = h->small;
+  a.obs_wt = h->obs_wt;
   a.hdr = h->d_hdr; a.en_lp = h->d_en_lp; a.en_mg = h->d_en_mg; a.en_inf = h->d_en_inf;
   a.tw_cd = h->d_tw_cd; a.tw_inf = h->d_tw_inf; a.cells = h->d_cells; a.opp_mt = h->d_opp; a.opp_hot = h->d_hot;
   a.np_mt = h->d_np; a.nxt = h->d_nxt; a.scratch = h->d_scratch; a.scratch_stride = h->scratch_stride;
@@ -336,6 +339,19 @@ td_handle* td_create(const td_config* cfg, int map_size, int n_boards, int mode,
     if (hipStreamCreateWithFlags(&h->side[q], hipStreamNonBlocking) != hipSuccess) rc = fail("side stream");
   if (!rc && hipEventCreateWithFlags(&h->ev_main, hipEventDisableTiming) != hipSuccess) rc = fail("event");
   if (rc) { std::string e = g_err; td_destroy(h); g_err = e; return nullptr; }
+  {  // the small-batch kernel where the whole batch is one round of waves, and
+     // write-through observation stores where the batch's observation fits the 256-MiB
+     // Infinity Cache (TD_SMALL / TD_OBS_WT = 0|1 override, for A/B runs)
+    int cus = 0;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+    const int resident = step_resident_boards(base_args(h), cus);
+    const double obs_bytes = (double)n_boards * NCH * h->NC * 4.0;
+    h->small = n_boards <= resident ? 1 : 0;
+    h->obs_wt = h->small && obs_bytes <= 192.0 * 1024 * 1024 ? 1 : 0;
+    auto ov = [](const char* name, int& v) { if (const char* e = std::getenv(name)) v = std::atoi(e) ? 1 : 0; };
+    ov("TD_SMALL", h->small);
+    ov("TD_OBS_WT", h->obs_wt);
+  }
   std::vector<uint32_t> seeds(B);
   for (size_t b = 0; b < B; ++b) seeds[b] = (uint32_t)b;
   if (td_seed(h, seeds.data(), seeds.data()) != 0) { std::string e = g_err; td_destroy(h); g_err = e; return nullptr; }

@@ -14,6 +14,8 @@ constexpr int HOT_WORDS = 12;
 struct StepArgs {
   int B, L, mode, multi, difficulty, autoreset;
   int opp_np;           // random_agent=False: the built-in opponents draw from np_mt (auto-reset off)
+  int small;            // the batch fits one round of step waves: td_step_kernel_small (td_step.hip)
+  int obs_wt;           // small kernel: observation stores write-through (the batch's obs fits the MALL)
   TdHdr* hdr;
   double* en_lp;
   double* en_mg;
@@ -60,6 +62,8 @@ struct StepArgs {
 };
 
 hipError_t launch_step(const StepArgs& a, hipStream_t s, bool reset);
+// Small-batch step-kernel workgroups (one per board) resident at once on `cus` compute units.
+int step_resident_boards(const StepArgs& a, int cus);
 // Draw staged layouts for every board whose ring has a free slot (side stream).
 hipError_t launch_refill(const StepArgs& a, hipStream_t s);
 // The built-in opponent (side 0: random_enemy_lv<level>, 1: random_tower_lv<level>)

@@ -29,8 +29,11 @@ namespace td {
 
 #ifdef TD_STAMPS
 #define STAMP(i) do { if (a.stamps && x.lane == 0) a.stamps[(size_t)b * 16 + (i)] = __builtin_amdgcn_s_memtime(); } while (0)
+// 100-MHz chip-wide clock (comparable across CUs and XCDs): wave start / end
+#define STAMP_RT(i) do { if (a.stamps && x.lane == 0) a.stamps[(size_t)b * 16 + (i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #else
 #define STAMP(i) do { } while (0)
+#define STAMP_RT(i) do { } while (0)
 #endif
 
 constexpr int MAX_KERNEL_L = 32;  // generic-L kernels: L <= 32
@@ -316,7 +319,7 @@ __device__ __forceinline__ void with_opp_rng(const StepArgs& a, int b, int lane,
 // defender operations (TDBoard.py:226-293), wave-uniform
 // ---------------------------------------------------------------------------
 template <int NC>
-__device__ void diamond(Smem<NC>& S, const Ctx& x, int cell, int delta) {
+__device__ __forceinline__ void diamond(Smem<NC>& S, const Ctx& x, int cell, int delta) {
   const int k = x.C.tower_distance, W = 2 * k + 1, L = x.L;
   const int r0 = cell / L, c0 = cell % L;
   for (int idx = x.lane; idx < W * W; idx += 64) {
@@ -333,7 +336,7 @@ __device__ void diamond(Smem<NC>& S, const Ctx& x, int cell, int delta) {
 }
 
 template <int NC>
-__device__ int tower_build(Smem<NC>& S, U& u, const Ctx& x, int t, int cell) {
+__device__ __forceinline__ int tower_build(Smem<NC>& S, U& u, const Ctx& x, int t, int cell) {
   const double price = x.C.t_price[t][0];
   if (u.cost_def < price) return FC_COST;                 // :228
   if (cw_block(S.cell[cell]) > 0) return FC_POS;          // :232
@@ -352,14 +355,14 @@ __device__ int tower_build(Smem<NC>& S, U& u, const Ctx& x, int t, int cell) {
 }
 
 template <int NC>
-__device__ int find_tower(Smem<NC>& S, const U& u, const Ctx& x, int cell) {
+__device__ __forceinline__ int find_tower(Smem<NC>& S, const U& u, const Ctx& x, int cell) {
   bool hit = x.lane < u.nt && (int)(S.tInf[x.lane] & 0xfffu) == cell;
   uint64_t m = ballot(hit);
   return m ? ctz64(m) : -1;
 }
 
 template <int NC>
-__device__ int tower_lvup(Smem<NC>& S, U& u, const Ctx& x, int cell) {
+__device__ __forceinline__ int tower_lvup(Smem<NC>& S, U& u, const Ctx& x, int cell) {
   int k = find_tower(S, u, x, cell);
   if (k < 0) return FC_TARGET;                            // :269-271
   uint32_t ti = S.tInf[k];
@@ -378,7 +381,7 @@ __device__ int tower_lvup(Smem<NC>& S, U& u, const Ctx& x, int cell) {
 }
 
 template <int NC>
-__device__ int tower_destruct(Smem<NC>& S, U& u, const Ctx& x, int cell) {
+__device__ __forceinline__ int tower_destruct(Smem<NC>& S, U& u, const Ctx& x, int cell) {
   int k = find_tower(S, u, x, cell);
   if (k < 0) return FC_TARGET;                            // :291-293
   uint32_t ti = S.tInf[k];
@@ -401,7 +404,7 @@ __device__ int tower_destruct(Smem<NC>& S, U& u, const Ctx& x, int cell) {
 }
 
 template <int NC>
-__device__ int defender_op(Smem<NC>& S, U& u, const Ctx& x, int op, int cell) {
+__device__ __forceinline__ int defender_op(Smem<NC>& S, U& u, const Ctx& x, int op, int cell) {
   if (op < 4) return tower_build(S, u, x, op, cell);
   if (op == 4) return tower_lvup(S, u, x, cell);
   return tower_destruct(S, u, x, cell);
@@ -418,7 +421,7 @@ __device__ int defender_op(Smem<NC>& S, U& u, const Ctx& x, int op, int cell) {
 // multi-action mode.  The real actions (grp[1]) go out as int64 (6, L, L) in
 // 128-B-aligned windows, like the observation.
 template <int NC>
-__device__ void defender_scan(Smem<NC>& S, U& u, const Ctx& x, const int64_t* A, int64_t* R, bool active) {
+__device__ __forceinline__ void defender_scan(Smem<NC>& S, U& u, const Ctx& x, const int64_t* A, int64_t* R, bool active) {
   const TdDevCfg& C = x.C;
   const int ncr = x.NCr, n = 6 * ncr;
   uint8_t* flag = &S.grp[0][0];
@@ -526,7 +529,7 @@ __device__ void defender_scan(Smem<NC>& S, U& u, const Ctx& x, const int64_t* A,
 // ---------------------------------------------------------------------------
 // Cluster types / real actions are packed 4 bits per slot (slot k at bits 4k..4k+3).
 template <int NC>
-__device__ int summon_cluster(Smem<NC>& S, U& u, const Ctx& x, uint32_t types, int road, uint32_t* real) {
+__device__ __forceinline__ int summon_cluster(Smem<NC>& S, U& u, const Ctx& x, uint32_t types, int road, uint32_t* real) {
   const TdDevCfg& C = x.C;
   const int lv = u.progress >= C.enemy_upgrade_at ? 1 : 0;  // :201
   const int st = u.start(road);
@@ -564,6 +567,10 @@ __device__ int summon_cluster(Smem<NC>& S, U& u, const Ctx& x, uint32_t types, i
 // ---------------------------------------------------------------------------
 // TDBoard.step (TDBoard.py:295-368) + enemy_LP statistics
 // ---------------------------------------------------------------------------
+// packed cell words (pack_obs_cells): the march direction and the distance to the end
+__device__ __forceinline__ int pk_dir(uint32_t w) { return (int)((w >> 21) & 3u); }
+__device__ __forceinline__ int pk_dist(uint32_t w) { return (int)(w >> 24); }
+
 __device__ __forceinline__ int cheb(int a, int b, int L) {
   int dr = a / L - b / L, dc = a % L - b % L;
   dr = dr < 0 ? -dr : dr;
@@ -582,7 +589,7 @@ __device__ __forceinline__ double damage(double LP, double atk, double def, bool
 }
 
 template <int NC>
-__device__ double board_step(Smem<NC>& S, U& u, const Ctx& x, const StepArgs& a, int b) {
+__device__ __forceinline__ double board_step(Smem<NC>& S, U& u, const Ctx& x, const StepArgs& a, int b) {
   const TdDevCfg& C = x.C;
   const int L = x.L, lane = x.lane;
   double reward = dadd(0.0, C.reward_time);                 // :298-299
@@ -601,7 +608,7 @@ __device__ double board_step(Smem<NC>& S, U& u, const Ctx& x, const StepArgs& a,
     lp[s] = val[s] ? S.eLP[i] : 0.0;
     mg[s] = val[s] ? S.eMg[i] : 0.0;
     inf[s] = val[s] ? S.eInf[i] : 0u;
-    key[s] = val[s] ? dsub((double)cw_dist(S.cell[en_cell(inf[s])]), mg[s]) : 0.0;
+    key[s] = val[s] ? dsub((double)pk_dist(S.cell[en_cell(inf[s])]), mg[s]) : 0.0;
   }
   int rank[2] = {0, 0};
   for (int j = 0; j < n; ++j) {  // enemy j's key from the lane that holds it
@@ -705,7 +712,7 @@ __device__ double board_step(Smem<NC>& S, U& u, const Ctx& x, const StepArgs& a,
     else mg[s] = dadd(mg[s], sp);
     while (mg[s] >= 1.0) {
       mg[s] = dsub(mg[s], 1.0);
-      const int d = cw_dir(S.cell[cell]);
+      const int d = pk_dir(S.cell[cell]);
       // map[5] codes (TDBoard.py:319): 0:+c 1:-c 2:+r 3:-r
       int r = cell / L + (d == 2) - (d == 3), c = cell % L + (d == 0) - (d == 1);
       if (r < 0 || r >= L || c < 0 || c >= L) { u.flags |= FLAG_BAD_MOVE; break; }
@@ -752,7 +759,7 @@ __device__ double board_step(Smem<NC>& S, U& u, const Ctx& x, const StepArgs& a,
 // order / count, all in numpy float32.  The first enemy of each group (its
 // "head") walks the list and owns the group's stats.
 template <int NC>
-__device__ void enemy_stats(Smem<NC>& S, const U& u, const Ctx& x) {
+__device__ __forceinline__ void enemy_stats(Smem<NC>& S, const U& u, const Ctx& x) {
   const TdDevCfg& C = x.C;
   const int n = u.n;
   if (n == 0) return;  // write_obs emits zero planes without reading grp
@@ -815,7 +822,7 @@ __device__ __forceinline__ void d9_table(Smem<NC>& S, int maxdist, int lane) {
 
 // Broadcast channels and the channel-9 table (TDBoard.py:115-142).
 template <int NC>
-__device__ void channel_scalars(Smem<NC>& S, const U& u, const Ctx& x) {
+__device__ __forceinline__ void channel_scalars(Smem<NC>& S, const U& u, const Ctx& x) {
   const TdDevCfg& C = x.C;
   const int l = x.lane;
   if (l < 48) {
@@ -858,15 +865,16 @@ __host__ __device__ constexpr int obs_kind(int ch) {
        : OK_CONST;
 }
 
-// Before the observation the cell words are replaced (in LDS) by what the planes
-// read of a cell: the binary-channel bits (cell_bits, bits 0-20) and the distance
-// to the end (bits 24-31) for channel 9.  The board's own cell words must have been
-// written back first (store_cells).
+// Once the step's actions are done (the towers and map[6] are final), the cell words
+// are replaced in LDS by what the rest of the step reads of a cell: the binary
+// observation bits (cell_bits, bits 0-20), the march direction map[5] (bits 21-22)
+// and the distance to the end map[4] (bits 24-31; channel 9 and the sort key).  The
+// board's own cell words must have been written back first (store_cells).
 template <int NC>
 __device__ __forceinline__ void pack_obs_cells(Smem<NC>& S, const Ctx& x) {
   for (int i = x.lane; i < x.NCr; i += 64) {
     const uint32_t w = S.cell[i];
-    S.cell[i] = cell_bits(w, S.twr[i]) | ((uint32_t)cw_dist(w) << 24);
+    S.cell[i] = cell_bits(w, S.twr[i]) | ((uint32_t)cw_dir(w) << 21) | ((uint32_t)cw_dist(w) << 24);
   }
   __syncthreads();
 }
@@ -967,6 +975,124 @@ __device__ __forceinline__ void write_obs(const Smem<NC>& S, const Ctx& x, float
   }
 }
 
+// Channel classes of the observation as 64-bit channel masks (TDBoard.get_states,
+// :112-143): bits of the packed cell word, the enemy_LP planes, channel 9 (distance
+// by table), and the broadcast channels.
+constexpr uint64_t kChBin = kBinaryChannels;
+constexpr uint64_t kChD9 = 1ull << 9;
+constexpr uint64_t kChEnemy = 0xFFFFull << 25;
+constexpr uint64_t kChAll = (1ull << NCH) - 1;
+constexpr uint64_t kChConst = kChAll & ~(kChBin | kChD9 | kChEnemy);
+
+// The (45, L, L) float32 observation of one board for compile-time L, into a
+// 16-B-aligned buffer: the 128-B-aligned 1-KB windows of write_obs (store k covers
+// stream units [A + 64k, A + 64k + 64), A = the board's first unit rounded down to a
+// line), software-pipelined.  For G windows at a time every lane first issues its
+// two LDS reads -- the 16-B packed cell quad and one word that is the broadcast value
+// (chv) or the enemy group quad (grp) -- then the windows are computed and stored.
+// The window's channel mix is wave-uniform (SALU): a window of one class takes a
+// short path, the per-cell tables (channel 9, enemy stats) are read only where the
+// window holds such channels.  Stores are buffer stores whose lanes outside the board
+// get an out-of-range offset: the hardware drops them, so no lane is masked off by a
+// branch.  wt: every line write-through (sc1) instead of non-temporal, where the
+// batch's observation fits the 256-MiB Infinity Cache (scripts/storepol.hip at 8,192
+// boards, 147 MB: 21.8 us sc1, 30.0 us nt; at 65,536 boards, 1.18 GB, nt whole lines
+// are the fastest form, with the two lines shared with the neighbours sc1).
+template <int NC, int LT, int G = 4>
+__device__ __forceinline__ void write_obs_lines(const Smem<NC>& S, int lane, float* out, bool any_enemy, bool wt) {
+  static_assert(LT >= 8, "a 128-B line spans at most two channel planes");
+  constexpr int Q = LT * LT / 4, N4 = NCH * Q;
+  constexpr int K = (N4 + 7 + 63) / 64;  // windows holding units of the board
+  constexpr uint32_t OOB = 0x80000000u;  // beyond the buffer's num_records: store dropped
+  const char* const sb = reinterpret_cast<const char*>(&S);
+  const int o_cell = (int)(reinterpret_cast<const char*>(S.cell) - sb);  // packed cell words (pack_obs_cells)
+  const int o_grp = (int)(reinterpret_cast<const char*>(&S.grp[0][0]) - sb);
+  const int o_chv = (int)(reinterpret_cast<const char*>(S.chv) - sb);
+  const int o_d9 = (int)(reinterpret_cast<const char*>(S.d9) - sb);
+  const int o_gst = (int)(reinterpret_cast<const char*>(&S.gst[0][0]) - sb);
+  const int mis = (int)((reinterpret_cast<uintptr_t>(out) >> 4) & 7u);  // units of the line before the board
+  const int head = mis ? 8 - mis : 0, tail = ((N4 + mis) & ~7) - mis;   // [0, head), [tail, N4): shared lines
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(out, 0, N4 * 16, 0x00020000);
+  const int i0 = lane - mis;
+  for (int k0 = 0; k0 < K; k0 += G) {
+    uint4 A[G];
+    uint32_t W[G];
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+      const int k = k0 + j;
+      if (K % G == 0 || k < K) {
+        int i = i0 + 64 * k;
+        i = i < 0 ? 0 : (i > N4 - 1 ? N4 - 1 : i);
+        const int ch = i / Q, q = i - ch * Q;
+        const int e = ch - 25;
+        A[j] = *reinterpret_cast<const uint4*>(sb + o_cell + 16 * q);
+        // enemy plane: the cell quad's group bytes; else the channel's broadcast value
+        // (bit select: a ternary here compiled to a divergent branch)
+        const int wa = o_grp + (e & 3) * NC + 4 * q, wb = o_chv + 4 * ch, m = -(int)((unsigned)e < 16u);
+        const int wo = wb ^ ((wa ^ wb) & m);
+        W[j] = *reinterpret_cast<const uint32_t*>(sb + wo);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+      const int k = k0 + j;
+      if (!(K % G == 0 || k < K)) continue;
+      // the window's channels (wave-uniform)
+      const int ulo = 64 * k - mis, uhi = ulo + 63;
+      const int clo = (ulo < 0 ? 0 : ulo) / Q, chi = (uhi > N4 - 1 ? N4 - 1 : uhi) / Q;
+      const uint64_t chm = ((chi >= 63 ? ~0ull : ((1ull << (chi + 1)) - 1)) & ~((1ull << clo) - 1)) & kChAll;
+      const bool edge = ulo < head || uhi >= tail;  // the window holds a line shared with a neighbour
+      int i = i0 + 64 * k;
+      const int ic = i < 0 ? 0 : (i > N4 - 1 ? N4 - 1 : i);
+      const int ch = ic / Q;
+      const int e = ch - 25;
+      const bool isen = (unsigned)e < 16u, isd9 = ch == 9, isbin = ((kChBin >> ch) & 1ull) != 0;
+      const uint32_t a4[4] = {A[j].x, A[j].y, A[j].z, A[j].w};
+      float v[4];
+      if ((chm & ~kChBin) == 0) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) v[c] = (float)((a4[c] >> ch) & 1u);
+      } else if ((chm & ~kChConst) == 0) {
+        const float cv = __uint_as_float(W[j]);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) v[c] = cv;
+      } else if ((chm & ~kChEnemy) == 0 && !any_enemy) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) v[c] = 0.0f;
+      } else {
+        float t[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+        if ((chm & kChD9) != 0 || ((chm & kChEnemy) != 0 && any_enemy)) {
+          // channel 9 by distance, enemy stats by the cell's group head
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const uint32_t g = (W[j] >> (8 * c)) & 0x7fu;
+            const int to = isd9 ? o_d9 + 4 * (int)(a4[c] >> 24) : o_gst + 16 * (int)g + 4 * ((e >> 2) & 3);
+            t[c] = *reinterpret_cast<const float*>(sb + to);
+          }
+        }
+        const float cv = __uint_as_float(W[j]);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const bool grp_here = any_enemy && ((W[j] >> (8 * c)) & 0xffu) != 0xffu;
+          const float ev = grp_here ? t[c] : 0.0f;
+          const float bv = (float)((a4[c] >> (ch & 31)) & 1u);
+          v[c] = isbin ? bv : isd9 ? t[c] : isen ? ev : cv;
+        }
+      }
+      const bool shared = i < head || i >= tail;  // a line shared with a neighbouring board
+      const f32x4 val = f32x4{v[0], v[1], v[2], v[3]};
+      const uint32_t off = (uint32_t)i * 16u;  // i < 0 or i >= N4: out of range already
+      if (wt) {  // wave-uniform
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, val), rs, off, 0, 16 /* sc1 */);
+      } else {
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, val), rs, shared ? OOB : off, 0, 2 /* nt */);
+        if (edge)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, val), rs, shared ? off : OOB, 0, 16 /* sc1 */);
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // board load / reset / store
 // ---------------------------------------------------------------------------
@@ -1020,7 +1146,7 @@ __device__ __forceinline__ double lane_f64(uint32_t v, int l) {
 
 // Commit the prefetched inputs of board b into the LDS image and the scalar state.
 template <int NC>
-__device__ void load_board(Smem<NC>& S, U& u, const Ctx& x, const StepArgs& a, int b, const Prefetch& P) {
+__device__ __forceinline__ void load_board(Smem<NC>& S, U& u, const Ctx& x, const StepArgs& a, int b, const Prefetch& P) {
   const size_t eb = (size_t)b * ECAP, cb = (size_t)b * x.NCr;
   if ((x.NCr & 3) == 0) {
     // 16-B cell loads: the first 256 cells came with the prefetch, the rest (L > 16)
@@ -1031,9 +1157,9 @@ __device__ void load_board(Smem<NC>& S, U& u, const Ctx& x, const StepArgs& a, i
     constexpr int NR = (NC / 4 + 63) / 64 - 1;  // further 16-B loads per lane: 0 (L <= 16) .. 3 (NC = 1024)
     uint4 r[NR > 0 ? NR : 1];
 #pragma unroll
-    for (int k = 0; k < NR; ++k) {
+    for (int k = 0; k < NR; ++k) {  // every element assigned (clamped index): the array stays in registers
       const int i = 64 * (k + 1) + x.lane;
-      if (i < n4) r[k] = g4[i];
+      r[k] = g4[i < n4 ? i : n4 - 1];
     }
     if (x.lane < n4) s4[x.lane] = P.c4;
 #pragma unroll
@@ -1082,7 +1208,7 @@ __device__ void load_board(Smem<NC>& S, U& u, const Ctx& x, const StepArgs& a, i
 
 // Fresh board from a layout record (TDGymBasic.reset :43-53, TDBoard.__init__ :14-79).
 template <int NC>
-__device__ void reset_board(Smem<NC>& S, U& u, const Ctx& x, const uint32_t* rec) {
+__device__ __forceinline__ void reset_board(Smem<NC>& S, U& u, const Ctx& x, const uint32_t* rec) {
   const TdDevCfg& C = x.C;
   // vector loads only (lane-indexed, then readlane): a record handed over by a
   // concurrently running refill must not come through the scalar cache
@@ -1107,7 +1233,7 @@ __device__ __forceinline__ void store_cells(const Smem<NC>& S, const U& u, const
 }
 
 template <int NC>
-__device__ void store_board(const Smem<NC>& S, const U& u, const Ctx& x, const StepArgs& a, int b) {
+__device__ __forceinline__ void store_board(const Smem<NC>& S, const U& u, const Ctx& x, const StepArgs& a, int b) {
   if (x.lane == 0) {
     TdHdr h;
     h.cost_def = u.cost_def; h.cost_atk = u.cost_atk; h.ep_return = u.ep_ret;
@@ -1237,7 +1363,7 @@ __device__ __forceinline__ void opponent_tower(Smem<NC>& S, U& u, const Ctx& x, 
 
 // Attacker clusters of TD-atk (TDAttack.py:36-46) and TD-2p (TDMulti.py:199-206, 229-241).
 template <int NC, int MODE>
-__device__ void attacker_actions(Smem<NC>& S, U& u, const Ctx& x, const StepArgs& a, int b) {
+__device__ __forceinline__ void attacker_actions(Smem<NC>& S, U& u, const Ctx& x, const StepArgs& a, int b) {
   const TdDevCfg& C = x.C;
   if (x.lane < 24) {
     int64_t v = a.atk_act[(size_t)b * 24 + x.lane];
@@ -1282,12 +1408,17 @@ __device__ void attacker_actions(Smem<NC>& S, U& u, const Ctx& x, const StepArgs
 // SCAN: the multi-action defender scan is compiled in (launched only when a.multi).
 // Its 16-B staging buffers raise the 30x30 kernel from 55 to 148 VGPRs, and the
 // discrete kernel should not pay for them in occupancy.
-template <int NC, int LT, int MODE, bool SCAN>
-__device__ void step_board(Smem<NC>& S, const Ctx& x, const StepArgs& a, int b, const Prefetch& P) {
+// SMALL: the batch runs as one round of waves (td_step_kernel_small); with a.obs_wt
+// the observation lines are stored write-through (write_obs_lines).  (Storing the
+// layout and tower planes at the start of the step, before the step logic, was
+// measured slower at 4,096 and 8,192 boards: 36.3 / 53.1 vs 25.7 / 38.3 us.)
+template <int NC, int LT, int MODE, bool SCAN, bool SMALL>
+__device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const StepArgs& a, int b, const Prefetch& P) {
   const TdDevCfg& C = x.C;
   uint32_t* const opp = a.opp_mt + (size_t)b * OPP_WORDS;
   uint32_t* const hot = a.opp_hot + (size_t)b * HOT_WORDS;
   U u;
+  STAMP_RT(9);
   STAMP(0);
   load_board(S, u, x, a, b, P);
   const int64_t act_in = (int64_t)(((uint64_t)lane_word(P.w, PF_ACT + 1) << 32) | lane_word(P.w, PF_ACT));
@@ -1312,6 +1443,7 @@ __device__ void step_board(Smem<NC>& S, const Ctx& x, const StepArgs& a, int b, 
     return;
   }
   float* const obs = a.obs + (size_t)b * NCH * x.NCr;
+  const bool wt = SMALL && a.obs_wt;
 
   u.atk_cd = u.atk_cd - 1 > 0 ? u.atk_cd - 1 : 0;
   u.def_cd = u.def_cd - 1 > 0 ? u.def_cd - 1 : 0;
@@ -1347,6 +1479,11 @@ __device__ void step_board(Smem<NC>& S, const Ctx& x, const StepArgs& a, int b, 
     if (MODE == MODE_ATK)
       with_opp_rng(a, b, x.lane, R, [&](auto& G) { opponent_tower(S, u, x, G, a.difficulty); });
   }
+  // the towers and map[6] are final: cell words back to HBM if they changed, then
+  // packed for the rest of the step (board_step reads the packed direction and distance)
+  store_cells(S, u, x, a, b);
+  u.cells_dirty = false;
+  pack_obs_cells(S, x);
   // pre-draw the next step's words: loads issued now, consumed at the end of the step
   if (MODE != MODE_2P) R.prefetch_issue(x.lane);
   __syncthreads();
@@ -1403,11 +1540,10 @@ __device__ void step_board(Smem<NC>& S, const Ctx& x, const StepArgs& a, int b, 
   STAMP(5);
   enemy_stats(S, u, x);  // no-op for a board without enemies (e.g. just reset)
   channel_scalars(S, u, x);
-  store_cells(S, u, x, a, b);
-  pack_obs_cells(S, x);
-  STAMP(6);
-  write_obs<NC, LT>(S, x, obs, u.n > 0);
-  STAMP(7);
+  if (was_reset) {  // the new episode's layout
+    store_cells(S, u, x, a, b);
+    pack_obs_cells(S, x);
+  }
   store_board(S, u, x, a, b);
 
   if (MODE != MODE_2P) R.prefetch_finish(x.lane);
@@ -1438,14 +1574,29 @@ __device__ void step_board(Smem<NC>& S, const Ctx& x, const StepArgs& a, int b, 
     }
   }
   if (MODE != MODE_2P && x.lane < 8) sst(&hot[4 + x.lane], R.cache);
+  // the observation last: nothing of the step is live any more, the writer has the registers
+  STAMP(6);
+  if constexpr (LT != 0) {
+    if ((reinterpret_cast<uintptr_t>(a.obs) & 15u) == 0) {
+#ifndef TD_DIAG_NO_OBS  // diagnostic builds only: the step without its observation
+      write_obs_lines<NC, LT>(S, x.lane, obs, u.n > 0, wt);
+#endif
+    } else {
+      write_obs<NC, LT>(S, x, obs, u.n > 0);
+    }
+  } else {
+    write_obs<NC, LT>(S, x, obs, u.n > 0);
+  }
+  STAMP(7);
   STAMP(8);
+  STAMP_RT(10);
 }
 
 // One workgroup (one wave) per board.  (A persistent variant that prefetched the
 // next board while stepping the current one measured slower: its static board
 // assignment leaves a one-board tail, and the step is bound by HBM writes.)
-template <int LT, int MODE, bool SCAN>
-__global__ __launch_bounds__(64) void td_step_kernel(StepArgs a) {
+template <int LT, int MODE, bool SCAN, bool SMALL>
+__device__ __forceinline__ void step_kernel_body(const StepArgs& a) {
   constexpr int NC = LT ? LT * LT : MAX_KERNEL_L * MAX_KERNEL_L;
   __shared__ Smem<NC> S;
   const int b = blockIdx.x;
@@ -1455,7 +1606,27 @@ __global__ __launch_bounds__(64) void td_step_kernel(StepArgs a) {
   const Ctx x{S.cfg, L, L * L, (int)threadIdx.x};
   Prefetch P;
   prefetch_issue(P, a, b, x.lane, x.NCr, MODE != MODE_ATK && !a.multi);
-  step_board<NC, LT, MODE, SCAN>(S, x, a, b, P);
+  step_board<NC, LT, MODE, SCAN, SMALL>(S, x, a, b, P);
+}
+
+// Large batches (several rounds of waves, HBM-write bound): 6 waves per SIMD at
+// L = 10 (106 SGPRs), no register pressure beyond the step's own.
+template <int LT, int MODE, bool SCAN>
+__global__ __launch_bounds__(64) void td_step_kernel(StepArgs a) {
+  step_kernel_body<LT, MODE, SCAN, false>(a);
+}
+
+// Batches that fit one round of waves.  8 waves per SIMD where LDS allows it (L = 10:
+// 5,072 B per board): the compiler then keeps the kernel at <= 80 SGPRs, the gfx950
+// limit for 8 resident waves (MI355X_MICROARCH.md, residency), so 8,192 boards -- 8
+// GPUs' share of BASELINE's 65,536 -- run as ONE round instead of 6,144 + 2,048.  At
+// 65,536 boards the same build is 7 % slower (SGPR spill code), hence two kernels.
+#ifndef TD_SMALL_ATTR
+#define TD_SMALL_ATTR __attribute__((amdgpu_waves_per_eu(8, 8)))
+#endif
+template <int LT, int MODE, bool SCAN>
+__global__ __launch_bounds__(64) TD_SMALL_ATTR void td_step_kernel_small(StepArgs a) {
+  step_kernel_body<LT, MODE, SCAN, true>(a);
 }
 
 // The built-in opponents called on their own, between steps (TDGymBasic.py:81-292,
@@ -1645,7 +1816,15 @@ __global__ __launch_bounds__(64) void td_reset_kernel(StepArgs a) {
   channel_scalars(S, u, x);
   store_cells(S, u, x, a, b);
   pack_obs_cells(S, x);
-  if (a.obs) write_obs<NC, LT>(S, x, a.obs + (size_t)b * NCH * x.NCr, false);
+  if (a.obs) {
+    float* const o = a.obs + (size_t)b * NCH * x.NCr;
+    if constexpr (LT != 0) {
+      if ((reinterpret_cast<uintptr_t>(a.obs) & 15u) == 0) write_obs_lines<NC, LT>(S, x.lane, o, false, false);
+      else write_obs<NC, LT>(S, x, o, false);
+    } else {
+      write_obs<NC, LT>(S, x, o, false);
+    }
+  }
   store_board(S, u, x, a, b);
   if (x.lane == 0) {
     a.reset_fail[b] = 0;
@@ -1695,15 +1874,45 @@ __global__ __launch_bounds__(64) void td_refill_kernel(StepArgs a) {
   }
 }
 
+// The step kernel of a mode: K<LT, MODE, SCAN> for K = td_step_kernel or td_step_kernel_small.
+#define TD_STEP_DISPATCH(K, LT, a, CALL)                                   \
+  do {                                                                     \
+    if ((a).mode == MODE_DEF && (a).multi) CALL((K<LT, MODE_DEF, true>));  \
+    else if ((a).mode == MODE_DEF) CALL((K<LT, MODE_DEF, false>));         \
+    else if ((a).mode == MODE_ATK) CALL((K<LT, MODE_ATK, false>));         \
+    else if ((a).multi) CALL((K<LT, MODE_2P, true>));                      \
+    else CALL((K<LT, MODE_2P, false>));                                    \
+  } while (0)
+
 template <int LT>
 static hipError_t launch2(const StepArgs& a, hipStream_t s, bool reset) {
+#define TD_LAUNCH(k) hipLaunchKernelGGL(k, dim3(a.B), dim3(64), 0, s, a)
   if (reset) hipLaunchKernelGGL(td_reset_kernel<LT>, dim3(a.B), dim3(64), 0, s, a);
-  else if (a.mode == MODE_DEF && a.multi) hipLaunchKernelGGL((td_step_kernel<LT, MODE_DEF, true>), dim3(a.B), dim3(64), 0, s, a);
-  else if (a.mode == MODE_DEF) hipLaunchKernelGGL((td_step_kernel<LT, MODE_DEF, false>), dim3(a.B), dim3(64), 0, s, a);
-  else if (a.mode == MODE_ATK) hipLaunchKernelGGL((td_step_kernel<LT, MODE_ATK, false>), dim3(a.B), dim3(64), 0, s, a);
-  else if (a.multi) hipLaunchKernelGGL((td_step_kernel<LT, MODE_2P, true>), dim3(a.B), dim3(64), 0, s, a);
-  else hipLaunchKernelGGL((td_step_kernel<LT, MODE_2P, false>), dim3(a.B), dim3(64), 0, s, a);
+  else if (LT != 0 && a.small && (reinterpret_cast<uintptr_t>(a.obs) & 15u) == 0) TD_STEP_DISPATCH(td_step_kernel_small, LT, a, TD_LAUNCH);
+  else TD_STEP_DISPATCH(td_step_kernel, LT, a, TD_LAUNCH);
+#undef TD_LAUNCH
   return hipGetLastError();
+}
+
+// Step-kernel workgroups (boards) resident at once on the device: the batch size up
+// to which a step runs as one round of waves (td_step_kernel_small).
+template <int LT>
+static int resident3(const StepArgs& a, int cus) {
+  int n = 0;
+  hipError_t e = hipErrorInvalidValue;
+#define TD_OCC(k) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, 64, 0)
+  TD_STEP_DISPATCH(td_step_kernel_small, LT, a, TD_OCC);
+#undef TD_OCC
+  return e == hipSuccess ? n * cus : 0;
+}
+
+int step_resident_boards(const StepArgs& a, int cus) {
+  switch (a.L) {
+    case 10: return resident3<10>(a, cus);
+    case 20: return resident3<20>(a, cus);
+    case 30: return resident3<30>(a, cus);
+    default: return 0;  // generic-L kernels: no small-batch build
+  }
 }
 
 hipError_t launch_step(const StepArgs& a, hipStream_t s, bool reset) {

@@ -39,7 +39,7 @@ if fn is not None:
     fn.restype = _lib.ctypes.c_int
     fn.argtypes = [_lib.c_vp, _lib.c_vp]
     fn(eng._h, stamps.data_ptr())
-names = ["load", "actions", "sort", "towers", "march+costs", "stats+scalars", "obs", "store+out"]
+names = ["load(+early obs)", "actions", "sort", "towers", "march+costs", "stats+state+out", "obs", "-"]
 acc = np.zeros(len(names))
 t0 = time.time()
 for k in range(burn, burn + 20):
@@ -57,7 +57,18 @@ if fn is not None:
     for n, v in zip(names, acc / 20):
         print("  %-14s %10.0f cycles/wave  %5.1f%%" % (n, v, 100 * v / (tot / 20)))
     s = stamps.cpu().numpy()
-    span = (s[:, 8].max() - s[:, 0].min())
-    print("  kernel span (first start -> last end) %.0f cycles; mean wave life %.0f cycles" % (span, (s[:, 8] - s[:, 0]).mean()))
+    print("  mean wave life %.0f cycles (s_memtime)" % (s[:, 8] - s[:, 0]).mean())
+    # 100-MHz chip clock (slots 9 / 10): wave start / end offsets from the first wave's start, in us
+    st0 = s[:, 9].min()
+    start = (s[:, 9] - st0) / 100.0
+    end = (s[:, 10] - st0) / 100.0
+    life = end - start
+    pct = lambda v: " ".join("p%d=%.2f" % (q, np.percentile(v, q)) for q in (0, 10, 50, 90, 99, 100))
+    print("  rt start us: " + pct(start))
+    print("  rt end   us: " + pct(end))
+    print("  rt life  us: " + pct(life))
+    print("  rt span us: %.2f (first wave start -> last wave end)" % end.max())
+    # cycles per realtime tick (shader clock estimate)
+    print("  shader clock ~ %.0f MHz" % (100.0 * (s[:, 8] - s[:, 0]).sum() / max(1, (s[:, 10] - s[:, 9]).sum())))
     st = eng.export_state(0, min(B, 4096))
     print("  mean enemies %.2f towers %.2f steps %.0f" % (st["hdr"]["n_en"].mean(), st["hdr"]["n_tw"].mean(), st["hdr"]["steps"].mean()))
