@@ -27,7 +27,9 @@ MAX and the episode-stat gather after the timed region (RCCL on GPUs).
 
 One JSON line on rank 0: metric/value/unit (the metric string, ``global_batch``,
 ``boards_per_gpu`` and ``scaling`` follow what actually ran), ``roofline`` for
-the step kernel (HIP events on the launch stream, algorithmic bytes per launch;
+the step kernel (its average duration from HIP timing events bound to every timed
+launch's own dispatch on the launch stream -- the timestamps rocprofv3's kernel
+trace reports -- and the algorithmic bytes per launch;
 ``traffic`` is the PMC-measured HBM bytes per launch of the same kernel build at
 the same boards per GPU, with its source, or null) and ``cpu_baseline`` (the C
 restatement oracle/td_cpu.c on this host's cores, rank 0, N=1;
@@ -65,7 +67,7 @@ DATA = {("def", False): "synthetic: uniform random defender actions, built-in lv
         ("2p", True): "synthetic: defender flags uniform in {0,1,2} (6,L,L), attacker clusters uniform in {0..4} (3,8), "
                       "seeded boards"}
 N_ACTION_BUFS = 8
-EVENT_EVERY = 4  # timed steps per sampled kernel duration
+EVENT_EVERY = 8  # timed steps per sampled kernel duration (an event pair per launch costs ~10 % of the step rate at 8,192 boards)
 FLAG_BITS = (("enemy_overflow", 1), ("tower_overflow", 2), ("bad_action", 4), ("no_layout", 8), ("bad_move", 16))  # distinct pre-drawn action batches cycled through the timed steps (multi-action shapes)
 
 
@@ -214,6 +216,13 @@ def main():
     ap.add_argument("--py-cpu-seconds", type=float, default=5.0, help="Python restatement leg (0 = skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--autoreset", type=int, default=1, help="diagnostic: 0 keeps finished boards stepping (not the metric)")
+    ap.add_argument("--timing", default="dispatch", choices=("dispatch", "marker", "none"),
+                    help="step-kernel durations: 'dispatch' = events bound to every %d-th timed launch "
+                         "(td_kernel_timing, the dispatch-packet timestamps rocprofv3 reports); 'marker' = torch "
+                         "event pairs around every %d-th launch (adds the marker packets' overhead); 'none' = "
+                         "no kernel timing (diagnostic A/B of the step rate)" % (EVENT_EVERY, EVENT_EVERY))
+    ap.add_argument("--refill-interval", type=int, default=None,
+                    help="diagnostic: steps between layout-refill launches in the timed region (0 = none)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -282,9 +291,13 @@ def main():
     # HIP events bracket every EVENT_EVERY-th step kernel on its stream: the kernel's
     # duration is sampled live over the timed region without a timing event pair
     # (and its cache flush) behind every launch
-    sampled = set(range(0, K, EVENT_EVERY))
+    sampled = set(range(0, K, EVENT_EVERY)) if args.timing == "marker" else set()
     ev = {k: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for k in sampled}
     eng.episode_stats(clear=True)  # the device accumulates finished episodes of the timed steps
+    if args.refill_interval is not None:
+        eng.set_refill_interval(args.refill_interval)
+    if args.timing == "dispatch":
+        eng.kernel_timing((K + EVENT_EVERY - 1) // EVENT_EVERY, EVENT_EVERY)  # timestamped by their own dispatch
 
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -304,7 +317,13 @@ def main():
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
 
-    kern_ms = [s.elapsed_time(e) for s, e in ev.values()]
+    if args.timing == "dispatch":
+        kern_ms = (eng.kernel_times().astype(np.float64) / 1e3).tolist()
+        eng.kernel_timing(0)
+    elif args.timing == "marker":
+        kern_ms = [s.elapsed_time(e) for s, e in ev.values()]
+    else:
+        kern_ms = [float("nan")]
     avg_kernel_s = float(np.mean(kern_ms)) / 1e3
     # after timing: MAX of the clocks over ranks, and the episode statistics of the
     # timed steps gathered to rank 0 (the only exchange; RCCL on GPUs)
@@ -337,6 +356,10 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": "td_step_kernel<%d, %s>" % (L, mode.upper()), "avg_kernel_us": avg_kernel_s * 1e6,
                          "kernel_samples": len(kern_ms) * world,
+                         "kernel_timing": {"dispatch": "dispatch-packet timestamps of every %dth timed launch "
+                                                       "(td_kernel_timing)" % EVENT_EVERY,
+                                           "marker": "torch event pairs around every %dth launch" % EVENT_EVERY,
+                                           "none": "not timed"}[args.timing],
                          "algorithmic_bytes_per_launch": B * bpe},
             "board_flags_nonzero": int((flags != 0).sum()),
             "board_flags": {name: int(((flags & bit) != 0).sum()) for name, bit in FLAG_BITS if ((flags & bit) != 0).any()},

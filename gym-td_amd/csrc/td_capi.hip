@@ -4,6 +4,7 @@
 // (layouts: numpy-legacy MT19937; built-in opponent: CPython MT19937) and the
 // staged next-episode layout.  Layouts are generated on the device
 // (td_refill_kernel / td_reset_kernel), so the step loop has no host work.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -43,12 +44,12 @@ int fail(const char* fmt, ...) {
     if (e_ != hipSuccess) return fail("%s: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, __LINE__); \
   } while (0)
 
-// Steps between refill launches.  At 65,536 boards every 4th step and every 16th
-// step per-step times are within 0.5 % (227.6 vs 228.5 us, 2,000 steps, no ring dry).
-#ifndef TD_REFILL_EVERY
-#define TD_REFILL_EVERY 4
-#endif
-inline int refill_every(int) { return TD_REFILL_EVERY; }
+// Steps between refill launches (td_set_refill_interval).  At 65,536 boards every 4th
+// step and every 16th step per-step times are within 0.5 % (227.6 vs 228.5 us, 2,000
+// steps, no ring dry).
+constexpr int kRefillEvery = 4;
+constexpr int kRefillWaves = 1024;
+constexpr int kWalksPerStep = 12;  // a pending draw advances 12 walks per step of refill interval (48 at 4)
 constexpr int kSideStreams = 2;  // refill streams: one stuck on a long draw does not stall the next (the HIP
                                  // runtime has 4 hardware queues per process; the step stream needs one)
 
@@ -80,6 +81,13 @@ struct td_handle {
   hipStream_t side[kSideStreams] = {};
   hipEvent_t ev_main = nullptr;
   int next_side = 0;
+  int refill_every = kRefillEvery;  // 0: no refill launches (td_set_refill_interval)
+  int refill_waves = kRefillWaves;  // waves per refill launch
+  int refill_nowait = 0, n_side = kSideStreams;  // A/B knobs (TD_REFILL_NOWAIT, TD_SIDE_STREAMS)
+  // td_kernel_timing: event pairs bound to the next `tev_cap` step-kernel dispatches
+  std::vector<hipEvent_t> tev;
+  int tev_cap = 0, tev_n = 0, tev_every = 1;
+  long long tev_from = 0;  // h->steps when td_kernel_timing was called
   long long steps = 0;
   std::vector<int32_t> last_reset_failed;
 };
@@ -163,6 +171,8 @@ StepArgs base_args(td_handle* h) {
   a.np_mt = h->d_np; a.nxt = h->d_nxt; a.scratch = h->d_scratch; a.scratch_stride = h->scratch_stride;
   a.lay_head = h->d_lay_head; a.lay_tail = h->d_lay_tail; a.lay_claim = h->d_lay_claim;
   a.slot_words = slot_words(h->L);
+  a.refill_grp = refill_group(h->B, h->refill_waves);
+  a.refill_walks = kWalksPerStep * (h->refill_every > 0 ? h->refill_every : kRefillEvery);
   a.reset_fail = h->d_fail; a.cfg = h->d_cfg;
   return a;
 }
@@ -211,10 +221,12 @@ int drop_all_staged(td_handle* h) {
 int start_refill(td_handle* h, hipStream_t s) {
   const int q = h->next_side;
   StepArgs a = base_args(h);
-  HIP_OK(hipEventRecord(h->ev_main, s));
-  HIP_OK(hipStreamWaitEvent(h->side[q], h->ev_main, 0));
+  if (!h->refill_nowait) {
+    HIP_OK(hipEventRecord(h->ev_main, s));
+    HIP_OK(hipStreamWaitEvent(h->side[q], h->ev_main, 0));
+  }
   HIP_OK(launch_refill(a, h->side[q]));
-  h->next_side = (q + 1) % kSideStreams;
+  h->next_side = (q + 1) % h->n_side;
   return 0;
 }
 
@@ -335,8 +347,29 @@ td_handle* td_create(const td_config* cfg, int map_size, int n_boards, int mode,
       rc = fail("episode records init");
   }
   if (!rc && hipMemcpy(h->d_cfg, &h->dcfg, sizeof(TdDevCfg), hipMemcpyHostToDevice) != hipSuccess) rc = fail("cfg upload");
-  for (int q = 0; q < kSideStreams && !rc; ++q)
-    if (hipStreamCreateWithFlags(&h->side[q], hipStreamNonBlocking) != hipSuccess) rc = fail("side stream");
+  // Side streams (layout refills): TD_SIDE_PRIO=1 creates them at the device's least
+  // priority, TD_SIDE_CUS=n restricts them to n CUs (A/B knobs; default: plain streams).
+  {
+    const char* ep = std::getenv("TD_SIDE_PRIO");
+    const char* ec = std::getenv("TD_SIDE_CUS");
+    const int ncu = ec ? std::atoi(ec) : 0;
+    int least = 0, greatest = 0;
+    (void)hipDeviceGetStreamPriorityRange(&least, &greatest);
+    for (int q = 0; q < kSideStreams && !rc; ++q) {
+      hipError_t e;
+      if (ncu > 0) {
+        std::vector<uint32_t> mask(16, 0u);
+        // spread the CUs over the mask (the bit order interleaves XCDs / SEs)
+        for (int i = 0; i < ncu && i < 512; ++i) { const int bit = (i * 37) % 256; mask[bit / 32] |= 1u << (bit % 32); }
+        e = hipExtStreamCreateWithCUMask(&h->side[q], 8, mask.data());
+      } else if (ep && std::atoi(ep)) {
+        e = hipStreamCreateWithPriority(&h->side[q], hipStreamNonBlocking, least);
+      } else {
+        e = hipStreamCreateWithFlags(&h->side[q], hipStreamNonBlocking);
+      }
+      if (e != hipSuccess) rc = fail("side stream: %s", hipGetErrorString(e));
+    }
+  }
   if (!rc && hipEventCreateWithFlags(&h->ev_main, hipEventDisableTiming) != hipSuccess) rc = fail("event");
   if (rc) { std::string e = g_err; td_destroy(h); g_err = e; return nullptr; }
   {  // the small-batch kernel where the whole batch is one round of waves, and
@@ -351,6 +384,10 @@ td_handle* td_create(const td_config* cfg, int map_size, int n_boards, int mode,
     auto ov = [](const char* name, int& v) { if (const char* e = std::getenv(name)) v = std::atoi(e) ? 1 : 0; };
     ov("TD_SMALL", h->small);
     ov("TD_OBS_WT", h->obs_wt);
+    if (const char* e = std::getenv("TD_REFILL_EVERY")) h->refill_every = std::max(0, std::atoi(e));  // A/B runs
+    if (const char* e = std::getenv("TD_REFILL_WAVES")) h->refill_waves = std::max(1, std::atoi(e));
+    if (const char* e = std::getenv("TD_REFILL_NOWAIT")) h->refill_nowait = std::atoi(e) ? 1 : 0;
+    if (const char* e = std::getenv("TD_SIDE_STREAMS")) h->n_side = std::min(kSideStreams, std::max(1, std::atoi(e)));
   }
   std::vector<uint32_t> seeds(B);
   for (size_t b = 0; b < B; ++b) seeds[b] = (uint32_t)b;
@@ -368,6 +405,7 @@ void td_destroy(td_handle* h) {
   for (void* p : dptrs)
     if (p) (void)hipFree(p);
   if (h->ev_main) (void)hipEventDestroy(h->ev_main);
+  for (hipEvent_t e : h->tev) (void)hipEventDestroy(e);
   for (int q = 0; q < kSideStreams; ++q)
     if (h->side[q]) (void)hipStreamDestroy(h->side[q]);
   delete h;
@@ -539,10 +577,49 @@ int td_step(td_handle* h, const td_step_io* io, void* stream) {
   a.last_ep = h->d_lastep;
   // the refill goes first: it waits for the previous step only, so a board whose ring
   // is dry in this step can wait for it (td_step.hip step_board) without a cycle
-  if (h->autoreset && (h->steps % refill_every(h->B)) == 0 && start_refill(h, s)) return -1;
-  HIP_OK(launch_step(a, s, false));
+  if (h->autoreset && h->refill_every > 0 && (h->steps % h->refill_every) == 0 && start_refill(h, s)) return -1;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (h->tev_n < h->tev_cap && (h->steps - h->tev_from) % h->tev_every == 0) {
+    e0 = h->tev[2 * (size_t)h->tev_n];
+    e1 = h->tev[2 * (size_t)h->tev_n + 1];
+    h->tev_n += 1;
+  }
+  HIP_OK(launch_step(a, s, false, e0, e1));
   h->steps += 1;
   return 0;
+}
+
+int td_set_refill_interval(td_handle* h, int steps) {
+  if (!h || steps < 0) return fail("td_set_refill_interval: bad arguments");
+  h->refill_every = steps;
+  return 0;
+}
+
+int td_kernel_timing(td_handle* h, int max_launches, int every) {
+  if (!h || max_launches < 0 || every < 1) return fail("td_kernel_timing: bad arguments");
+  HIP_OK(hipDeviceSynchronize());
+  while ((int)h->tev.size() < 2 * max_launches) {
+    hipEvent_t e = nullptr;
+    HIP_OK(hipEventCreate(&e));
+    h->tev.push_back(e);
+  }
+  h->tev_cap = max_launches;
+  h->tev_n = 0;
+  h->tev_every = every;
+  h->tev_from = h->steps;
+  return 0;
+}
+
+int td_kernel_times(td_handle* h, float* us, int cap) {
+  if (!h || (cap > 0 && !us)) return fail("td_kernel_times: bad arguments");
+  const int n = h->tev_n;
+  for (int i = 0; i < n && i < cap; ++i) {
+    HIP_OK(hipEventSynchronize(h->tev[2 * (size_t)i + 1]));
+    float ms = 0.0f;
+    HIP_OK(hipEventElapsedTime(&ms, h->tev[2 * (size_t)i], h->tev[2 * (size_t)i + 1]));
+    us[i] = ms * 1000.0f;
+  }
+  return n;
 }
 
 int td_episode_stats(td_handle* h, double* dev_out, int clear, void* stream) {

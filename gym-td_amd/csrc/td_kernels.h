@@ -36,6 +36,8 @@ struct StepArgs {
   uint32_t* lay_tail;   // [B]
   uint32_t* lay_claim;  // [B] 1 while a refill wave draws the board's layouts
   int slot_words;
+  int refill_grp;       // boards scanned per refill wave (refill_group)
+  int refill_walks;     // walks per board per refill launch (a draw resumes in the next launch)
   uint8_t* scratch;     // [B][scratch_stride] a pending layout draw: RoadResume header + generator arrays
   size_t scratch_stride;
   uint8_t* reset_fail;  // [B] reset kernel: road generation failed (board left unchanged)
@@ -61,7 +63,8 @@ struct StepArgs {
   const uint8_t* reset_mask;  // reset kernel only (nullptr = all boards)
 };
 
-hipError_t launch_step(const StepArgs& a, hipStream_t s, bool reset);
+// ev0 / ev1: optional timing events bound to the step kernel's dispatch (td_kernel_timing).
+hipError_t launch_step(const StepArgs& a, hipStream_t s, bool reset, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
 // Small-batch step-kernel workgroups (one per board) resident at once on `cus` compute units.
 int step_resident_boards(const StepArgs& a, int cus);
 // Draw staged layouts for every board whose ring has a free slot (side stream).
@@ -73,20 +76,16 @@ hipError_t launch_opponent(const StepArgs& a, int side, int level, hipStream_t s
 constexpr int NSLOT = 4;  // staged layouts per board: four episodes of slack for the refill
 __host__ __device__ inline uint32_t slot_tag(uint32_t n) { return 0x80000000u | (n & 0x7fffffffu); }
 __host__ __device__ inline int slot_words(int L) { return (8 + L * L + 31) & ~31; }
-// Boards scanned per refill wave: one wave per board up to 4,096 boards, at most
-// 4,096 waves above (16 boards per wave at 65,536), so a board in need rarely
-// queues behind another board's draw in the same wave.
-#ifndef TD_REFILL_WAVES
-#define TD_REFILL_WAVES 1024
-#endif
-__host__ __device__ inline int refill_group(int B) {
-  const int g = (B + TD_REFILL_WAVES - 1) / TD_REFILL_WAVES;
+// Boards scanned per refill wave when a refill launch has `waves` waves (at most 64:
+// one ballot per wave).
+__host__ __device__ inline int refill_group(int B, int waves) {
+  const int g = (B + waves - 1) / waves;
   return g < 1 ? 1 : (g > 64 ? 64 : g);
 }
 
 constexpr int kRoadAttempts = 1000;  // bound of each create_road_v2 retry loop (reference: unbounded)
 constexpr int kLayoutRetries = 64;   // auto-reset: failing draws skipped before giving up
-constexpr int kRefillWalks = 48;     // walks per board per refill launch (a draw resumes in the next launch)
+
 constexpr uint64_t kTakeSpinTicks = 100000000ull;  // 1 s of the 100-MHz clock: longest wait for a refill wave
 
 }  // namespace td

@@ -18,6 +18,8 @@
 // Python/numpy rounding order matters.
 #include <hip/hip_runtime.h>
 
+#include <hip/hip_ext.h>
+
 #include "td_kernels.h"
 #include "td_layout.h"
 #include "td_rng.h"
@@ -1601,6 +1603,9 @@ __device__ __forceinline__ void step_kernel_body(const StepArgs& a) {
   __shared__ Smem<NC> S;
   const int b = blockIdx.x;
   if (b >= a.B) return;
+#ifdef TD_STEP_PRIO  // A/B builds: step waves ahead of concurrent refill waves in issue arbitration
+  __builtin_amdgcn_s_setprio(TD_STEP_PRIO);
+#endif
   stage_cfg(S, a.cfg);
   const int L = LT ? LT : a.L;
   const Ctx x{S.cfg, L, L * L, (int)threadIdx.x};
@@ -1706,7 +1711,7 @@ struct LayoutSmem {
 // -- the RoadResume header, then the generator's arrays -- with the partial record
 // in the ring slot (its tag still the old one) and the stream position in np_mt.
 // The next refill continues it draw for draw.  So a refill launch runs at most
-// ~kRefillWalks walks per board -- except for a board whose ring is empty, whose
+// ~a.refill_walks walks per board -- except for a board whose ring is empty, whose
 // draw runs to the end at once (rare: the initial fill, or episodes shorter than the
 // refill can follow).
 __device__ __forceinline__ RoadResume* resume_hdr(const StepArgs& a, int b) {
@@ -1842,7 +1847,7 @@ __global__ __launch_bounds__(64) void td_refill_kernel(StepArgs a) {
   constexpr int NC = LT ? LT * LT : MAX_KERNEL_L * MAX_KERNEL_L;
   __shared__ LayoutSmem<NC> G;
   const int lane = (int)threadIdx.x;
-  const int grp = refill_group(a.B);
+  const int grp = a.refill_grp;
   for (int base = (int)blockIdx.x * grp; base < a.B; base += (int)gridDim.x * grp) {
     const int b = base + lane;
     const bool mine = lane < grp && b < a.B;
@@ -1862,8 +1867,8 @@ __global__ __launch_bounds__(64) void td_refill_kernel(StepArgs a) {
       while (t - h < (uint32_t)NSLOT) {
         uint32_t* slot = a.nxt + ((size_t)bb * NSLOT + t % NSLOT) * a.slot_words;
         // an empty ring is urgent (the board needs this layout at its next episode end):
-        // its draw runs to the end; otherwise at most kRefillWalks walks this launch
-        const int st = wave_layout(G, a, bb, kLayoutRetries, slot, t, t == h ? 0x7fffffff : kRefillWalks);
+        // its draw runs to the end; otherwise at most a.refill_walks walks this launch
+        const int st = wave_layout(G, a, bb, kLayoutRetries, slot, t, t == h ? 0x7fffffff : a.refill_walks);
         __syncthreads();
         if (st != ROAD_OK) break;  // out of walks (continued next launch), or 65 failing draws in a row
         ++t;
@@ -1884,9 +1889,16 @@ __global__ __launch_bounds__(64) void td_refill_kernel(StepArgs a) {
     else CALL((K<LT, MODE_2P, false>));                                    \
   } while (0)
 
+// ev0 / ev1 (optional): timing events bound to the step kernel's own dispatch
+// (hipExtLaunchKernelGGL), so their interval is the kernel's start-to-end as the
+// dispatch packet timestamps it -- no marker packets around the launch.
 template <int LT>
-static hipError_t launch2(const StepArgs& a, hipStream_t s, bool reset) {
-#define TD_LAUNCH(k) hipLaunchKernelGGL(k, dim3(a.B), dim3(64), 0, s, a)
+static hipError_t launch2(const StepArgs& a, hipStream_t s, bool reset, hipEvent_t ev0, hipEvent_t ev1) {
+#define TD_LAUNCH(k)                                                                    \
+  do {                                                                                  \
+    if (ev0) hipExtLaunchKernelGGL(k, dim3(a.B), dim3(64), 0, s, ev0, ev1, 0, a);       \
+    else hipLaunchKernelGGL(k, dim3(a.B), dim3(64), 0, s, a);                           \
+  } while (0)
   if (reset) hipLaunchKernelGGL(td_reset_kernel<LT>, dim3(a.B), dim3(64), 0, s, a);
   else if (LT != 0 && a.small && (reinterpret_cast<uintptr_t>(a.obs) & 15u) == 0) TD_STEP_DISPATCH(td_step_kernel_small, LT, a, TD_LAUNCH);
   else TD_STEP_DISPATCH(td_step_kernel, LT, a, TD_LAUNCH);
@@ -1915,18 +1927,18 @@ int step_resident_boards(const StepArgs& a, int cus) {
   }
 }
 
-hipError_t launch_step(const StepArgs& a, hipStream_t s, bool reset) {
+hipError_t launch_step(const StepArgs& a, hipStream_t s, bool reset, hipEvent_t ev0, hipEvent_t ev1) {
   switch (a.L) {
-    case 10: return launch2<10>(a, s, reset);
-    case 20: return launch2<20>(a, s, reset);
-    case 30: return launch2<30>(a, s, reset);
-    default: return launch2<0>(a, s, reset);
+    case 10: return launch2<10>(a, s, reset, ev0, ev1);
+    case 20: return launch2<20>(a, s, reset, ev0, ev1);
+    case 30: return launch2<30>(a, s, reset, ev0, ev1);
+    default: return launch2<0>(a, s, reset, ev0, ev1);
   }
 }
 
 template <int LT>
 static void launch_refill2(const StepArgs& a, hipStream_t s) {
-  const int grp = refill_group(a.B);
+  const int grp = a.refill_grp;
   const int waves = (a.B + grp - 1) / grp;
   hipLaunchKernelGGL(td_refill_kernel<LT>, dim3(waves), dim3(64), 0, s, a);
 }

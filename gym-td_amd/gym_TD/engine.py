@@ -285,6 +285,24 @@ class TDEngine(object):
         _lib.check(_lib.lib.td_opponent(self._h, {"enemy": 0, "tower": 1}[side], int(level),
                                         _lib.ptr(m, _lib.ctypes.c_uint8) if m is not None else None, self._stream()))
 
+    def set_refill_interval(self, steps):
+        """Steps between layout-refill launches (auto-reset; 0 = none, rings only drain)."""
+        _lib.check(_lib.lib.td_set_refill_interval(self._h, int(steps)))
+
+    def kernel_timing(self, max_launches, every=1):
+        """Time the step kernels of every ``every``-th step from now, ``max_launches`` of
+        them, from their dispatch timestamps (events bound to the launch itself); read
+        them with kernel_times()."""
+        _lib.check(_lib.lib.td_kernel_timing(self._h, int(max_launches), int(every)))
+
+    def kernel_times(self):
+        """Durations (microseconds, numpy float32) of the step kernels timed since kernel_timing()."""
+        cap = 1 << 20
+        n = _lib.check(_lib.lib.td_kernel_times(self._h, None, 0))
+        out = np.zeros(max(n, 1), dtype=np.float32)
+        n = _lib.check(_lib.lib.td_kernel_times(self._h, _lib.ptr(out, _lib.ctypes.c_float), min(n, cap)))
+        return out[:n]
+
     def flags(self):
         f = np.zeros(self.B, dtype=np.int32)
         _lib.check(_lib.lib.td_get_flags(self._h, _lib.ptr(f, _lib.ctypes.c_int32)))

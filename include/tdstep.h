@@ -145,6 +145,18 @@ int td_reset_layouts(td_handle* h, const uint32_t* recs, const int32_t* boards, 
  * per-element one (same bytes, slower). */
 int td_step(td_handle* h, const td_step_io* io, void* stream);
 
+/* Steps between launches of the layout refill kernel on the side streams (auto-reset;
+ * default 4, 0 = none: the staged rings then only drain).  A tuning / diagnostic knob. */
+int td_set_refill_interval(td_handle* h, int steps);
+
+/* Kernel timing: every `every`-th td_step call from now on, up to max_launches of them,
+ * binds a pair of timing events to its step kernel's own dispatch (hipExtLaunchKernel;
+ * no marker packets); max_launches = 0 turns it off.  td_kernel_times waits for them
+ * and writes each kernel's start-to-end duration in microseconds (the dispatch-packet
+ * timestamps rocprofv3 reports); returns the count. */
+int td_kernel_timing(td_handle* h, int max_launches, int every);
+int td_kernel_times(td_handle* h, float* us, int cap);
+
 /* Episodes finished by td_step since the last clear (SURVEY.md §8(b) td_episode_stats):
  * dev_out[0] = count, dev_out[1] = sum of their returns (f64, device memory, asynchronous
  * on `stream`; the sum is accumulated with atomics, so its rounding order is unspecified).
