@@ -237,7 +237,7 @@ int run_reset(td_handle* h, const std::vector<uint8_t>& mask, float* obs, hipStr
   a.obs = obs;
   a.reset_mask = h->d_mask;
   HIP_OK(launch_step(a, s, true));
-  if (h->autoreset && start_refill(h, s)) return -1;
+  if (h->autoreset && !h->opp_np && start_refill(h, s)) return -1;
   HIP_OK(hipDeviceSynchronize());
   return 0;
 }
@@ -420,20 +420,35 @@ int td_set_config(td_handle* h, const td_config* cfg) {
   return 0;
 }
 
+// Both mode setters first wait for the device: a refill may still be drawing on a side
+// stream.  Layouts staged so far stay valid for random_agent=True (they are the stream's
+// next layouts, in order), so turning auto-reset off keeps them for explicit resets.
 int td_set_autoreset(td_handle* h, int on) {
   if (!h) return fail("NULL handle");
-  if (on && h->opp_np)
-    return fail("auto-reset needs random_agent=True: with random_agent=False the opponents draw from the "
-                "layout stream, which auto-reset draws ahead of play");
+  HIP_OK(hipDeviceSynchronize());
   h->autoreset = on ? 1 : 0;
   return 0;
 }
 
+// random_agent=False interleaves the opponent's draws with the layout draws on one
+// stream, so no layout may have been drawn ahead of play: refused while any board has a
+// staged layout or a pending draw (td_seed with new numpy seeds, or running the staged
+// layouts out with explicit resets, clears them).
 int td_set_random_agent(td_handle* h, int random_agent) {
   if (!h) return fail("NULL handle");
-  if (!random_agent && h->autoreset)
-    return fail("random_agent=False needs auto-reset off (td_set_autoreset(h, 0) first): the opponents then "
-                "draw from the layout stream, which auto-reset draws ahead of play");
+  HIP_OK(hipDeviceSynchronize());
+  if (!random_agent && !h->opp_np) {
+    std::vector<uint32_t> head((size_t)h->B), tail((size_t)h->B);
+    HIP_OK(hipMemcpy(head.data(), h->d_lay_head, (size_t)h->B * 4, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(tail.data(), h->d_lay_tail, (size_t)h->B * 4, hipMemcpyDeviceToHost));
+    std::vector<RoadResume> res((size_t)h->B);
+    HIP_OK(hipMemcpy2D(res.data(), sizeof(RoadResume), h->d_scratch, h->scratch_stride, sizeof(RoadResume),
+                       (size_t)h->B, hipMemcpyDeviceToHost));
+    for (int b = 0; b < h->B; ++b)
+      if (head[(size_t)b] != tail[(size_t)b] || res[(size_t)b].phase != RP_NEW)
+        return fail("random_agent=False: board %d has layouts drawn ahead of play (auto-reset refills); "
+                    "set it before the first reset, or re-seed the layout streams first", b);
+  }
   h->opp_np = random_agent ? 0 : 1;
   return 0;
 }
@@ -577,7 +592,11 @@ int td_step(td_handle* h, const td_step_io* io, void* stream) {
   a.last_ep = h->d_lastep;
   // the refill goes first: it waits for the previous step only, so a board whose ring
   // is dry in this step can wait for it (td_step.hip step_board) without a cycle
-  if (h->autoreset && h->refill_every > 0 && (h->steps % h->refill_every) == 0 && start_refill(h, s)) return -1;
+  // random_agent=True: layouts are staged ahead by refills on the side streams.
+  // random_agent=False: they are drawn in stream order right after the step (below).
+  if (h->autoreset && !h->opp_np && h->refill_every > 0 && (h->steps % h->refill_every) == 0 &&
+      start_refill(h, s))
+    return -1;
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (h->tev_n < h->tev_cap && (h->steps - h->tev_from) % h->tev_every == 0) {
     e0 = h->tev[2 * (size_t)h->tev_n];
@@ -585,6 +604,7 @@ int td_step(td_handle* h, const td_step_io* io, void* stream) {
     h->tev_n += 1;
   }
   HIP_OK(launch_step(a, s, false, e0, e1));
+  if (h->autoreset && h->opp_np) HIP_OK(launch_autoreset(a, s));
   h->steps += 1;
   return 0;
 }

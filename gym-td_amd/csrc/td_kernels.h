@@ -67,6 +67,9 @@ struct StepArgs {
 hipError_t launch_step(const StepArgs& a, hipStream_t s, bool reset, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
 // Small-batch step-kernel workgroups (one per board) resident at once on `cus` compute units.
 int step_resident_boards(const StepArgs& a, int cus);
+// random_agent=False with auto-reset: reset the boards the step just finished (a.done),
+// drawing their layouts from the shared numpy stream now (same stream, after the step).
+hipError_t launch_autoreset(const StepArgs& a, hipStream_t s);
 // Draw staged layouts for every board whose ring has a free slot (side stream).
 hipError_t launch_refill(const StepArgs& a, hipStream_t s);
 // The built-in opponent (side 0: random_enemy_lv<level>, 1: random_tower_lv<level>)

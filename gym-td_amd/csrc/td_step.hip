@@ -1508,7 +1508,7 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
   if (done) u.episodes += 1;
   bool was_reset = false;
   uint32_t lay_head = 0;
-  if (done && a.autoreset) {
+  if (done && a.autoreset && !a.opp_np) {  // random_agent=False: td_autoreset_kernel follows
     // consume staged layout number lay_head, published by a refill kernel on a side
     // stream while this grid may be running: relaxed sc1 poll of its tag, then one
     // agent-scope acquire before the plain vector loads of the record
@@ -1772,21 +1772,15 @@ __device__ int wave_layout(LayoutSmem<NC>& G, const StepArgs& a, int b, int retr
   return st;
 }
 
-// TDGymBasic.reset for the boards in reset_mask (the device is idle: td_capi
-// synchronises first).  The layout is the caller's record (td_reset_layouts), else
-// the board's next staged layout, else a draw from its numpy stream now; a failing
-// draw (no retry) is reported in reset_fail and leaves the board unchanged, as the
-// reference raises.
-template <int LT>
-__global__ __launch_bounds__(64) void td_reset_kernel(StepArgs a) {
-  constexpr int NC = LT ? LT * LT : MAX_KERNEL_L * MAX_KERNEL_L;
-  __shared__ union U_ {
-    Smem<NC> board;
-    LayoutSmem<NC> gen;
-  } sh;
-  const int b = blockIdx.x;
-  if (b >= a.B) return;
-  if (a.reset_mask && !a.reset_mask[b]) return;
+// TDGymBasic.reset of board b, by one wave (the device is idle for this board: no refill
+// holds it).  The layout is the caller's record (td_reset_layouts), else the board's
+// next staged layout, else a draw from its numpy stream now -- skipping up to `retries`
+// failing draws.  A draw that still fails leaves the board unchanged and returns its
+// road status (the reference raises); else the board is reset, its first observation
+// written, and ROAD_OK returned.  keep_flags: an auto-reset keeps the board's flags,
+// an explicit reset clears them.
+template <int NC, int LT>
+__device__ int reset_one(Smem<NC>& S, LayoutSmem<NC>& gen, const StepArgs& a, int b, int retries, bool keep_flags) {
   const int L = LT ? LT : a.L;
   const uint32_t* rec;
   bool from_ring = false;
@@ -1799,24 +1793,20 @@ __global__ __launch_bounds__(64) void td_reset_kernel(StepArgs a) {
     const uint32_t tail = a.lay_tail[b];
     uint32_t* slot = a.nxt + ((size_t)b * NSLOT + head % NSLOT) * a.slot_words;
     if (tail == head) {  // nothing staged: draw now
-      const int st = wave_layout(sh.gen, a, b, 0, slot, head, 0x7fffffff);
+      const int st = wave_layout(gen, a, b, retries, slot, head, 0x7fffffff);
       __syncthreads();
-      if (st != ROAD_OK) {
-        if (threadIdx.x == 0) a.reset_fail[b] = (uint8_t)st;
-        return;
-      }
+      if (st != ROAD_OK) return st;
       if (threadIdx.x == 0) a.lay_tail[b] = tail + 1u;
     }
     rec = slot;
     from_ring = true;
   }
-  Smem<NC>& S = sh.board;
   stage_cfg(S, a.cfg);
   __syncthreads();
   const Ctx x{S.cfg, L, L * L, (int)threadIdx.x};
   U u;
   u.episodes = a.hdr[b].episodes;
-  u.flags = 0;
+  u.flags = keep_flags ? a.hdr[b].flags : 0;
   reset_board(S, u, x, rec);
   channel_scalars(S, u, x);
   store_cells(S, u, x, a, b);
@@ -1831,9 +1821,53 @@ __global__ __launch_bounds__(64) void td_reset_kernel(StepArgs a) {
     }
   }
   store_board(S, u, x, a, b);
-  if (x.lane == 0) {
-    a.reset_fail[b] = 0;
-    if (from_ring) a.lay_head[b] = head + 1u;
+  if (x.lane == 0 && from_ring) a.lay_head[b] = head + 1u;
+  return ROAD_OK;
+}
+
+template <int NC>
+union ResetSmem {
+  Smem<NC> board;
+  LayoutSmem<NC> gen;
+};
+
+// TDGymBasic.reset for the boards in reset_mask (td_reset / td_reset_layouts: the
+// device is idle, td_capi synchronises first).  A failing draw (no retry) is reported
+// in reset_fail and leaves the board unchanged, as the reference raises.
+template <int LT>
+__global__ __launch_bounds__(64) void td_reset_kernel(StepArgs a) {
+  constexpr int NC = LT ? LT * LT : MAX_KERNEL_L * MAX_KERNEL_L;
+  __shared__ ResetSmem<NC> sh;
+  const int b = blockIdx.x;
+  if (b >= a.B) return;
+  if (a.reset_mask && !a.reset_mask[b]) return;
+  const int st = reset_one<NC, LT>(sh.board, sh.gen, a, b, 0, false);
+  if (threadIdx.x == 0) a.reset_fail[b] = (uint8_t)st;
+}
+
+// Auto-reset with random_agent=False (TDGymBasic.py:87-89,101-103 under gym 0.21's
+// AsyncVectorEnv, which calls reset() right after the step that ends an episode): the
+// built-in opponent and reset() draw from the same numpy stream, so the next layout
+// cannot be drawn ahead of play.  Launched right behind each step kernel on its
+// stream: a wave scans 64 boards' done flags (written by that step) and resets the
+// finished boards in turn, drawing each layout from the board's stream now, exactly
+// where the reference's reset() would -- failing draws skipped as in every auto-reset.
+// The step kernel left those boards finished (no staged layout is consumed in this
+// mode); their observation is overwritten with the new episode's first one.
+template <int LT>
+__global__ __launch_bounds__(64) void td_autoreset_kernel(StepArgs a) {
+  constexpr int NC = LT ? LT * LT : MAX_KERNEL_L * MAX_KERNEL_L;
+  __shared__ ResetSmem<NC> sh;
+  const int lane = (int)threadIdx.x;
+  const int b0 = (int)blockIdx.x * 64;
+  const bool mine = b0 + lane < a.B && a.done[b0 + lane] != 0;
+  uint64_t m = ballot(mine);
+  while (m) {
+    const int b = b0 + ctz64(m);
+    m &= m - 1;
+    const int st = reset_one<NC, LT>(sh.board, sh.gen, a, b, kLayoutRetries, true);
+    __syncthreads();
+    if (st != ROAD_OK && lane == 0) a.hdr[b].flags |= FLAG_NO_LAYOUT;  // keeps stepping its finished episode
   }
 }
 
@@ -1934,6 +1968,21 @@ hipError_t launch_step(const StepArgs& a, hipStream_t s, bool reset, hipEvent_t 
     case 30: return launch2<30>(a, s, reset, ev0, ev1);
     default: return launch2<0>(a, s, reset, ev0, ev1);
   }
+}
+
+template <int LT>
+static void launch_autoreset2(const StepArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(td_autoreset_kernel<LT>, dim3((a.B + 63) / 64), dim3(64), 0, s, a);
+}
+
+hipError_t launch_autoreset(const StepArgs& a, hipStream_t s) {
+  switch (a.L) {
+    case 10: launch_autoreset2<10>(a, s); break;
+    case 20: launch_autoreset2<20>(a, s); break;
+    case 30: launch_autoreset2<30>(a, s); break;
+    default: launch_autoreset2<0>(a, s); break;
+  }
+  return hipGetLastError();
 }
 
 template <int LT>

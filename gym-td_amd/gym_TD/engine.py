@@ -42,6 +42,11 @@ class TDEngine(object):
     host_io: step inputs and outputs live in pinned host memory that the kernels
           read and write directly (zero-copy).  For the single-env classes: one
           launch and one stream synchronisation per step, no per-tensor copies.
+          A host_io step() is synchronous: it returns once the kernel has read the
+          staged actions and written the outputs.
+    random_agent: TDGymBasic's random_agent (False: the built-in opponent draws from
+          each board's layout stream; with auto-reset the next layout is then drawn
+          right after the step that ends the episode, in stream order).
     """
 
     def __init__(self, map_size, n_boards, mode="def", multi_action=None, difficulty=1, device=None,
@@ -224,6 +229,9 @@ class TDEngine(object):
                 self._atk_np[...] = np.asarray(atk_act, dtype=np.int64).reshape(self._atk_np.shape)
                 io.atk_act = self._atk_in.data_ptr()
             _lib.check(_lib.lib.td_step(self._h, io, self._stream()))
+            # the outputs are the caller's as soon as this returns, and the next call
+            # rewrites the staged actions: wait for the kernel
+            torch.cuda.current_stream(self.device).synchronize()
             return self.obs, self.reward, self.done
         if self.mode != "atk":
             d = _as_dev(def_act, torch.int64, self.device)

@@ -290,15 +290,19 @@ class TDVecEnv(object):
     do not depend on how boards are sharded over GPUs.  Auto-reset follows gym
     0.21's AsyncVectorEnv: a finished board's returned obs is its next episode's
     first obs; ``infos['episode_return'/'episode_length']`` hold the finished
-    episode's totals where ``done``.
+    episode's totals where ``done``.  ``random_agent=False`` (TDGymBasic.py:87-89,
+    101-103): the built-in opponents draw from each board's layout stream, and each
+    auto-reset draws the next layout right after the step that ended the episode,
+    as AsyncVectorEnv's reset() would.
     """
 
     def __init__(self, map_size, num_envs, mode="def", difficulty=1, multi_action=None, seed=0, global_offset=0,
-                 device=None, info=True, autoreset=True, host_io=False):
+                 device=None, info=True, autoreset=True, host_io=False, random_agent=True):
         self.map_size, self.num_envs, self.mode = int(map_size), int(num_envs), mode
         seeds = np.arange(num_envs, dtype=np.int64) + int(seed) + int(global_offset)
         self.engine = TDEngine(map_size, num_envs, mode, multi_action, difficulty, device=device,
-                               np_seeds=seeds, py_seeds=seeds, autoreset=autoreset, info=info, host_io=host_io)
+                               np_seeds=seeds, py_seeds=seeds, autoreset=autoreset, info=info, host_io=host_io,
+                               random_agent=random_agent)
         L = self.map_size
         self.observation_space = Box(low=0., high=1., shape=(45, L, L), dtype=np.float32)
         dspace = (Box(low=0., high=2., shape=(6, L, L), dtype=np.int64) if self.engine.multi

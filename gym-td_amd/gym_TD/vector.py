@@ -42,7 +42,8 @@ class VectorEnv(object):
     (every auto-reset draws the env's next layout); the single-env classes support it.
     """
 
-    def __init__(self, env_id, num_envs, map_size=None, difficulty=1, seed=None, fixed_seed=False, device=None):
+    def __init__(self, env_id, num_envs, map_size=None, difficulty=1, seed=None, fixed_seed=False, device=None,
+                 random_agent=True):
         if fixed_seed:
             raise NotImplementedError("fixed_seed=True: use the single-env classes (gym_TD.envs.TDDefense ...)")
         self.kind, self.map_size = _parse(env_id, map_size)
@@ -52,8 +53,9 @@ class VectorEnv(object):
         self._seed = 0 if seed is None else int(seed)
         self._difficulty = difficulty
         # host_io: the kernels write the numpy outputs straight into pinned host memory
+        self._random_agent = bool(random_agent)
         self.vec = _envs.TDVecEnv(self.map_size, self.num_envs, self.kind, difficulty=difficulty, seed=self._seed,
-                                  device=device, info=True, host_io=True)
+                                  device=device, info=True, host_io=True, random_agent=self._random_agent)
         self.observation_space = self.vec.observation_space
         self.single_action_space = self.vec.action_space
         self.action_space = self.vec.action_space
@@ -64,9 +66,11 @@ class VectorEnv(object):
     def _make_single(self, i):
         def make():
             if self.kind == "2p":
-                return _envs.TDMulti(self.map_size, seed=self._seed + i, opponent_seed=self._seed + i)
+                return _envs.TDMulti(self.map_size, seed=self._seed + i, opponent_seed=self._seed + i,
+                                     random_agent=self._random_agent)
             cls = _envs.TDDefense if self.kind == "def" else _envs.TDAttack
-            return cls(self.map_size, difficulty=self._difficulty, seed=self._seed + i, opponent_seed=self._seed + i)
+            return cls(self.map_size, difficulty=self._difficulty, seed=self._seed + i, opponent_seed=self._seed + i,
+                       random_agent=self._random_agent)
         return make
 
     def seed(self, seeds=None):

@@ -112,8 +112,13 @@ int td_set_autoreset(td_handle* h, int on);
 /* TDGymBasic(random_agent=...) (TDGymBasic.py:18-26): with random_agent = 0 the built-in
  * opponents draw from each board's numpy layout stream (np_random, :87-89,101-103,
  * 118-120,139-160,176-177,188-190,213-256) instead of its CPython stream; the destruct
- * branch's tower index stays on CPython random (:191, :287).  Requires auto-reset off
- * (the layout stream is then shared by play and reset(), in order). */
+ * branch's tower index stays on CPython random (:191, :287).  Play and reset() then
+ * share the stream in order: with auto-reset on, a finished board's next layout is drawn
+ * right after the step that ended its episode (a second kernel on the step's stream), as
+ * gym's AsyncVectorEnv calls reset() there; nothing is staged ahead.  Switching to 0 is
+ * refused while a board holds layouts an auto-reset refill drew ahead of play (set it
+ * before the first reset, or re-seed with td_seed).  Both mode setters synchronise the
+ * device first. */
 int td_set_random_agent(td_handle* h, int random_agent);
 
 /* Board b's layout stream = numpy.random.RandomState(np_seeds[b]) and its built-in

@@ -199,6 +199,75 @@ def test_vecenv_autoreset_vs_oracle():
         ve.close()
 
 
+@pytest.mark.parametrize("L,B,mode,difficulty,steps", [
+    (10, 64, "def", 1, 400), (10, 48, "def", 0, 300), (10, 48, "atk", 2, 300), (20, 24, "atk", 1, 400)])
+def test_vecenv_random_agent_false_autoreset(L, B, mode, difficulty, steps):
+    """random_agent=False under auto-reset (TDGymBasic.py:87-89,101-103 in gym 0.21's
+    AsyncVectorEnv, train/main.py:329-347): the built-in opponent draws from each board's
+    layout stream and every finished board's next layout is drawn from that stream right
+    after the step that ended the episode (td_autoreset_kernel), failing draws skipped.
+    Against the oracle's random_agent=False branch, bit for bit, over many short
+    episodes; the streams end where the oracle's end."""
+    ov = dict(base_LP=1, defender_init_cost=0, defender_cost_rate=0.02) if mode == "def" else dict(base_LP=1)
+    cfg = O.Config(**ov)
+    seeds, orc = _first_ok_seeds(L, B, 6000 + 13 * difficulty, mode, False, difficulty, cfg, random_agent=False)
+    with reference_settings(ov, False):
+        ve = E.TDVecEnv(L, B, mode, difficulty=difficulty, seed=0, random_agent=False)
+    eng = ve.engine
+    eng.seed(np_seeds=seeds, py_seeds=seeds)
+    try:
+        obs = ve.reset().cpu().numpy()
+        for b, o in enumerate(orc):
+            assert np.array_equal(obs[b], o._board.get_states())
+        rng = np.random.RandomState(17 + L)
+        resets = skipped = 0
+        for k in range(steps):
+            if mode == "def":
+                acts = np.array([policies.discrete_def(rng, L) for o in orc], dtype=np.int64)
+            else:
+                acts = np.stack([policies.atk(rng) for _ in orc]).astype(np.int64)
+            obs_t, rew_t, done_t, _ = ve.step(torch.from_numpy(acts).cuda())
+            ob, rw, dn = obs_t.cpu().numpy(), rew_t.cpu().numpy(), done_t.cpu().numpy()
+            st = eng.export_state()
+            for b, o in enumerate(orc):
+                if mode == "def":
+                    wo, wr, wd, _ = o.step(int(acts[b]))
+                else:
+                    wo, wr, wd, _ = o.step(None, acts[b])
+                assert canon.fhex(rw[b]) == canon.fhex(wr), (k, b)
+                assert bool(dn[b]) == wd, (k, b)
+                if wd:
+                    wo, s = _oracle_reset_skipping(o)
+                    skipped += s
+                    resets += 1
+                assert np.array_equal(ob[b], wo), (k, b, np.argwhere(ob[b] != wo)[:5].tolist())
+                assert canon.state_digest(eng.board_state(b, st)) == canon.state_digest(canon.oracle_state(o)), (k, b)
+        assert resets >= B // 3  # episodes end and auto-reset throughout the run
+        assert (eng.flags() == 0).all()
+        for b in range(0, B, max(1, B // 8)):
+            ns = orc[b].np_random.get_state()
+            assert eng.get_np_state(b).tolist() == list(ns[1]) + [int(ns[2])], b
+    finally:
+        ve.close()
+
+
+def test_random_agent_false_refused_with_staged_layouts():
+    """Layouts an auto-reset refill drew ahead of play would put the numpy stream out of
+    the reference's order once the opponent draws from it: switching random_agent off is
+    refused then, and allowed again after re-seeding the layout streams."""
+    from gym_TD import _lib
+    eng = TDEngine(10, 8, "def", False, 1, np_seeds=range(8), py_seeds=range(8), autoreset=True)
+    try:
+        eng.reset_all()
+        torch.cuda.synchronize()
+        with pytest.raises(_lib.TDError):
+            _lib.check(_lib.lib.td_set_random_agent(eng._h, 0))
+        eng.seed(np_seeds=range(8))
+        _lib.check(_lib.lib.td_set_random_agent(eng._h, 0))
+    finally:
+        eng.close()
+
+
 @pytest.mark.parametrize("mode,multi,shards", [("def", False, 2), ("2p", True, 2), ("def", False, 8)])
 def test_vecenv_sharding_invariance(mode, multi, shards):
     """Board i of the global batch follows the same trajectory whether it is
@@ -650,6 +719,3 @@ def test_random_agent_false_vs_oracle(cls, mode, L, difficulty, steps):
         assert ended or mode == "atk"
     finally:
         env.close()
-    # auto-reset draws layouts ahead of play: refused with random_agent=False
-    with pytest.raises(Exception):
-        TDEngine(L, 2, mode, False, difficulty, autoreset=True, random_agent=False)
