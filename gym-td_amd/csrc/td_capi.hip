@@ -62,7 +62,9 @@ struct td_handle {
   int lw = 0;  // layout record words
   size_t scratch_stride = 0;
   TdDevCfg dcfg;
-  TdDevCfg* d_cfg = nullptr;
+  TdDevCfg* d_cfg = nullptr;  // [NCFG]: one constant block per paramConfig epoch
+  int epoch = 0;              // the current block
+  int cfg_fresh = 1;          // blocks [cfg_fresh, NCFG) never used yet
   TdHdr* d_hdr = nullptr;
   double *d_en_lp = nullptr, *d_en_mg = nullptr, *d_tw_cd = nullptr;
   uint32_t *d_en_inf = nullptr, *d_tw_inf = nullptr, *d_cells = nullptr, *d_opp = nullptr, *d_np = nullptr;
@@ -111,9 +113,9 @@ void build_dev_cfg(const td_config& c, TdDevCfg& d) {
   // lvup(atk, rge, dmgrge, intv=tower_cost[t][l], cost += tower_attack_interval[t][l]).
   for (int t = 0; t < 4; ++t) {
     d.t_intv[t][0] = c.tower_attack_interval[t][0];
-    d.t_value[t][0] = c.tower_cost[t][0];
     d.t_intv[t][1] = c.tower_cost[t][1];
-    d.t_value[t][1] = c.tower_cost[t][0] + c.tower_attack_interval[t][1];
+    d.t_addcost[t][0] = 0.0;
+    d.t_addcost[t][1] = c.tower_attack_interval[t][1];
   }
   d.destruct_return = c.tower_destruct_return;
   d.frozen_ratio = c.frozen_ratio;
@@ -143,7 +145,7 @@ int check_cfg(const td_config& c) {
   if (c.max_cluster_length != 8 || c.max_num_of_roads != 3) return fail("max_cluster_length must be 8, max_num_of_roads 3");
   if (c.max_episode_steps <= 0) return fail("max_episode_steps must be > 0");
   if (c.tower_distance < 0 || c.tower_distance > 15) return fail("tower_distance out of range");
-  if (c.frozen_time < 0 || c.frozen_time > 0xffff) return fail("frozen_time out of range");
+  if (c.frozen_time < 0 || c.frozen_time > 255) return fail("frozen_time must be in [0, 255] (8-bit slowdown)");
   if (c.base_LP < 1) return fail("base_LP must be a positive int (None is not supported)");
   for (int t = 0; t < 4; ++t)
     for (int l = 0; l < 2; ++l)
@@ -173,7 +175,7 @@ StepArgs base_args(td_handle* h) {
   a.slot_words = slot_words(h->L);
   a.refill_grp = refill_group(h->B, h->refill_waves);
   a.refill_walks = kWalksPerStep * (h->refill_every > 0 ? h->refill_every : kRefillEvery);
-  a.reset_fail = h->d_fail; a.cfg = h->d_cfg;
+  a.reset_fail = h->d_fail; a.cfg = h->d_cfg + h->epoch; a.cfgs = h->d_cfg; a.epoch = h->epoch;
   return a;
 }
 
@@ -319,7 +321,7 @@ td_handle* td_create(const td_config* cfg, int map_size, int n_boards, int mode,
   build_dev_cfg(*cfg, h->dcfg);
   const size_t B = (size_t)n_boards;
   int rc = 0;
-  rc |= dalloc(&h->d_cfg, 1);
+  rc |= dalloc(&h->d_cfg, NCFG);
   rc |= dalloc(&h->d_hdr, B);
   rc |= dalloc(&h->d_en_lp, B * ECAP);
   rc |= dalloc(&h->d_en_mg, B * ECAP);
@@ -411,18 +413,46 @@ void td_destroy(td_handle* h) {
   delete h;
 }
 
+// paramConfig on a live engine (TDParam.py:98-100).  The reference reads most values
+// live from `config`, but an Enemy / Tower keeps the stats it was created (or upgraded)
+// with and a TDBoard the max_cost / base_LP of its reset.  So a new block becomes the
+// current epoch; entities keep referring to the block of their own epoch.  Blocks are
+// recycled only when no live enemy or tower refers to them (td_cfg_usage_kernel).
 int td_set_config(td_handle* h, const td_config* cfg) {
   if (!h || !cfg) return fail("td_set_config: NULL argument");
   if (check_cfg(*cfg)) return -1;
-  build_dev_cfg(*cfg, h->dcfg);
+  TdDevCfg d;
+  build_dev_cfg(*cfg, d);
   HIP_OK(hipDeviceSynchronize());
-  HIP_OK(hipMemcpy(h->d_cfg, &h->dcfg, sizeof(TdDevCfg), hipMemcpyHostToDevice));
+  if (std::memcmp(&d, &h->dcfg, sizeof d) == 0) return 0;  // nothing changed
+  int slot = -1;
+  if (h->cfg_fresh < NCFG) {
+    slot = h->cfg_fresh++;
+  } else {
+    uint32_t* d_used = nullptr;
+    HIP_OK(hipMalloc((void**)&d_used, NCFG / 8));
+    HIP_OK(hipMemset(d_used, 0, NCFG / 8));
+    StepArgs a = base_args(h);
+    const hipError_t e = launch_cfg_usage(a, d_used, nullptr);
+    uint32_t used[NCFG / 32];
+    const hipError_t e2 = e == hipSuccess ? hipMemcpy(used, d_used, sizeof used, hipMemcpyDeviceToHost) : e;
+    (void)hipFree(d_used);
+    HIP_OK(e2);
+    for (int k = 0; k < NCFG && slot < 0; ++k)
+      if (k != h->epoch && !((used[k / 32] >> (k % 32)) & 1u)) slot = k;
+    if (slot < 0) return fail("td_set_config: %d configs are still referenced by live enemies/towers", NCFG);
+  }
+  HIP_OK(hipMemcpy(h->d_cfg + slot, &d, sizeof d, hipMemcpyHostToDevice));
+  h->dcfg = d;
+  h->epoch = slot;
   return 0;
 }
 
 // Both mode setters first wait for the device: a refill may still be drawing on a side
 // stream.  Layouts staged so far stay valid for random_agent=True (they are the stream's
 // next layouts, in order), so turning auto-reset off keeps them for explicit resets.
+int td_config_epoch(td_handle* h) { return h ? h->epoch : fail("NULL handle"); }
+
 int td_set_autoreset(td_handle* h, int on) {
   if (!h) return fail("NULL handle");
   HIP_OK(hipDeviceSynchronize());
@@ -705,6 +735,20 @@ static int state_copy(td_handle* h, int b0, int count, void* host, bool to_host)
     return 0;
   };
   uint32_t* opp = (uint32_t*)(p + (size_t)count * (sizeof(TdHdr) + ECAP * 20 + TCAP * 12 + (size_t)h->NC * 4));
+  std::vector<uint8_t> retagged;
+  if (!to_host) {
+    // imported enemies and towers take the current config epoch: epoch tags of another
+    // engine (or of blocks since recycled) mean nothing here
+    retagged.assign(p, p + td_state_bytes(h, count));
+    uint8_t* q = retagged.data();
+    uint32_t* einf = (uint32_t*)(q + (size_t)count * (sizeof(TdHdr) + ECAP * 16));
+    uint32_t* tinf = (uint32_t*)(q + (size_t)count * (sizeof(TdHdr) + ECAP * 20 + TCAP * 8));
+    for (size_t i = 0; i < (size_t)count * ECAP; ++i) einf[i] = (einf[i] & 0x00ffffffu) | ((uint32_t)h->epoch << 24);
+    for (size_t i = 0; i < (size_t)count * TCAP; ++i)
+      tinf[i] = (tinf[i] & 0x0000ffffu) | ((uint32_t)h->epoch << 16) | ((uint32_t)h->epoch << 24);
+    p = q;
+    opp = (uint32_t*)(p + (size_t)count * (sizeof(TdHdr) + ECAP * 20 + TCAP * 12 + (size_t)h->NC * 4));
+  }
   std::vector<uint32_t> hot((size_t)count * HOT_WORDS);
   if (!to_host) {  // the hot record follows the imported words (no pre-drawn outputs)
     for (int i = 0; i < count; ++i) {

@@ -44,7 +44,9 @@ struct StepArgs {
   const int32_t* ovr_idx;   // reset kernel, td_reset_layouts: [B] record index in ovr_rec, or -1
   const uint32_t* ovr_rec;  // caller-supplied layout records (layout_words(L) each)
   uint64_t* stamps;     // TD_STAMPS diagnostic builds only: [B][16] s_memtime per phase
-  const TdDevCfg* cfg;
+  const TdDevCfg* cfg;   // the current constant block (= cfgs + epoch)
+  const TdDevCfg* cfgs;  // [NCFG] one block per paramConfig epoch (entities keep their epoch's values)
+  int epoch;
   const int64_t* def_act;
   const int64_t* atk_act;
   float* obs;
@@ -70,6 +72,8 @@ int step_resident_boards(const StepArgs& a, int cus);
 // random_agent=False with auto-reset: reset the boards the step just finished (a.done),
 // drawing their layouts from the shared numpy stream now (same stream, after the step).
 hipError_t launch_autoreset(const StepArgs& a, hipStream_t s);
+// Config epochs referred to by live enemies / towers: bit e of used[NCFG / 32] (zeroed by the caller).
+hipError_t launch_cfg_usage(const StepArgs& a, uint32_t* used, hipStream_t s);
 // Draw staged layouts for every board whose ring has a free slot (side stream).
 hipError_t launch_refill(const StepArgs& a, hipStream_t s);
 // The built-in opponent (side 0: random_enemy_lv<level>, 1: random_tower_lv<level>)

@@ -160,7 +160,9 @@ __device__ __forceinline__ void stage_cfg(Smem<NC>& S, const TdDevCfg* g) {
 // Wave-uniform scalar board state (identical in every lane).
 struct U {
   double cost_def, cost_atk, ep_ret, progress;
+  double max_cost;  // captured at reset (TDBoard.py:70)
   int steps, base_LP, atk_cd, def_cd, n, nt, num_roads, end_cell, maxdist, flags, episodes;
+  int max_base_LP;  // captured at reset (TDBoard.py:72)
   bool cells_dirty;  // map[6] changed (tower built / destroyed) or a new layout: write the cells back
   uint64_t starts;  // start cells of roads 0-2, 16 bits each (a shift, not an indexed field: keeps U in registers)
   __device__ __forceinline__ int start(int road) const { return (int)((starts >> (16 * road)) & 0xffffu); }
@@ -170,9 +172,21 @@ struct U {
 };
 
 struct Ctx {
-  const TdDevCfg& C;
+  const TdDevCfg& C;  // the current constant block (epoch ep), staged in LDS
   int L, NCr, lane;
+  const TdDevCfg* tab;  // every epoch's block (HBM)
+  int ep;
 };
+
+// A value an enemy or tower captured when it was created or upgraded (TDElements.py:
+// 4-43, 45-63, 134-170): from the block of its epoch -- the staged current one, or
+// (after a paramConfig) an older block in HBM.
+template <class F>
+__device__ __forceinline__ double captured(const Ctx& x, int ep, F f) {
+  double v = f(x.C);
+  if (ep != x.ep) v = f(x.tab[ep]);
+  return v;
+}
 
 // ---------------------------------------------------------------------------
 // CPython MT19937 for the built-in opponent, state in HBM, wave-parallel twist
@@ -344,7 +358,7 @@ __device__ __forceinline__ int tower_build(Smem<NC>& S, U& u, const Ctx& x, int 
   if (cw_block(S.cell[cell]) > 0) return FC_POS;          // :232
   if (u.nt >= TCAP) { u.flags |= FLAG_TW_OVERFLOW; return FC_CAP; }
   if (x.lane == 0) {
-    S.tInf[u.nt] = tw_pack(cell, t, 0);
+    S.tInf[u.nt] = tw_pack(cell, t, 0, x.ep, x.ep);
     S.tCd[u.nt] = 0.0;
     S.twr[cell] = (uint8_t)(0x80 | t);
   }
@@ -374,7 +388,7 @@ __device__ __forceinline__ int tower_lvup(Smem<NC>& S, U& u, const Ctx& x, int c
   if (u.cost_def < price) return FC_COST;
   __syncthreads();
   if (x.lane == 0) {
-    S.tInf[k] = tw_pack(cell, t, lv + 1);
+    S.tInf[k] = tw_pack(cell, t, lv + 1, tw_ec(ti), x.ep);
     S.twr[cell] = (uint8_t)(0x80 | ((lv + 1) << 2) | t);
   }
   u.cost_def = dsub(u.cost_def, price);                   // :266
@@ -388,8 +402,12 @@ __device__ __forceinline__ int tower_destruct(Smem<NC>& S, U& u, const Ctx& x, i
   if (k < 0) return FC_TARGET;                            // :291-293
   uint32_t ti = S.tInf[k];
   int t = (ti >> 12) & 3, lv = (ti >> 14) & 1;
-  u.cost_def = dadd(u.cost_def, dmul(x.C.t_value[t][lv], x.C.destruct_return));  // :276
-  u.cost_def = pymin(u.cost_def, x.C.max_cost);                                  // :277
+  // Tower.cost: tower_cost[t][0] when built, + tower_attack_interval[t][1] at the upgrade
+  // (the upgrade_tower argument swap), each from the epoch it was captured in
+  double value = captured(x, tw_ec(ti), [&](const TdDevCfg& c) { return c.t_price[t][0]; });
+  if (lv >= 1) value = dadd(value, captured(x, tw_eu(ti), [&](const TdDevCfg& c) { return c.t_addcost[t][lv]; }));
+  u.cost_def = dadd(u.cost_def, dmul(value, x.C.destruct_return));  // :276
+  u.cost_def = pymin(u.cost_def, u.max_cost);                      // :277
   u.cells_dirty = true;
   // towers.remove(t): keep the order of the rest (:278)
   uint32_t vi = 0;
@@ -554,7 +572,7 @@ __device__ __forceinline__ int summon_cluster(Smem<NC>& S, U& u, const Ctx& x, u
         if (x.lane == 0) {
           S.eLP[u.n] = C.e_lp[t][lv];
           S.eMg[u.n] = 0.0;
-          S.eInf[u.n] = en_pack(st, t, lv, 0);
+          S.eInf[u.n] = en_pack(st, t, lv, 0, x.ep);
         }
         u.n += 1;
         summoned = true;
@@ -588,6 +606,12 @@ __device__ __forceinline__ double damage(double LP, double atk, double def, bool
   LP = dsub(LP, dmg);
   if (LP <= 0.0) LP = 0.0;
   return LP;
+}
+
+// Enemy.defense as the enemy captured it (TDElements.py:33-43)
+__device__ __forceinline__ double e_def(const Ctx& x, uint32_t inf) {
+  const int t = en_type(inf), lv = en_lv(inf);
+  return captured(x, en_ep(inf), [&](const TdDevCfg& c) { return c.e_def[t][lv]; });
 }
 
 template <int NC>
@@ -649,29 +673,29 @@ __device__ __forceinline__ double board_step(Smem<NC>& S, U& u, const Ctx& x, co
       double cd = dsub(__shfl(tcd, k), 1.0);                 // :307
       if (!(cd > 0.0)) {
         const uint32_t ti = __shfl(tinf_l, k);
-        const int tt = (ti >> 12) & 3, tl = (ti >> 14) & 1, tc = ti & 0xfff;
-        const double rge = C.t_rge[tt][tl];
+        const int tt = (ti >> 12) & 3, tl = (ti >> 14) & 1, tc = ti & 0xfff, te = tw_eu(ti);
+        const double rge = captured(x, te, [&](const TdDevCfg& c) { return c.t_rge[tt][tl]; });
         bool in0 = val[0] && (double)cheb(en_cell(inf[0]), tc, L) <= rge;
         bool in1 = val[1] && (double)cheb(en_cell(inf[1]), tc, L) <= rge;
         uint64_t m0 = ballot(in0), m1 = ballot(in1);
         if (m0 | m1) {
           const int tgt = m0 ? ctz64(m0) : 64 + ctz64(m1);
-          cd = dadd(cd, C.t_intv[tt][tl]);                   // cd += intv
-          const double atk = C.t_atk[tt][tl];
+          cd = dadd(cd, captured(x, te, [&](const TdDevCfg& c) { return c.t_intv[tt][tl]; }));  // cd += intv
+          const double atk = captured(x, te, [&](const TdDevCfg& c) { return c.t_atk[tt][tl]; });
           if (tt <= 1) {  // TowerArrow / TowerMagic (TDElements.py:71-93)
             if (lane == (tgt & 63)) {
-              if (tgt < 64) lp[0] = damage(lp[0], atk, C.e_def[en_type(inf[0])][en_lv(inf[0])], tt == 1);
-              else lp[1] = damage(lp[1], atk, C.e_def[en_type(inf[1])][en_lv(inf[1])], tt == 1);
+              if (tgt < 64) lp[0] = damage(lp[0], atk, e_def(x, inf[0]), tt == 1);
+              else lp[1] = damage(lp[1], atk, e_def(x, inf[1]), tt == 1);
             }
           } else {
             const uint32_t tinf = (tgt >> 6) ? __shfl(inf[1], tgt & 63) : __shfl(inf[0], tgt & 63);
             const int tgc = en_cell(tinf);
-            const double dr = C.t_dmg[tt][tl];
+            const double dr = captured(x, te, [&](const TdDevCfg& c) { return c.t_dmg[tt][tl]; });
             if (tt == 2) {  // TowerBomb splash (:95-110)
 #pragma unroll
               for (int s = 0; s < 2; ++s)
                 if (val[s] && (double)cheb(tgc, en_cell(inf[s]), L) <= dr)
-                  lp[s] = damage(lp[s], atk, C.e_def[en_type(inf[s])][en_lv(inf[s])], false);
+                  lp[s] = damage(lp[s], atk, e_def(x, inf[s]), false);
             } else {  // TowerFrozen: first enemy within splash of the target (:112-132)
               bool h0 = val[0] && (double)cheb(tgc, en_cell(inf[0]), L) <= dr;
               bool h1 = val[1] && (double)cheb(tgc, en_cell(inf[1]), L) <= dr;
@@ -679,9 +703,9 @@ __device__ __forceinline__ double board_step(Smem<NC>& S, U& u, const Ctx& x, co
               if (q0 | q1) {
                 const int f = q0 ? ctz64(q0) : 64 + ctz64(q1);
                 if (lane == (f & 63)) {
-                  const uint32_t slow = (uint32_t)C.frozen_time << 16;
-                  if (f < 64) { lp[0] = damage(lp[0], atk, 0.0, true); inf[0] = (inf[0] & 0xffffu) | slow; }
-                  else { lp[1] = damage(lp[1], atk, 0.0, true); inf[1] = (inf[1] & 0xffffu) | slow; }
+                  const uint32_t slow = (uint32_t)C.frozen_time << 16;  // config.frozen_time, read live (:126)
+                  if (f < 64) { lp[0] = damage(lp[0], atk, 0.0, true); inf[0] = (inf[0] & 0xff00ffffu) | slow; }
+                  else { lp[1] = damage(lp[1], atk, 0.0, true); inf[1] = (inf[1] & 0xff00ffffu) | slow; }
                 }
               }
             }
@@ -709,7 +733,7 @@ __device__ __forceinline__ double board_step(Smem<NC>& S, U& u, const Ctx& x, co
     const uint32_t e = inf[s];
     const int t = en_type(e), lv = en_lv(e);
     int slow = en_slow(e), cell = en_cell(e);
-    const double sp = C.e_speed[t][lv];
+    const double sp = captured(x, en_ep(e), [&](const TdDevCfg& c) { return c.e_speed[t][lv]; });
     if (slow > 0) { mg[s] = dadd(mg[s], dmul(sp, C.frozen_ratio)); slow -= 1; }
     else mg[s] = dadd(mg[s], sp);
     while (mg[s] >= 1.0) {
@@ -721,7 +745,7 @@ __device__ __forceinline__ double board_step(Smem<NC>& S, U& u, const Ctx& x, co
       cell = r * L + c;
       if (cell == u.end_cell) { leak[s] = true; break; }
     }
-    inf[s] = en_pack(cell, t, lv, slow);
+    inf[s] = en_pack(cell, t, lv, slow, en_ep(e));
   }
   // a bad move is rare and lane-local: fold the flag into the uniform copy
   if (ballot((u.flags & FLAG_BAD_MOVE) != 0)) u.flags |= FLAG_BAD_MOVE;
@@ -744,8 +768,8 @@ __device__ __forceinline__ double board_step(Smem<NC>& S, U& u, const Ctx& x, co
   double rate;
   if (u.progress >= 0.5) rate = C.atk_final_rate;
   else rate = dadd(dmul(C.atk_init_rate, dsub(1.0, u.progress)), dmul(C.atk_final_rate, u.progress));
-  u.cost_atk = pymin(dadd(u.cost_atk, rate), C.max_cost);
-  u.cost_def = pymin(dadd(u.cost_def, C.def_rate), C.max_cost);
+  u.cost_atk = pymin(dadd(u.cost_atk, rate), u.max_cost);  // self.max_cost (:352-353)
+  u.cost_def = pymin(dadd(u.cost_def, C.def_rate), u.max_cost);
   __syncthreads();
   // the enemy list is final for this step: write it back now (its LDS is reused by the stats)
   const size_t eb = (size_t)b * ECAP;
@@ -777,7 +801,8 @@ __device__ __forceinline__ void enemy_stats(Smem<NC>& S, const U& u, const Ctx& 
     if (val[s]) {
       uint32_t e = S.eInf[i];
       key[s] = e & 0x3fffu;  // cell | type << 12
-      r[s] = f32(ddiv(S.eLP[i], C.e_lp[en_type(e)][en_lv(e)]));  // r = LP / maxLP (:358)
+      const int t = en_type(e), lv = en_lv(e);
+      r[s] = f32(ddiv(S.eLP[i], captured(x, en_ep(e), [&](const TdDevCfg& c) { return c.e_lp[t][lv]; })));  // LP / maxLP (:358)
     }
   }
   float mn[2] = {1.0f, 1.0f}, mx[2] = {0.0f, 0.0f}, sm[2] = {0.0f, 0.0f};
@@ -829,9 +854,9 @@ __device__ __forceinline__ void channel_scalars(Smem<NC>& S, const U& u, const C
   const int l = x.lane;
   if (l < 48) {
     float v = 0.0f;
-    if (l == 5) v = f32(ddiv((double)u.base_LP, (double)C.base_LP));
-    else if (l == 11) v = f32(ddiv(u.cost_def, C.max_cost));
-    else if (l == 12) v = f32(ddiv(u.cost_atk, C.max_cost));
+    if (l == 5) v = f32(ddiv((double)u.base_LP, (double)u.max_base_LP));
+    else if (l == 11) v = f32(ddiv(u.cost_def, u.max_cost));
+    else if (l == 12) v = f32(ddiv(u.cost_atk, u.max_cost));
     else if (l == 13) v = f32(u.progress);
     else if (l >= 21 && l < 25) v = (u.cost_def >= C.t_price[l - 21][0]) ? 1.0f : 0.0f;
     else if (l >= 41 && l < 45) v = f32(ddiv(ddiv(u.cost_def, C.e_cost[l - 41][0]), (double)C.max_cluster_length));
@@ -1111,7 +1136,8 @@ struct Prefetch {
 #define TD_PF_TW 16
 #endif
 constexpr int PF_ACT = 24, PF_HOT = 26, PF_EN = 16, PF_TW = TD_PF_TW;
-static_assert(offsetof(TdHdr, steps) == 24 && offsetof(TdHdr, start_cell) == 56 && offsetof(TdHdr, episodes) == 76,
+static_assert(offsetof(TdHdr, steps) == 24 && offsetof(TdHdr, start_cell) == 56 && offsetof(TdHdr, episodes) == 76 &&
+                  offsetof(TdHdr, max_cost) == 80 && offsetof(TdHdr, max_base_LP) == 88,
               "Prefetch header word map");
 
 __device__ __forceinline__ void prefetch_issue(Prefetch& P, const StepArgs& a, int b, int lane, int ncr,
@@ -1179,7 +1205,7 @@ __device__ __forceinline__ void load_board(Smem<NC>& S, U& u, const Ctx& x, cons
   }
   // TdHdr words (td_common.h): 0-5 cost_def, cost_atk, ep_return; 6 steps, 7 base_LP,
   // 8 atk_cd, 9 def_cd, 10 n_en, 11 n_tw, 12 num_roads, 13 end_cell, 14-16 start_cell,
-  // 17 maxdist, 18 flags, 19 episodes
+  // 17 maxdist, 18 flags, 19 episodes, 20-21 max_cost, 22 max_base_LP
   u.cost_def = lane_f64(P.w, 0); u.cost_atk = lane_f64(P.w, 2); u.ep_ret = lane_f64(P.w, 4);
   u.steps = (int)lane_word(P.w, 6); u.base_LP = (int)lane_word(P.w, 7);
   u.atk_cd = (int)lane_word(P.w, 8); u.def_cd = (int)lane_word(P.w, 9);
@@ -1187,6 +1213,7 @@ __device__ __forceinline__ void load_board(Smem<NC>& S, U& u, const Ctx& x, cons
   u.num_roads = (int)lane_word(P.w, 12); u.end_cell = (int)lane_word(P.w, 13);
   u.set_starts((int)lane_word(P.w, 14), (int)lane_word(P.w, 15), (int)lane_word(P.w, 16));
   u.maxdist = (int)lane_word(P.w, 17); u.flags = (int)lane_word(P.w, 18); u.episodes = (int)lane_word(P.w, 19);
+  u.max_cost = lane_f64(P.w, 20); u.max_base_LP = (int)lane_word(P.w, 22);
   u.progress = ddiv((double)u.steps, (double)x.C.max_episode_steps);
   u.cells_dirty = false;
   if (x.lane < u.n && x.lane < PF_EN) { S.eLP[x.lane] = P.lp; S.eMg[x.lane] = P.mg; S.eInf[x.lane] = P.inf; }
@@ -1220,6 +1247,7 @@ __device__ __forceinline__ void reset_board(Smem<NC>& S, U& u, const Ctx& x, con
   u.set_starts(rdl(hw, 4), rdl(hw, 5), rdl(hw, 6));
   u.cost_def = C.def_init_cost; u.cost_atk = C.atk_init_cost;
   u.base_LP = C.base_LP; u.steps = 0; u.progress = 0.0;
+  u.max_cost = C.max_cost; u.max_base_LP = C.base_LP;  // TDBoard(max_cost, base_LP) from config at reset
   u.atk_cd = 0; u.def_cd = 0; u.n = 0; u.nt = 0; u.ep_ret = 0.0;
   u.cells_dirty = true;
   __syncthreads();
@@ -1243,7 +1271,7 @@ __device__ __forceinline__ void store_board(const Smem<NC>& S, const U& u, const
     h.n_en = u.n; h.n_tw = u.nt; h.num_roads = u.num_roads; h.end_cell = u.end_cell;
     h.start_cell[0] = u.start(0); h.start_cell[1] = u.start(1); h.start_cell[2] = u.start(2);
     h.maxdist = u.maxdist; h.flags = u.flags; h.episodes = u.episodes;
-    h.pad[0] = h.pad[1] = h.pad[2] = h.pad[3] = 0;
+    h.max_cost = u.max_cost; h.max_base_LP = u.max_base_LP; h.pad = 0;
     a.hdr[b] = h;
   }
   const size_t tb = (size_t)b * TCAP;
@@ -1502,7 +1530,10 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
     if (MODE == MODE_ATK) win = u.base_LP <= 0 ? 1 : 0;
     else win = u.base_LP > 0 ? 1 : 0;
   }
-  const uint8_t allow = (uint8_t)((u.atk_cd <= 1 ? 1 : 0) | (u.def_cd <= 1 ? 2 : 0));
+  // info['AllowNextMove'] bits 0-1; bits 2-4 / 5-7: the cool-downs themselves, saturated at 7
+  // (TDGymBasic's attacker_cd / defender_cd attributes after the step)
+  const int acd = u.atk_cd < 7 ? u.atk_cd : 7, dcd = u.def_cd < 7 ? u.def_cd : 7;
+  const uint8_t allow = (uint8_t)((u.atk_cd <= 1 ? 1 : 0) | (u.def_cd <= 1 ? 2 : 0) | (acd << 2) | (dcd << 5));
   const double ep_ret = u.ep_ret;
 
   if (done) u.episodes += 1;
@@ -1608,7 +1639,7 @@ __device__ __forceinline__ void step_kernel_body(const StepArgs& a) {
 #endif
   stage_cfg(S, a.cfg);
   const int L = LT ? LT : a.L;
-  const Ctx x{S.cfg, L, L * L, (int)threadIdx.x};
+  const Ctx x{S.cfg, L, L * L, (int)threadIdx.x, a.cfgs, a.epoch};
   Prefetch P;
   prefetch_issue(P, a, b, x.lane, x.NCr, MODE != MODE_ATK && !a.multi);
   step_board<NC, LT, MODE, SCAN, SMALL>(S, x, a, b, P);
@@ -1647,7 +1678,7 @@ __global__ __launch_bounds__(64) void td_opponent_kernel(StepArgs a, int side, i
   if (a.reset_mask && !a.reset_mask[b]) return;
   stage_cfg(S, a.cfg);
   const int L = LT ? LT : a.L;
-  const Ctx x{S.cfg, L, L * L, (int)threadIdx.x};
+  const Ctx x{S.cfg, L, L * L, (int)threadIdx.x, a.cfgs, a.epoch};
   Prefetch P;
   prefetch_issue(P, a, b, x.lane, x.NCr, false);
   U u;
@@ -1803,7 +1834,7 @@ __device__ int reset_one(Smem<NC>& S, LayoutSmem<NC>& gen, const StepArgs& a, in
   }
   stage_cfg(S, a.cfg);
   __syncthreads();
-  const Ctx x{S.cfg, L, L * L, (int)threadIdx.x};
+  const Ctx x{S.cfg, L, L * L, (int)threadIdx.x, a.cfgs, a.epoch};
   U u;
   u.episodes = a.hdr[b].episodes;
   u.flags = keep_flags ? a.hdr[b].flags : 0;
@@ -1968,6 +1999,28 @@ hipError_t launch_step(const StepArgs& a, hipStream_t s, bool reset, hipEvent_t 
     case 30: return launch2<30>(a, s, reset, ev0, ev1);
     default: return launch2<0>(a, s, reset, ev0, ev1);
   }
+}
+
+// The paramConfig epochs live enemies and towers still refer to (td_set_config
+// recycles the others): one wave per board, bits OR-ed into used[NCFG / 32].
+__global__ __launch_bounds__(64) void td_cfg_usage_kernel(StepArgs a, uint32_t* used) {
+  const int b = blockIdx.x, l = (int)threadIdx.x;
+  if (b >= a.B) return;
+  const int n = a.hdr[b].n_en, nt = a.hdr[b].n_tw;
+  for (int i = l; i < n; i += 64) {
+    const int e = en_ep(a.en_inf[(size_t)b * ECAP + i]);
+    atomicOr(&used[e >> 5], 1u << (e & 31));
+  }
+  if (l < nt) {
+    const uint32_t ti = a.tw_inf[(size_t)b * TCAP + l];
+    atomicOr(&used[tw_ec(ti) >> 5], 1u << (tw_ec(ti) & 31));
+    atomicOr(&used[tw_eu(ti) >> 5], 1u << (tw_eu(ti) & 31));
+  }
+}
+
+hipError_t launch_cfg_usage(const StepArgs& a, uint32_t* used, hipStream_t s) {
+  hipLaunchKernelGGL(td_cfg_usage_kernel, dim3(a.B), dim3(64), 0, s, a, used);
+  return hipGetLastError();
 }
 
 template <int LT>

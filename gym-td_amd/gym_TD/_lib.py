@@ -81,6 +81,7 @@ def _load():
         "td_episode_records": (ctypes.c_int, [c_vp, c_vp, c_vp]),
         "td_opponent": (ctypes.c_int, [c_vp, ctypes.c_int, ctypes.c_int, c_u8p, c_vp]),
         "td_set_refill_interval": (ctypes.c_int, [c_vp, ctypes.c_int]),
+        "td_config_epoch": (ctypes.c_int, [c_vp]),
         "td_kernel_timing": (ctypes.c_int, [c_vp, ctypes.c_int, ctypes.c_int]),
         "td_kernel_times": (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_float), ctypes.c_int]),
         "td_py_seed": (None, [c_u32p, ctypes.c_uint32]),

@@ -5,6 +5,7 @@ The batched counterpart of TDGymBasic + TDDefense / TDAttack / TDMulti
 outputs are torch tensors on the engine's device; every step is one kernel
 launch on torch's current stream.
 """
+import copy
 import types
 
 import numpy as np
@@ -19,7 +20,7 @@ HDR_DTYPE = np.dtype([
     ("cost_def", "<f8"), ("cost_atk", "<f8"), ("ep_return", "<f8"), ("steps", "<i4"), ("base_LP", "<i4"),
     ("atk_cd", "<i4"), ("def_cd", "<i4"), ("n_en", "<i4"), ("n_tw", "<i4"), ("num_roads", "<i4"),
     ("end_cell", "<i4"), ("start_cell", "<i4", (3,)), ("maxdist", "<i4"), ("flags", "<i4"), ("episodes", "<i4"),
-    ("pad", "<i4", (4,))])
+    ("max_cost", "<f8"), ("max_base_LP", "<i4"), ("pad", "<i4")])
 assert HDR_DTYPE.itemsize == _lib.HDR_BYTES
 
 
@@ -62,6 +63,7 @@ class TDEngine(object):
         self.multi = bool(multi_action)
         self.difficulty = int(difficulty)
         self._cfg_c = P.to_c(cfg or P.config, hp)
+        self._cfg_hist = {0: copy.deepcopy(cfg or P.config)}  # paramConfig epoch -> config (td_config_epoch)
         h = _lib.lib.td_create(self._cfg_c, self.L, self.B, MODES[mode], int(self.multi), self.difficulty,
                                self.device.index or 0)
         if not h:
@@ -129,8 +131,16 @@ class TDEngine(object):
             pass
 
     def set_config(self, cfg=None, hp=None):
+        """paramConfig on this engine: the new values apply from the next step; live
+        enemies and towers keep the values they were created / upgraded with, and each
+        board the max_cost / base_LP of its last reset (TDElements.py:4-69, TDBoard.py:66-72)."""
         self._cfg_c = P.to_c(cfg or P.config, hp)
         _lib.check(_lib.lib.td_set_config(self._h, self._cfg_c))
+        self._cfg_hist[_lib.lib.td_config_epoch(self._h)] = copy.deepcopy(cfg or P.config)
+
+    def config_of_epoch(self, ep):
+        """The game config of paramConfig epoch ``ep`` (entity words carry their epoch)."""
+        return self._cfg_hist.get(ep, P.config)
 
     def seed(self, np_seeds=None, py_seeds=None):
         """Per-board seeds (int or array of B)."""
@@ -326,7 +336,7 @@ class TDEngine(object):
         h = st["hdr"][i]
         n, nt, L = int(h["n_en"]), int(h["n_tw"]), self.L
         inf = st["en_inf"][i][:n]
-        ens = [(int((u >> 12) & 3), int((u >> 14) & 1), int(u & 0xFFF) // L, int(u & 0xFFF) % L, int(u >> 16),
+        ens = [(int((u >> 12) & 3), int((u >> 14) & 1), int(u & 0xFFF) // L, int(u & 0xFFF) % L, int((u >> 16) & 0xFF),
                 float(st["en_lp"][i][k]), float(st["en_mg"][i][k])) for k, u in enumerate(inf)]
         tinf = st["tw_inf"][i][:nt]
         tws = [(int((u >> 12) & 3), int((u >> 14) & 1), int(u & 0xFFF) // L, int(u & 0xFFF) % L,

@@ -38,18 +38,22 @@ class TDBoardView(object):
     max_cost, base_LP, max_base_LP, steps, progress, map_size."""
 
     def __init__(self, engine, b, obs=None):
-        cfg, hp = P.config, P.hyper_parameters
+        hp = P.hyper_parameters
         st = engine.export_state(b, 1)
         s = engine.board_state(0, st)
-        self.map_size = L = engine.L
+        self.map_size = engine.L
         self.map, self.start, self.end = engine.map_planes(0, st)
         self.cost_def, self.cost_atk = s["cost_def"], s["cost_atk"]
-        self.max_cost = cfg.max_cost
-        self.base_LP, self.max_base_LP = s["base_LP"], cfg.base_LP
+        h = st["hdr"][0]
+        self.max_cost, self.base_LP, self.max_base_LP = float(h["max_cost"]), s["base_LP"], int(h["max_base_LP"])
         self.steps = s["steps"]
         self.progress = self.steps / hp.max_episode_steps
+        # an Enemy / Tower shows the values it captured (TDElements.py:4-69, 134-170): the
+        # config of the paramConfig epoch it was created / upgraded under
+        cfg_of = engine.config_of_epoch
         self.enemies = []
-        for (t, lv, r, c, slow, lp, mg) in s["enemies"]:
+        for k, (t, lv, r, c, slow, lp, mg) in enumerate(s["enemies"]):
+            cfg = cfg_of(int(st["en_inf"][0][k]) >> 24)
             e = _Enemy()
             e.type, e.lv, e.loc, e.LP, e.margin, e.slowdown = t, lv, [r, c], lp, mg, slow
             e.maxLP, e.speed = cfg.enemy_LP[t][lv], cfg.enemy_speed[t][lv]
@@ -57,13 +61,15 @@ class TDBoardView(object):
             e.dist = int(self.map[4, r, c])
             self.enemies.append(e)
         self.towers = []
-        for (t, lv, r, c, cd) in s["towers"]:
+        for k, (t, lv, r, c, cd) in enumerate(s["towers"]):
+            u = int(st["tw_inf"][0][k])
+            cb, cu = cfg_of((u >> 16) & 0xFF), cfg_of(u >> 24)  # built under / current stats from
             w = _Tower()
             w.type, w.lv, w.loc, w.cd = t, lv, [r, c], cd
-            w.atk, w.rge, w.dmgrge = cfg.tower_attack[t][lv], cfg.tower_range[t][lv], cfg.tower_splash_range[t][lv]
+            w.atk, w.rge, w.dmgrge = cu.tower_attack[t][lv], cu.tower_range[t][lv], cu.tower_splash_range[t][lv]
             # upgrade_tower's argument swap (TDElements.py:163-169)
-            w.intv = cfg.tower_attack_interval[t][0] if lv == 0 else cfg.tower_cost[t][lv]
-            w.cost = cfg.tower_cost[t][0] + (cfg.tower_attack_interval[t][1] if lv else 0)
+            w.intv = cu.tower_attack_interval[t][0] if lv == 0 else cu.tower_cost[t][lv]
+            w.cost = cb.tower_cost[t][0] + (cu.tower_attack_interval[t][1] if lv else 0)
             self.towers.append(w)
         self._obs = obs
         self.flags = s["flags"]
@@ -152,9 +158,13 @@ class _TDBasic(object):
         done = bool(n.done[0])
         win = int(n.win[0])
         an = int(n.allow_next[0])
-        self.attacker_cd = 0 if (an & 1) else 2  # only "<= 1" is observable from the step
-        self.defender_cd = 0 if (an & 2) else 2
-        return self._obs.copy(), reward, done, (None if win < 0 else bool(win)), an
+        # TDGymBasic's cool-down attributes (TDDefense.py:38-39,75; TDAttack.py:31-32,44):
+        # allow_next carries them saturated at 7, the board header holds them exactly
+        self.attacker_cd, self.defender_cd = (an >> 2) & 7, (an >> 5) & 7
+        if self.attacker_cd == 7 or self.defender_cd == 7:
+            h = e.export_state(0, 1)["hdr"][0]
+            self.attacker_cd, self.defender_cd = int(h["atk_cd"]), int(h["def_cd"])
+        return self._obs.copy(), reward, done, (None if win < 0 else bool(win)), an & 3
 
     def render(self, mode="human"):
         raise NotImplementedError("rendering (TDBoard.render, pyglet) is out of scope for the device engine")
@@ -330,7 +340,7 @@ class TDVecEnv(object):
         e = self.engine
         infos = {}
         if e.info_enabled:
-            infos = {"Win": e.win, "AllowNextMove": e.allow_next, "episode_return": e.ep_return,
+            infos = {"Win": e.win, "AllowNextMove": e.allow_next & 3, "episode_return": e.ep_return,
                      "episode_length": e.ep_len}
             if e.real_def is not None:
                 infos["RealAction"] = e.real_def

@@ -77,6 +77,7 @@ typedef struct td_config {
  *   fail_def  int32 [B]   fail_atk int32 [B][3] (-1 = no entry)       info['FailCode']
  *   win       int8 [B] (-1 = None)                                     info['Win']
  *   allow_next uint8 [B] (bit0 attacker_cd<=1, bit1 defender_cd<=1)   info['AllowNextMove']
+ *             bits 2-4 / 5-7: attacker_cd / defender_cd after the step, saturated at 7
  *   ep_return double [B], ep_len int32 [B]: running episode return / length after this
  *             step (the finished episode's totals when done[b]). */
 typedef struct td_step_io {
@@ -107,7 +108,13 @@ void td_config_default(td_config* cfg);
 td_handle* td_create(const td_config* cfg, int map_size, int n_boards, int mode, int multi_action,
                      int difficulty, int device);
 void td_destroy(td_handle* h);
+/* paramConfig on a live engine (TDParam.py:98-100): values the reference reads live from
+ * `config` change from the next step; enemies and towers keep the stats they were created
+ * or upgraded with (TDElements.py:4-69, 134-170) and each board the max_cost / base_LP of
+ * its last reset (TDBoard.py:66-72) -- the device keeps one constant block per config
+ * epoch (up to 256 still referenced by live entities).  td_config_epoch: the current one. */
 int td_set_config(td_handle* h, const td_config* cfg);
+int td_config_epoch(td_handle* h);
 int td_set_autoreset(td_handle* h, int on);
 /* TDGymBasic(random_agent=...) (TDGymBasic.py:18-26): with random_agent = 0 the built-in
  * opponents draw from each board's numpy layout stream (np_random, :87-89,101-103,
@@ -197,7 +204,9 @@ int td_layout_generate(uint32_t* np_state625, int map_size, int max_attempts, ui
 
 /* Board state, array-major for boards [b0, b0+count):
  *   hdr[count] (96 B each: see td_common.h TdHdr), en_lp f64[count][128], en_mg f64[count][128],
- *   en_inf u32[count][128], tw_cd f64[count][32], tw_inf u32[count][32], cells u32[count][L*L],
+ *   en_inf u32[count][128] (cell | type<<12 | lv<<14 | slowdown<<16 | config epoch<<24),
+ *   tw_cd f64[count][32], tw_inf u32[count][32] (cell | type<<12 | lv<<14 | build epoch<<16 |
+ *   stats epoch<<24; imported entities take the current epoch), cells u32[count][L*L],
  *   opp_mt u32[count][626] (the opponent's CPython stream: 624 words, position, and the
  *   lazy-twist boundary -- words [w[625], 624) still hold the previous block).  Synchronous. */
 size_t td_state_bytes(td_handle* h, int count);

@@ -3,6 +3,8 @@ TD-2p boards stepped together in one launch (every built-in opponent level,
 discrete and multi-action, the info tensors), and the TDVecEnv rollout surface
 (auto-reset with failing layout draws, sharding invariance of trajectories).
 Everything is compared bit-exactly with the CPU oracle on the same seeds."""
+import copy
+
 import numpy as np
 import pytest
 import torch
@@ -377,39 +379,69 @@ def test_export_import_roundtrip():
 
 
 def test_paramconfig_reaches_live_engines():
-    """paramConfig (TDParam.py:98-100) re-uploads the constant block of live engines.
-    The reference's enemies and towers keep the values they captured when created, so
-    the comparison restarts both sides on fresh episodes (same streams) after the call:
-    from there the device follows the oracle under the new values."""
+    """paramConfig (TDParam.py:98-100) in the middle of episodes, twice, on a live engine.
+    The reference reads most values live from `config`, but an Enemy / Tower keeps the
+    stats it was created or upgraded with (TDElements.py:4-69, 134-170: maxLP, speed,
+    defense; atk, rge, dmgrge, intv, cost) and a TDBoard the max_cost / base_LP of its
+    reset (TDBoard.py:66-72).  The device keeps one constant block per config epoch and
+    tags entities with theirs: bit-exact against the oracle (whose Enemy / Tower objects
+    capture like the reference's) through both changes and a reset of half the boards."""
     import gym_TD
     from gym_TD import params as P
-    L, B = 10, 8
-    ov = dict(reward_time=0.004, tower_range=[[4, 4], [3, 3], [5, 5], [4, 4]],
-              enemy_speed=[[.2, .2], [.2, .2], [.15, .15], [.1, .1]], defender_init_cost=30)
+    L, B = 10, 16
+    ov1 = dict(reward_time=0.004, tower_range=[[4, 4], [3, 3], [5, 5], [4, 4]],
+               enemy_speed=[[.2, .2], [.2, .2], [.15, .15], [.1, .1]], enemy_LP=[[600, 1500], [1500, 2500],
+               [5000, 7000], [7000, 9000]], enemy_defense=[[10, 10], [150, 200], [500, 700], [60, 90]],
+               tower_attack=[[500, 600], [700, 800], [600, 700], [400, 450]], max_cost=60, base_LP=7,
+               tower_attack_interval=[[3, 3], [5, 5], [6, 6], [4.5, 4.5]], defender_cost_rate=0.5)
+    ov2 = dict(tower_cost=[[8, 9], [15, 16], [20, 21], [11, 12]], tower_splash_range=[[0, 0], [0, 0], [2, 2], [1, 1]],
+               frozen_ratio=0.3, tower_destruct_return=0.75, enemy_speed=[[.3, .3], [.15, .15], [.12, .12], [.1, .1]],
+               max_cost=150, attacker_cost_final_rate=1.5)
     seeds, orc = _first_ok_seeds(L, B, 7000, "def", False, 1)
-    saved = {k: getattr(P.config, k) for k in ov}
+    saved = {k: copy.deepcopy(getattr(P.config, k)) for k in set(ov1) | set(ov2)}
     eng = TDEngine(L, B, "def", False, 1, np_seeds=seeds, py_seeds=seeds, autoreset=False)
     try:
         eng.reset()
         rng = np.random.RandomState(8)
-        for k in range(90):
-            if k == 30:
-                gym_TD.paramConfig(**ov)
+        epochs = set()
+        for k in range(160):
+            if k in (30, 70):
+                ov = ov1 if k == 30 else ov2
+                gym_TD.paramConfig(**ov)  # re-uploads the live engine's config (a new epoch)
                 for o in orc:
                     for key, v in ov.items():
-                        setattr(o.cfg, key, v)
-                    o.reset()
-                _, failed = eng.reset()
-                assert not failed
-            acts = np.array([policies.discrete_def(rng, L, o._board.map[0], 0.5) for o in orc], dtype=np.int64)
+                        setattr(o.cfg, key, copy.deepcopy(v))
+            if k == 110:  # half the boards start a new episode: they capture the new max_cost / base_LP
+                m = np.zeros(B, np.uint8)
+                m[::2] = 1
+                _, failed = eng.reset(m)
+                while failed:  # the reference raises on these draws: both sides draw again
+                    m[:] = 0
+                    m[failed] = 1
+                    _, failed = eng.reset(m)
+                for b in range(0, B, 2):
+                    _oracle_reset_skipping(orc[b])
+            acts = np.array([policies.discrete_def(rng, L, o._board.map[0], 0.6) for o in orc], dtype=np.int64)
             eng.step(def_act=torch.from_numpy(acts))
             ob, rw = eng.obs.cpu().numpy(), eng.reward.cpu().numpy()
             st = eng.export_state()
             for b, o in enumerate(orc):
+                if o._board.done():
+                    continue
                 wo, wr, _, _ = o.step(int(acts[b]))
                 assert canon.fhex(rw[b]) == canon.fhex(wr), (k, b)
                 assert canon.state_digest(eng.board_state(b, st)) == canon.state_digest(canon.oracle_state(o)), (k, b)
-                assert np.array_equal(ob[b], wo), (k, b)
+                assert np.array_equal(ob[b], wo), (k, b, np.argwhere(ob[b] != wo)[:5].tolist())
+            for b in range(B):
+                n, nt = int(st["hdr"][b]["n_en"]), int(st["hdr"][b]["n_tw"])
+                epochs |= {int(u) >> 24 for u in st["en_inf"][b][:n]} | {int(u) >> 24 for u in st["tw_inf"][b][:nt]}
+        assert len(epochs) >= 2  # entities of different config epochs lived side by side
+        # the drop-in view shows each entity's captured values
+        view = E.TDBoardView(eng, 1)
+        for e in view.enemies:
+            w = [x for x in orc[1]._board.enemies if x.loc == e.loc and x.type == e.type and x.LP == e.LP]
+            assert w and w[0].maxLP == e.maxLP and w[0].speed == e.speed and w[0].defense == e.defense
+        assert view.max_cost == orc[1]._board.max_cost and view.max_base_LP == orc[1]._board.max_base_LP
     finally:
         gym_TD.paramConfig(**saved)
         eng.close()
@@ -701,6 +733,8 @@ def test_random_agent_false_vs_oracle(cls, mode, L, difficulty, steps):
             assert canon.fhex(r) == canon.fhex(wr), k
             assert np.array_equal(o, wo), k
             assert d == bool(wd), k
+            # the env's cool-down attributes (TDDefense.py:38-39,75; TDAttack.py:31-32,44)
+            assert (env.attacker_cd, env.defender_cd) == (orc.attacker_cd, orc.defender_cd), k
             if d:
                 ended = True
                 try:
