@@ -379,12 +379,13 @@ td_handle* td_create(const td_config* cfg, int map_size, int n_boards, int mode,
      // Infinity Cache (TD_SMALL / TD_OBS_WT = 0|1 override, for A/B runs)
     int cus = 0;
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
-    const int resident = step_resident_boards(base_args(h), cus);
+    const int resident = step_resident_boards(base_args(h), cus, 1);
+    const int resident2 = step_resident_boards(base_args(h), cus, 2);
     const double obs_bytes = (double)n_boards * NCH * h->NC * 4.0;
-    h->small = n_boards <= resident ? 1 : 0;
+    h->small = n_boards <= resident2 ? 2 : n_boards <= resident ? 1 : 0;
     h->obs_wt = h->small && obs_bytes <= 192.0 * 1024 * 1024 ? 1 : 0;
     auto ov = [](const char* name, int& v) { if (const char* e = std::getenv(name)) v = std::atoi(e) ? 1 : 0; };
-    ov("TD_SMALL", h->small);
+    if (const char* e = std::getenv("TD_SMALL")) h->small = std::max(0, std::min(2, std::atoi(e)));
     ov("TD_OBS_WT", h->obs_wt);
     if (const char* e = std::getenv("TD_REFILL_EVERY")) h->refill_every = std::max(0, std::atoi(e));  // A/B runs
     if (const char* e = std::getenv("TD_REFILL_WAVES")) h->refill_waves = std::max(1, std::atoi(e));

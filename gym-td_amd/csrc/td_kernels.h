@@ -14,7 +14,7 @@ constexpr int HOT_WORDS = 12;
 struct StepArgs {
   int B, L, mode, multi, difficulty, autoreset;
   int opp_np;           // random_agent=False: the built-in opponents draw from np_mt (auto-reset off)
-  int small;            // the batch fits one round of step waves: td_step_kernel_small (td_step.hip)
+  int small;            // the batch fits one round of step waves: 1 td_step_kernel_small, 2 td_step_kernel_small2
   int obs_wt;           // small kernel: observation stores write-through (the batch's obs fits the MALL)
   TdHdr* hdr;
   double* en_lp;
@@ -67,8 +67,9 @@ struct StepArgs {
 
 // ev0 / ev1: optional timing events bound to the step kernel's dispatch (td_kernel_timing).
 hipError_t launch_step(const StepArgs& a, hipStream_t s, bool reset, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
-// Small-batch step-kernel workgroups (one per board) resident at once on `cus` compute units.
-int step_resident_boards(const StepArgs& a, int cus);
+// Small-batch step-kernel workgroups (one per board) resident at once on `cus` compute
+// units, for the one-wave (td_step_kernel_small) or two-wave (td_step_kernel_small2) build.
+int step_resident_boards(const StepArgs& a, int cus, int waves);
 // random_agent=False with auto-reset: reset the boards the step just finished (a.done),
 // drawing their layouts from the shared numpy stream now (same stream, after the step).
 hipError_t launch_autoreset(const StepArgs& a, hipStream_t s);

@@ -115,6 +115,19 @@ __device__ __forceinline__ void sst(T* p, T v) {
   }
 }
 
+// The step of one board runs in one wave: its LDS hand-offs between lanes need the
+// wave's LDS operations drained and the compiler kept from moving memory accesses
+// across, not a workgroup barrier -- so the small-batch kernel can give a board a
+// second wave that waits at one real barrier for the observation (td_step_kernel_small2).
+__device__ __forceinline__ void wsync() {
+#ifdef TD_WSYNC_BARRIER  // A/B builds: a workgroup barrier (one-wave workgroups only)
+  __syncthreads();
+#else
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+#endif
+}
+
 // ---------------------------------------------------------------------------
 // per-board LDS image
 // ---------------------------------------------------------------------------
@@ -145,6 +158,7 @@ struct alignas(16) Smem {
       float d9[64];       // channel 9 by distance (road length < 2L <= 64)
     };
   };
+  uint32_t obs_go, obs_any;  // td_step_kernel_small2: the stepping wave tells the second one to write
   TdDevCfg cfg;           // constant block, staged once per board: per-lane table lookups hit LDS
 };
 
@@ -348,7 +362,7 @@ __device__ __forceinline__ void diamond(Smem<NC>& S, const Ctx& x, int cell, int
       S.cell[r * L + c] = (w & 0x00ffffffu) | ((uint32_t)(cnt & 0xff) << 24);
     }
   }
-  __syncthreads();
+  wsync();
 }
 
 template <int NC>
@@ -365,7 +379,7 @@ __device__ __forceinline__ int tower_build(Smem<NC>& S, U& u, const Ctx& x, int 
   u.nt += 1;
   u.cost_def = dsub(u.cost_def, price);                   // :238
   u.cells_dirty = true;
-  __syncthreads();
+  wsync();
   diamond(S, x, cell, +1);                                // :239-245
   return FC_OK;
 }
@@ -386,13 +400,13 @@ __device__ __forceinline__ int tower_lvup(Smem<NC>& S, U& u, const Ctx& x, int c
   if (lv >= x.C.max_tower_lv) return FC_LVMAX;            // :252
   double price = x.C.t_price[t][lv + 1];                  // :256
   if (u.cost_def < price) return FC_COST;
-  __syncthreads();
+  wsync();
   if (x.lane == 0) {
     S.tInf[k] = tw_pack(cell, t, lv + 1, tw_ec(ti), x.ep);
     S.twr[cell] = (uint8_t)(0x80 | ((lv + 1) << 2) | t);
   }
   u.cost_def = dsub(u.cost_def, price);                   // :266
-  __syncthreads();
+  wsync();
   return FC_OK;
 }
 
@@ -414,11 +428,11 @@ __device__ __forceinline__ int tower_destruct(Smem<NC>& S, U& u, const Ctx& x, i
   double vc = 0.0;
   int j = x.lane;
   if (j >= k && j + 1 < u.nt) { vi = S.tInf[j + 1]; vc = S.tCd[j + 1]; }
-  __syncthreads();
+  wsync();
   if (j >= k && j + 1 < u.nt) { S.tInf[j] = vi; S.tCd[j] = vc; }
   if (x.lane == 0) S.twr[cell] = 0;
   u.nt -= 1;
-  __syncthreads();
+  wsync();
   diamond(S, x, cell, -1);                                // :281-287
   return FC_OK;
 }
@@ -448,7 +462,7 @@ __device__ __forceinline__ void defender_scan(Smem<NC>& S, U& u, const Ctx& x, c
   uint8_t* real = &S.grp[1][0];
   uint32_t* fw = reinterpret_cast<uint32_t*>(flag);
   for (int i = x.lane; i < (2 * NC) / 4; i += 64) fw[i] = 0u;  // grp[0] and grp[1]
-  __syncthreads();
+  wsync();
   bool bad = false;
   if ((ncr & 1) == 0 && (reinterpret_cast<uintptr_t>(A) & 15u) == 0) {  // 16-B units of two cells of one plane
     typedef long long i64x2 __attribute__((ext_vector_type(2)));
@@ -483,7 +497,7 @@ __device__ __forceinline__ void defender_scan(Smem<NC>& S, U& u, const Ctx& x, c
     }
   }
   if (ballot(bad)) u.flags |= FLAG_BAD_ACTION;
-  __syncthreads();
+  wsync();
   for (int base = 0; base < ncr && active; base += 64) {
     const int cell = base + x.lane;
     const bool valid = cell < ncr;
@@ -523,7 +537,7 @@ __device__ __forceinline__ void defender_scan(Smem<NC>& S, U& u, const Ctx& x, c
       last = j;
     }
   }
-  __syncthreads();
+  wsync();
   if (R) {
     if ((ncr & 1) == 0 && (reinterpret_cast<uintptr_t>(R) & 15u) == 0) {
       typedef long long i64x2 __attribute__((ext_vector_type(2)));
@@ -645,11 +659,11 @@ __device__ __forceinline__ double board_step(Smem<NC>& S, U& u, const Ctx& x, co
       if (kj < key[s] || (kj == key[s] && j < i)) rank[s] += 1;
     }
   }
-  __syncthreads();
+  wsync();
 #pragma unroll
   for (int s = 0; s < 2; ++s)
     if (val[s]) { S.eLP[rank[s]] = lp[s]; S.eMg[rank[s]] = mg[s]; S.eInf[rank[s]] = inf[s]; }
-  __syncthreads();
+  wsync();
   // lane owns sorted enemies lane and lane + 64
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
@@ -759,7 +773,7 @@ __device__ __forceinline__ double board_step(Smem<NC>& S, U& u, const Ctx& x, co
   const uint64_t k0 = ballot(keep0), k1 = ballot(keep1);
   const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   const int n2 = popc64(k0) + popc64(k1);
-  __syncthreads();
+  wsync();
   if (keep0) { int d = popc64(k0 & lt); S.eLP[d] = lp[0]; S.eMg[d] = mg[0]; S.eInf[d] = inf[0]; }
   if (keep1) { int d = popc64(k0) + popc64(k1 & lt); S.eLP[d] = lp[1]; S.eMg[d] = mg[1]; S.eInf[d] = inf[1]; }
   u.n = n2;
@@ -770,7 +784,7 @@ __device__ __forceinline__ double board_step(Smem<NC>& S, U& u, const Ctx& x, co
   else rate = dadd(dmul(C.atk_init_rate, dsub(1.0, u.progress)), dmul(C.atk_final_rate, u.progress));
   u.cost_atk = pymin(dadd(u.cost_atk, rate), u.max_cost);  // self.max_cost (:352-353)
   u.cost_def = pymin(dadd(u.cost_def, C.def_rate), u.max_cost);
-  __syncthreads();
+  wsync();
   // the enemy list is final for this step: write it back now (its LDS is reused by the stats)
   const size_t eb = (size_t)b * ECAP;
   for (int i = lane; i < n2; i += 64) {
@@ -837,7 +851,7 @@ __device__ __forceinline__ void enemy_stats(Smem<NC>& S, const U& u, const Ctx& 
       S.grp[key[s] >> 12][key[s] & 0xfffu] = (uint8_t)i;
     }
   }
-  __syncthreads();
+  wsync();
 }
 
 // Channel 9 by distance (per episode): s[9] = map[4] / (max(map[4]) + 1), an
@@ -863,7 +877,7 @@ __device__ __forceinline__ void channel_scalars(Smem<NC>& S, const U& u, const C
     S.chv[l] = v;
   }
   d9_table(S, u.maxdist, l);
-  __syncthreads();
+  wsync();
 }
 
 
@@ -903,7 +917,7 @@ __device__ __forceinline__ void pack_obs_cells(Smem<NC>& S, const Ctx& x) {
     const uint32_t w = S.cell[i];
     S.cell[i] = cell_bits(w, S.twr[i]) | ((uint32_t)cw_dir(w) << 21) | ((uint32_t)cw_dist(w) << 24);
   }
-  __syncthreads();
+  wsync();
 }
 
 template <int NC>
@@ -1025,11 +1039,11 @@ constexpr uint64_t kChConst = kChAll & ~(kChBin | kChD9 | kChEnemy);
 // batch's observation fits the 256-MiB Infinity Cache (scripts/storepol.hip at 8,192
 // boards, 147 MB: 21.8 us sc1, 30.0 us nt; at 65,536 boards, 1.18 GB, nt whole lines
 // are the fastest form, with the two lines shared with the neighbours sc1).
-template <int NC, int LT, int G = 4>
+template <int NC, int LT, int KB = 0, int KE = -1, int G = 4>
 __device__ __forceinline__ void write_obs_lines(const Smem<NC>& S, int lane, float* out, bool any_enemy, bool wt) {
   static_assert(LT >= 8, "a 128-B line spans at most two channel planes");
   constexpr int Q = LT * LT / 4, N4 = NCH * Q;
-  constexpr int K = (N4 + 7 + 63) / 64;  // windows holding units of the board
+  constexpr int K = KE >= 0 ? KE : (N4 + 7 + 63) / 64;  // windows [KB, K) of the board's (N4 + 7 + 63) / 64
   constexpr uint32_t OOB = 0x80000000u;  // beyond the buffer's num_records: store dropped
   const char* const sb = reinterpret_cast<const char*>(&S);
   const int o_cell = (int)(reinterpret_cast<const char*>(S.cell) - sb);  // packed cell words (pack_obs_cells)
@@ -1041,13 +1055,13 @@ __device__ __forceinline__ void write_obs_lines(const Smem<NC>& S, int lane, flo
   const int head = mis ? 8 - mis : 0, tail = ((N4 + mis) & ~7) - mis;   // [0, head), [tail, N4): shared lines
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(out, 0, N4 * 16, 0x00020000);
   const int i0 = lane - mis;
-  for (int k0 = 0; k0 < K; k0 += G) {
+  for (int k0 = KB; k0 < K; k0 += G) {
     uint4 A[G];
     uint32_t W[G];
 #pragma unroll
     for (int j = 0; j < G; ++j) {
       const int k = k0 + j;
-      if (K % G == 0 || k < K) {
+      if ((K - KB) % G == 0 || k < K) {
         int i = i0 + 64 * k;
         i = i < 0 ? 0 : (i > N4 - 1 ? N4 - 1 : i);
         const int ch = i / Q, q = i - ch * Q;
@@ -1063,7 +1077,7 @@ __device__ __forceinline__ void write_obs_lines(const Smem<NC>& S, int lane, flo
 #pragma unroll
     for (int j = 0; j < G; ++j) {
       const int k = k0 + j;
-      if (!(K % G == 0 || k < K)) continue;
+      if (!((K - KB) % G == 0 || k < K)) continue;
       // the window's channels (wave-uniform)
       const int ulo = 64 * k - mis, uhi = ulo + 63;
       const int clo = (ulo < 0 ? 0 : ulo) / Q, chi = (uhi > N4 - 1 ? N4 - 1 : uhi) / Q;
@@ -1087,23 +1101,25 @@ __device__ __forceinline__ void write_obs_lines(const Smem<NC>& S, int lane, flo
 #pragma unroll
         for (int c = 0; c < 4; ++c) v[c] = 0.0f;
       } else {
-        float t[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-        if ((chm & kChD9) != 0 || ((chm & kChEnemy) != 0 && any_enemy)) {
-          // channel 9 by distance, enemy stats by the cell's group head
+        // a window of several channel kinds: each lane takes its own channel's path
+        // (a select over every kind's value measured 1.5 % slower at 8,192 boards)
+        if (isbin) {
+#pragma unroll
+          for (int c = 0; c < 4; ++c) v[c] = (float)((a4[c] >> (ch & 31)) & 1u);
+        } else if (isd9) {  // channel 9 by distance
+#pragma unroll
+          for (int c = 0; c < 4; ++c) v[c] = *reinterpret_cast<const float*>(sb + o_d9 + 4 * (int)(a4[c] >> 24));
+        } else if (isen && any_enemy) {  // enemy stats by the cell's group head
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
-            const uint32_t g = (W[j] >> (8 * c)) & 0x7fu;
-            const int to = isd9 ? o_d9 + 4 * (int)(a4[c] >> 24) : o_gst + 16 * (int)g + 4 * ((e >> 2) & 3);
-            t[c] = *reinterpret_cast<const float*>(sb + to);
+            const uint32_t g = (W[j] >> (8 * c)) & 0xffu;
+            const float f = *reinterpret_cast<const float*>(sb + o_gst + 16 * (int)(g & 0x7fu) + 4 * ((e >> 2) & 3));
+            v[c] = g != 0xffu ? f : 0.0f;
           }
-        }
-        const float cv = __uint_as_float(W[j]);
+        } else {
+          const float cv = isen ? 0.0f : __uint_as_float(W[j]);
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          const bool grp_here = any_enemy && ((W[j] >> (8 * c)) & 0xffu) != 0xffu;
-          const float ev = grp_here ? t[c] : 0.0f;
-          const float bv = (float)((a4[c] >> (ch & 31)) & 1u);
-          v[c] = isbin ? bv : isd9 ? t[c] : isen ? ev : cv;
+          for (int c = 0; c < 4; ++c) v[c] = cv;
         }
       }
       const bool shared = i < head || i >= tail;  // a line shared with a neighbouring board
@@ -1124,7 +1140,7 @@ __device__ __forceinline__ void write_obs_lines(const Smem<NC>& S, int lane, flo
 // board load / reset / store
 // ---------------------------------------------------------------------------
 // The inputs of one board step, all loads issued before any is waited on.
-// Lane l holds enemy slot l (l < PF_EN), tower slot l (l < PF_TW), cells l and l + 64, and one word
+// Lane l holds enemy slot l (l < PFE), tower slot l (l < PFT), cells l and l + 64, and one word
 // of `w`: lanes 0-23 the header, 24-25 the discrete defender action, 26-37 the
 // opponent stream's hot record.
 struct Prefetch {
@@ -1132,23 +1148,28 @@ struct Prefetch {
   uint4 c4;  // cells 4 lane .. 4 lane + 3 (board of L*L % 4 == 0), else cells lane and lane + 64 in .x / .y
   uint32_t inf, tinf, w;
 };
-#ifndef TD_PF_TW
-#define TD_PF_TW 16
+// PFE / PFT: enemy / tower slots fetched speculatively with the header (template
+// arguments below).  The small-batch kernel (latency-bound) takes 16 of each up front;
+// the large-batch kernel (HBM-bound) takes none and loads exactly the live slots once
+// the header's counts are in (one dependent round trip, hidden by the other waves).
+#ifndef TD_LARGE_PF
+#define TD_LARGE_PF 0
 #endif
-constexpr int PF_ACT = 24, PF_HOT = 26, PF_EN = 16, PF_TW = TD_PF_TW;
+constexpr int PF_ACT = 24, PF_HOT = 26, PF_SMALL = 16, PF_LARGE = TD_LARGE_PF;
 static_assert(offsetof(TdHdr, steps) == 24 && offsetof(TdHdr, start_cell) == 56 && offsetof(TdHdr, episodes) == 76 &&
                   offsetof(TdHdr, max_cost) == 80 && offsetof(TdHdr, max_base_LP) == 88,
               "Prefetch header word map");
 
+template <int PFE, int PFT>
 __device__ __forceinline__ void prefetch_issue(Prefetch& P, const StepArgs& a, int b, int lane, int ncr,
                                                bool want_act) {
   const size_t eb = (size_t)b * ECAP, tb = (size_t)b * TCAP, cb = (size_t)b * ncr;
-  if (lane < PF_EN) {  // enemy slots beyond PF_EN (rare) load after the header
+  if (lane < PFE) {  // enemy slots beyond PFE load after the header
     P.lp = a.en_lp[eb + lane];
     P.mg = a.en_mg[eb + lane];
     P.inf = a.en_inf[eb + lane];
   }
-  if (lane < PF_TW) {  // tower slots beyond PF_TW load after the header
+  if (lane < PFT) {  // tower slots beyond PFT load after the header
     P.tcd = a.tw_cd[tb + lane];
     P.tinf = a.tw_inf[tb + lane];
   }
@@ -1173,7 +1194,7 @@ __device__ __forceinline__ double lane_f64(uint32_t v, int l) {
 }
 
 // Commit the prefetched inputs of board b into the LDS image and the scalar state.
-template <int NC>
+template <int NC, int PFE, int PFT>
 __device__ __forceinline__ void load_board(Smem<NC>& S, U& u, const Ctx& x, const StepArgs& a, int b, const Prefetch& P) {
   const size_t eb = (size_t)b * ECAP, cb = (size_t)b * x.NCr;
   if ((x.NCr & 3) == 0) {
@@ -1216,12 +1237,12 @@ __device__ __forceinline__ void load_board(Smem<NC>& S, U& u, const Ctx& x, cons
   u.max_cost = lane_f64(P.w, 20); u.max_base_LP = (int)lane_word(P.w, 22);
   u.progress = ddiv((double)u.steps, (double)x.C.max_episode_steps);
   u.cells_dirty = false;
-  if (x.lane < u.n && x.lane < PF_EN) { S.eLP[x.lane] = P.lp; S.eMg[x.lane] = P.mg; S.eInf[x.lane] = P.inf; }
-  for (int i = PF_EN + x.lane; i < u.n; i += 64) { S.eLP[i] = a.en_lp[eb + i]; S.eMg[i] = a.en_mg[eb + i]; S.eInf[i] = a.en_inf[eb + i]; }
+  if (x.lane < u.n && x.lane < PFE) { S.eLP[x.lane] = P.lp; S.eMg[x.lane] = P.mg; S.eInf[x.lane] = P.inf; }
+  for (int i = PFE + x.lane; i < u.n; i += 64) { S.eLP[i] = a.en_lp[eb + i]; S.eMg[i] = a.en_mg[eb + i]; S.eInf[i] = a.en_inf[eb + i]; }
   uint32_t tinf = P.tinf;
   if (x.lane < u.nt) {
     double tcd = P.tcd;
-    if (x.lane >= PF_TW) {
+    if (x.lane >= PFT) {
       const size_t tb = (size_t)b * TCAP;
       tcd = a.tw_cd[tb + x.lane];
       tinf = a.tw_inf[tb + x.lane];
@@ -1229,10 +1250,10 @@ __device__ __forceinline__ void load_board(Smem<NC>& S, U& u, const Ctx& x, cons
     S.tCd[x.lane] = tcd;
     S.tInf[x.lane] = tinf;
   }
-  __syncthreads();
+  wsync();
   if (x.lane < u.nt)
     S.twr[tinf & 0xfffu] = (uint8_t)(0x80u | (((tinf >> 14) & 1u) << 2) | ((tinf >> 12) & 3u));
-  __syncthreads();
+  wsync();
 }
 
 // Fresh board from a layout record (TDGymBasic.reset :43-53, TDBoard.__init__ :14-79).
@@ -1250,7 +1271,7 @@ __device__ __forceinline__ void reset_board(Smem<NC>& S, U& u, const Ctx& x, con
   u.max_cost = C.max_cost; u.max_base_LP = C.base_LP;  // TDBoard(max_cost, base_LP) from config at reset
   u.atk_cd = 0; u.def_cd = 0; u.n = 0; u.nt = 0; u.ep_ret = 0.0;
   u.cells_dirty = true;
-  __syncthreads();
+  wsync();
 }
 
 // Cell words back to HBM when map[6] changed or a new layout was loaded (before
@@ -1297,7 +1318,7 @@ __device__ __forceinline__ void opponent_enemy(Smem<NC>& S, U& u, const Ctx& x, 
     types = t * 0x11111111u;
   }
   summon_cluster(S, u, x, types, road, nullptr);
-  __syncthreads();
+  wsync();
   u.atk_cd = x.C.atk_interval;  // the (ok, real) tuple is always truthy
 }
 
@@ -1327,11 +1348,11 @@ __device__ __forceinline__ void build_near_road(Smem<NC>& S, U& u, const Ctx& x,
     if (isr) cells[nroad + popc64(m & lt)] = (uint16_t)c;
     nroad += popc64(m);
   }
-  __syncthreads();
+  wsync();
   for (int i = nroad - 1; i >= 1; --i) {
     int j = (int)R.shuffle_j(i);
     if (x.lane == 0) { uint16_t tmp = cells[i]; cells[i] = cells[j]; cells[j] = tmp; }
-    __syncthreads();
+    wsync();
   }
   if (draw_type) t = (int)R.ri(0, 3);
   for (int i = 0; i < nroad; ++i) {
@@ -1407,7 +1428,7 @@ __device__ __forceinline__ void attacker_actions(Smem<NC>& S, U& u, const Ctx& x
     if (x.lane < 24) { int64_t v = a.atk_act[(size_t)b * 24 + x.lane]; bad = v < 0 || v > 4; }
     if (ballot(bad)) u.flags |= FLAG_BAD_ACTION;
   }
-  __syncthreads();
+  wsync();
   if (u.atk_cd != 0) return;
   for (int i = 0; i < u.num_roads; ++i) {
     uint32_t cl = 0;
@@ -1430,7 +1451,7 @@ __device__ __forceinline__ void attacker_actions(Smem<NC>& S, U& u, const Ctx& x
       }
       if (x.lane == 0) S.fail_atk[i] = fc;
     }
-    __syncthreads();
+    wsync();
   }
 }
 
@@ -1442,7 +1463,14 @@ __device__ __forceinline__ void attacker_actions(Smem<NC>& S, U& u, const Ctx& x
 // the observation lines are stored write-through (write_obs_lines).  (Storing the
 // layout and tower planes at the start of the step, before the step logic, was
 // measured slower at 4,096 and 8,192 boards: 36.3 / 53.1 vs 25.7 / 38.3 us.)
-template <int NC, int LT, int MODE, bool SCAN, bool SMALL>
+// Observation windows written by the stepping wave of a two-wave board (the first half).
+template <int LT>
+__host__ __device__ constexpr int obs_half() { return ((NCH * LT * LT / 4 + 7 + 63) / 64 + 1) / 2; }
+
+// SPLIT: the board's workgroup has a second wave (td_step_kernel_small2) that waits at
+// the one workgroup barrier of this path and then writes the second half of the
+// observation windows.
+template <int NC, int LT, int MODE, bool SCAN, bool SMALL, bool SPLIT = false>
 __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const StepArgs& a, int b, const Prefetch& P) {
   const TdDevCfg& C = x.C;
   uint32_t* const opp = a.opp_mt + (size_t)b * OPP_WORDS;
@@ -1450,7 +1478,8 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
   U u;
   STAMP_RT(9);
   STAMP(0);
-  load_board(S, u, x, a, b, P);
+  constexpr int PF = SMALL ? PF_SMALL : PF_LARGE;
+  load_board<NC, PF, PF>(S, u, x, a, b, P);
   const int64_t act_in = (int64_t)(((uint64_t)lane_word(P.w, PF_ACT + 1) << 32) | lane_word(P.w, PF_ACT));
   // built-in opponent stream: position, lazy-twist boundary and the next draws
   // (pre-computed by the previous step) come from the board's hot record
@@ -1469,6 +1498,10 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
       a.reward[b] = 0.0;
       a.done[b] = 1;
       if (a.win) a.win[b] = -1;
+    }
+    if constexpr (SPLIT) {
+      if (x.lane == 0) S.obs_go = 0u;
+      __syncthreads();
     }
     return;
   }
@@ -1516,7 +1549,7 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
   pack_obs_cells(S, x);
   // pre-draw the next step's words: loads issued now, consumed at the end of the step
   if (MODE != MODE_2P) R.prefetch_issue(x.lane);
-  __syncthreads();
+  wsync();
   STAMP(2);
 
   // ---- TDBoard.step
@@ -1609,7 +1642,11 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
   if (MODE != MODE_2P && x.lane < 8) sst(&hot[4 + x.lane], R.cache);
   // the observation last: nothing of the step is live any more, the writer has the registers
   STAMP(6);
-  if constexpr (LT != 0) {
+  if constexpr (SPLIT) {
+    if (x.lane == 0) { S.obs_go = 1u; S.obs_any = u.n > 0 ? 1u : 0u; }
+    __syncthreads();  // the second wave writes windows [KH, K)
+    write_obs_lines<NC, LT, 0, obs_half<LT>()>(S, x.lane, obs, u.n > 0, wt);
+  } else if constexpr (LT != 0) {
     if ((reinterpret_cast<uintptr_t>(a.obs) & 15u) == 0) {
 #ifndef TD_DIAG_NO_OBS  // diagnostic builds only: the step without its observation
       write_obs_lines<NC, LT>(S, x.lane, obs, u.n > 0, wt);
@@ -1641,7 +1678,8 @@ __device__ __forceinline__ void step_kernel_body(const StepArgs& a) {
   const int L = LT ? LT : a.L;
   const Ctx x{S.cfg, L, L * L, (int)threadIdx.x, a.cfgs, a.epoch};
   Prefetch P;
-  prefetch_issue(P, a, b, x.lane, x.NCr, MODE != MODE_ATK && !a.multi);
+  constexpr int PF = SMALL ? PF_SMALL : PF_LARGE;
+  prefetch_issue<PF, PF>(P, a, b, x.lane, x.NCr, MODE != MODE_ATK && !a.multi);
   step_board<NC, LT, MODE, SCAN, SMALL>(S, x, a, b, P);
 }
 
@@ -1665,6 +1703,30 @@ __global__ __launch_bounds__(64) TD_SMALL_ATTR void td_step_kernel_small(StepArg
   step_kernel_body<LT, MODE, SCAN, true>(a);
 }
 
+// Batches up to half the resident waves: two waves per board.  The first steps the board
+// as in td_step_kernel_small; the second waits at one barrier and writes the second half
+// of the observation windows beside it, which shortens a board's critical path where the
+// batch leaves issue slots free (4,096 boards: 8,192 waves, 8 per SIMD).
+template <int LT, int MODE, bool SCAN>
+__global__ __launch_bounds__(128) TD_SMALL_ATTR void td_step_kernel_small2(StepArgs a) {
+  constexpr int NC = LT * LT;
+  __shared__ Smem<NC> S;
+  const int b = blockIdx.x;
+  if (b >= a.B) return;
+  const int lane = (int)threadIdx.x & 63;
+  if (threadIdx.x < 64) {
+    stage_cfg(S, a.cfg);
+    const Ctx x{S.cfg, LT, NC, lane, a.cfgs, a.epoch};
+    Prefetch P;
+    prefetch_issue<PF_SMALL, PF_SMALL>(P, a, b, lane, NC, MODE != MODE_ATK && !a.multi);
+    step_board<NC, LT, MODE, SCAN, true, true>(S, x, a, b, P);
+  } else {
+    __syncthreads();
+    if (S.obs_go)
+      write_obs_lines<NC, LT, obs_half<LT>()>(S, lane, a.obs + (size_t)b * NCH * NC, S.obs_any != 0u, a.obs_wt != 0);
+  }
+}
+
 // The built-in opponents called on their own, between steps (TDGymBasic.py:81-292,
 // called directly by demo.py:78-79): random_enemy_lv{0,1} (side 0) or
 // random_tower_lv{0,1,2} (side 1) for every masked board, on the board's opponent
@@ -1680,9 +1742,9 @@ __global__ __launch_bounds__(64) void td_opponent_kernel(StepArgs a, int side, i
   const int L = LT ? LT : a.L;
   const Ctx x{S.cfg, L, L * L, (int)threadIdx.x, a.cfgs, a.epoch};
   Prefetch P;
-  prefetch_issue(P, a, b, x.lane, x.NCr, false);
+  prefetch_issue<PF_SMALL, PF_SMALL>(P, a, b, x.lane, x.NCr, false);
   U u;
-  load_board(S, u, x, a, b, P);
+  load_board<NC, PF_SMALL, PF_SMALL>(S, u, x, a, b, P);
   if (u.num_roads < 1 || u.num_roads > 3) return;  // never reset: nothing to act on
   uint32_t* const hot = a.opp_hot + (size_t)b * HOT_WORDS;
   WaveMt R{a.opp_mt + (size_t)b * OPP_WORDS, lane_word(P.w, PF_HOT + 0), lane_word(P.w, PF_HOT + 1)};
@@ -1964,30 +2026,46 @@ static hipError_t launch2(const StepArgs& a, hipStream_t s, bool reset, hipEvent
     if (ev0) hipExtLaunchKernelGGL(k, dim3(a.B), dim3(64), 0, s, ev0, ev1, 0, a);       \
     else hipLaunchKernelGGL(k, dim3(a.B), dim3(64), 0, s, a);                           \
   } while (0)
-  if (reset) hipLaunchKernelGGL(td_reset_kernel<LT>, dim3(a.B), dim3(64), 0, s, a);
-  else if (LT != 0 && a.small && (reinterpret_cast<uintptr_t>(a.obs) & 15u) == 0) TD_STEP_DISPATCH(td_step_kernel_small, LT, a, TD_LAUNCH);
-  else TD_STEP_DISPATCH(td_step_kernel, LT, a, TD_LAUNCH);
+#define TD_LAUNCH2(k)                                                                    \
+  do {                                                                                   \
+    if (ev0) hipExtLaunchKernelGGL(k, dim3(a.B), dim3(128), 0, s, ev0, ev1, 0, a);       \
+    else hipLaunchKernelGGL(k, dim3(a.B), dim3(128), 0, s, a);                           \
+  } while (0)
+  const bool aligned = (reinterpret_cast<uintptr_t>(a.obs) & 15u) == 0;
+  if (reset) {
+    hipLaunchKernelGGL(td_reset_kernel<LT>, dim3(a.B), dim3(64), 0, s, a);
+  } else if constexpr (LT != 0) {
+    if (a.small == 2 && aligned) TD_STEP_DISPATCH(td_step_kernel_small2, LT, a, TD_LAUNCH2);
+    else if (a.small && aligned) TD_STEP_DISPATCH(td_step_kernel_small, LT, a, TD_LAUNCH);
+    else TD_STEP_DISPATCH(td_step_kernel, LT, a, TD_LAUNCH);
+  } else {
+    TD_STEP_DISPATCH(td_step_kernel, LT, a, TD_LAUNCH);
+  }
 #undef TD_LAUNCH
+#undef TD_LAUNCH2
   return hipGetLastError();
 }
 
 // Step-kernel workgroups (boards) resident at once on the device: the batch size up
 // to which a step runs as one round of waves (td_step_kernel_small).
 template <int LT>
-static int resident3(const StepArgs& a, int cus) {
+static int resident3(const StepArgs& a, int cus, int waves) {
   int n = 0;
   hipError_t e = hipErrorInvalidValue;
 #define TD_OCC(k) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, 64, 0)
-  TD_STEP_DISPATCH(td_step_kernel_small, LT, a, TD_OCC);
+#define TD_OCC2(k) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, 128, 0)
+  if (waves == 2) TD_STEP_DISPATCH(td_step_kernel_small2, LT, a, TD_OCC2);
+  else TD_STEP_DISPATCH(td_step_kernel_small, LT, a, TD_OCC);
 #undef TD_OCC
+#undef TD_OCC2
   return e == hipSuccess ? n * cus : 0;
 }
 
-int step_resident_boards(const StepArgs& a, int cus) {
+int step_resident_boards(const StepArgs& a, int cus, int waves) {
   switch (a.L) {
-    case 10: return resident3<10>(a, cus);
-    case 20: return resident3<20>(a, cus);
-    case 30: return resident3<30>(a, cus);
+    case 10: return resident3<10>(a, cus, waves);
+    case 20: return resident3<20>(a, cus, waves);
+    case 30: return resident3<30>(a, cus, waves);
     default: return 0;  // generic-L kernels: no small-batch build
   }
 }
