@@ -125,7 +125,12 @@ class _TDBasic(object):
         self.reset()
 
     def seed(self, seed=None):
-        """TDGymBasic.seed (:30-32): the layout stream becomes RandomState(seed)."""
+        """TDGymBasic.seed (:30-32): the layout stream becomes RandomState(seed).
+
+        The reference calls gym's ``seeding.np_random(seed)``, which in gym <= 0.21
+        hashes the seed before seeding; this build (like the golden generator's gym
+        stub) seeds RandomState(seed) directly -- a documented deviation,
+        parity unpinned since gym is not importable here."""
         if seed is None:
             seed = _new_seed()
         self._engine.set_np_state(0, np.random.RandomState(seed).get_state())
