@@ -49,7 +49,11 @@ int fail(const char* fmt, ...) {
 // steps, no ring dry).
 constexpr int kRefillEvery = 4;
 constexpr int kRefillWaves = 1024;
-constexpr int kWalksPerStep = 12;  // a pending draw advances 12 walks per step of refill interval (48 at 4)
+// A pending draw advances 3 walks per step of refill interval (12 per launch at 4): the
+// fewer walks a refill wave runs per launch, the less it holds a wave slot the next
+// step's waves need (8,192 boards: 37.9 us per step at 48 walks, 36.5 at 12, 36.6 at 4,
+// 36.9 at 1; 34.3 without refills, profiles/r02/s21_session.log).
+constexpr int kWalksPerStep = 3;
 constexpr int kSideStreams = 2;  // refill streams: one stuck on a long draw does not stall the next (the HIP
                                  // runtime has 4 hardware queues per process; the step stream needs one)
 
@@ -86,6 +90,7 @@ struct td_handle {
   int refill_every = kRefillEvery;  // 0: no refill launches (td_set_refill_interval)
   int refill_waves = kRefillWaves;  // waves per refill launch
   int refill_nowait = 0, n_side = kSideStreams;  // A/B knobs (TD_REFILL_NOWAIT, TD_SIDE_STREAMS)
+  int refill_walks = 0;  // walks per board per refill launch (0: 12 per step of interval; TD_REFILL_WALKS)
   // td_kernel_timing: event pairs bound to the next `tev_cap` step-kernel dispatches
   std::vector<hipEvent_t> tev;
   int tev_cap = 0, tev_n = 0, tev_every = 1;
@@ -174,7 +179,8 @@ StepArgs base_args(td_handle* h) {
   a.lay_head = h->d_lay_head; a.lay_tail = h->d_lay_tail; a.lay_claim = h->d_lay_claim;
   a.slot_words = slot_words(h->L);
   a.refill_grp = refill_group(h->B, h->refill_waves);
-  a.refill_walks = kWalksPerStep * (h->refill_every > 0 ? h->refill_every : kRefillEvery);
+  a.refill_waves = h->refill_waves;
+  a.refill_walks = h->refill_walks > 0 ? h->refill_walks : kWalksPerStep * (h->refill_every > 0 ? h->refill_every : kRefillEvery);
   a.reset_fail = h->d_fail; a.cfg = h->d_cfg + h->epoch; a.cfgs = h->d_cfg; a.epoch = h->epoch;
   return a;
 }
@@ -390,6 +396,7 @@ td_handle* td_create(const td_config* cfg, int map_size, int n_boards, int mode,
     if (const char* e = std::getenv("TD_REFILL_EVERY")) h->refill_every = std::max(0, std::atoi(e));  // A/B runs
     if (const char* e = std::getenv("TD_REFILL_WAVES")) h->refill_waves = std::max(1, std::atoi(e));
     if (const char* e = std::getenv("TD_REFILL_NOWAIT")) h->refill_nowait = std::atoi(e) ? 1 : 0;
+    if (const char* e = std::getenv("TD_REFILL_WALKS")) h->refill_walks = std::max(1, std::atoi(e));
     if (const char* e = std::getenv("TD_SIDE_STREAMS")) h->n_side = std::min(kSideStreams, std::max(1, std::atoi(e)));
   }
   std::vector<uint32_t> seeds(B);

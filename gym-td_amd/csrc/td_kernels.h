@@ -36,7 +36,8 @@ struct StepArgs {
   uint32_t* lay_tail;   // [B]
   uint32_t* lay_claim;  // [B] 1 while a refill wave draws the board's layouts
   int slot_words;
-  int refill_grp;       // boards scanned per refill wave (refill_group)
+  int refill_grp;       // boards scanned per refill wave per pass (refill_group)
+  int refill_waves;     // waves per refill launch (each walks ceil(B / refill_grp / refill_waves) groups)
   int refill_walks;     // walks per board per refill launch (a draw resumes in the next launch)
   uint8_t* scratch;     // [B][scratch_stride] a pending layout draw: RoadResume header + generator arrays
   size_t scratch_stride;

@@ -1788,14 +1788,315 @@ hipError_t launch_opponent(const StepArgs& a, int side, int level, hipStream_t s
 // episode layouts on the device
 // ---------------------------------------------------------------------------
 // LDS image of one layout draw: the board's numpy stream, the output record,
-// create_road_v2's scratch and the draw's resume state.  Lane 0 runs the (serial)
-// generator entirely out of LDS; the other lanes stage everything in and out.
+// create_road_v2's scratch and the draw's resume state (WaveRoadGen runs on it).
 template <int NC>
 struct LayoutSmem {
   uint32_t mt[OPP_WORDS];
   uint32_t rec[LAYOUT_HDR + NC];
   uint8_t scratch[14 * NC + 64];
   RoadResume res;
+};
+
+// create_road_v2 (TDRoadGen.py:4-199) and TDGymBasic.reset's num_roads draw (:42) run by
+// a whole wave: the device form of td_layout.h RoadGen::draw, draw for draw the same
+// (both are pinned against the reference's road table).  RoadGen on one lane waited on
+// LDS for every stream draw (three dependent words of the lazy twist) and for every
+// move (the field byte); here the stream is a window of 64 tempered outputs in a
+// register, one per lane, refilled 64 at a time with one LDS round trip, and the field
+// / turn maps are bitmaps in registers (lane j holds cells [32j, 32j + 32)), read with
+// v_readlane.  Control flow is wave-uniform.  The road lists stay in LDS (the resumable
+// state); the main road, its branch points and the stamping of a road onto the record
+// run one cell per lane (an accepted road is shorter than 2L <= 64 cells).
+template <int NC>
+struct WaveRoadGen {
+  static constexpr int NW = (NC + 31) / 32;  // bitmap words (at most)
+  uint32_t* mt;   // LDS stream words (LazyMt format: [624] position, [625] lazy-twist boundary)
+  uint32_t* rec;  // LDS record
+  uint32_t* picks;
+  uint16_t *r1, *r2, *rb, *mainr;
+  uint32_t *fieldw, *rotw;  // the bitmaps' resumable copies in the scratch
+  int L, lane;
+  uint32_t pos, tw, base, n, win;
+  uint32_t field, rot;
+
+  // scratch carve for L*L = nc cells: picks u32[nc], r1 / r2 / rb / mainr u16[nc], field / rot
+  // u32[(nc + 31) / 32] -- 12 nc + 8 (nc + 31) / 32 <= road_scratch_bytes(L) bytes
+  __device__ void carve(uint8_t* sc, int nc) {
+    picks = reinterpret_cast<uint32_t*>(sc);
+    r1 = reinterpret_cast<uint16_t*>(sc + 4 * nc);
+    r2 = r1 + nc; rb = r2 + nc; mainr = rb + nc;
+    fieldw = reinterpret_cast<uint32_t*>(sc + 12 * nc);
+    rotw = fieldw + (nc + 31) / 32;
+  }
+
+  // ---- the numpy-legacy stream (LazyMt semantics, 64 words per refill) ----
+  __device__ void refill() {
+    if (pos >= (uint32_t)MT_N) { pos = 0; tw = 0; }
+    base = pos;
+    n = (uint32_t)MT_N - pos < 64u ? (uint32_t)MT_N - pos : 64u;
+    const uint32_t q = base + (uint32_t)lane;
+    const bool mine = (uint32_t)lane < n, lazy = mine && q >= tw;
+    uint32_t y = 0;
+    if (mine) {
+      y = mt[q];
+      if (lazy) {  // new[q] from old[q], old[q + 1] and old[q + 397] / new[q - 227] (< base: done)
+        const uint32_t nb = mt[q == MT_N - 1 ? 0u : q + 1u];
+        const uint32_t far = mt[q < (uint32_t)(MT_N - MT_M) ? q + MT_M : q - (MT_N - MT_M)];
+        const uint32_t yy = (y & 0x80000000u) | (nb & 0x7fffffffu);
+        y = far ^ (yy >> 1) ^ ((yy & 1u) ? 0x9908b0dfu : 0u);
+      }
+    }
+    wsync();  // every lane's old words are read before any new word is stored
+    if (lazy) mt[q] = y;
+    if (base + n > tw) tw = base + n;
+    win = mt_temper(y);
+  }
+  __device__ __forceinline__ uint32_t next() {
+    if (pos - base >= n) refill();
+    const uint32_t r = rdl(win, (int)(pos - base));
+    ++pos;
+    return r;
+  }
+  __device__ int np_randint(int lo, int hi) {  // numpy legacy masked rejection (hi exclusive)
+    if (hi <= lo) return lo;
+    const uint32_t rng = (uint32_t)(hi - lo - 1);
+    if (rng == 0) return lo;
+    uint32_t mask = rng;
+    mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4; mask |= mask >> 8; mask |= mask >> 16;
+    uint32_t v = next() & mask;
+    while (v > rng) v = next() & mask;
+    return lo + (int)v;
+  }
+
+  // ---- field / turn bitmaps ----
+  __device__ __forceinline__ bool bit(uint32_t m, int c) const { return (rdl(m, c >> 5) >> (c & 31)) & 1u; }
+  __device__ __forceinline__ uint32_t with(uint32_t m, int c) const {
+    return m | (lane == (c >> 5) ? 1u << (c & 31) : 0u);
+  }
+  __device__ __forceinline__ uint32_t without(uint32_t m, int c) const {
+    return m & ~(lane == (c >> 5) ? 1u << (c & 31) : 0u);
+  }
+  __device__ __forceinline__ bool inner(int r, int c) const { return r > 0 && r < L - 1 && c > 0 && c < L - 1; }
+
+  // generate_road (TDRoadGen.py:31-119), as RoadGen::walk; *last = the last cell appended
+  __device__ int walk(int r0, int c0, int d, uint16_t* out, int* len, int* last) {
+    int pr = r0, pc = c0, cnt = 0, pending = 0, loop = 0;
+    while (inner(pr, pc) && loop < 100) {
+      ++loop;
+      const int shape = np_randint(0, 2);
+      const int seg = np_randint(L * 3 / 20, L / 4);
+      bool cross = false;
+      auto run = [&](int k_max, int dd, bool reset_cross) {
+        const int dr = dd == 0 ? 1 : dd == 2 ? -1 : 0, dc = dd == 1 ? -1 : dd == 3 ? 1 : 0;  // :15
+        for (int k = 0; k < k_max; ++k) {
+          pr += dr; pc += dc;
+          const int cell = pr * L + pc;
+          if (bit(field, cell)) { pr -= dr; pc -= dc; cross = true; return; }
+          if (reset_cross) cross = false;
+          if (lane == 0) out[cnt] = (uint16_t)cell;
+          ++cnt;
+          field = with(field, cell);
+          if (!inner(pr, pc)) return;
+        }
+      };
+      if (shape <= 0) {
+        run(seg * 2, d, false);
+      } else {
+        run(seg, d, false);
+        if (!inner(pr, pc)) break;
+        int rd;
+        if (pending != 0) { rd = pending; pending = 0; }
+        else { rd = np_randint(0, 2) * 2 - 1; pending = -rd; }
+        rot = with(rot, pr * L + pc);
+        d = (d + 4 + rd) % 4;
+        run(seg, d, true);
+      }
+      if (cross) {  // the free neighbours in direction order, one picked at random
+        const uint32_t fm = (bit(field, (pr + 1) * L + pc) ? 0u : 1u) | (bit(field, pr * L + pc - 1) ? 0u : 2u) |
+                            (bit(field, (pr - 1) * L + pc) ? 0u : 4u) | (bit(field, pr * L + pc + 1) ? 0u : 8u);
+        const int nf = __popc(fm);
+        if (nf == 0) { *len = cnt; *last = pr * L + pc; return 0; }
+        int pick = np_randint(0, nf);
+        uint32_t m = fm;
+        while (pick-- > 0) m &= m - 1;
+        d = __builtin_ctz(m);
+        pending = 0;
+        rot = with(rot, pr * L + pc);
+      }
+    }
+    *len = cnt;
+    *last = pr * L + pc;
+    return loop >= 100 ? 0 : 1;
+  }
+
+  // clean_up (TDRoadGen.py:121-124): field and turn marks of the road's cells cleared
+  __device__ void erase(const uint16_t* road, int cnt) {
+    wsync();
+    for (int i0 = 0; i0 < cnt; i0 += 64) {
+      const uint32_t cv = i0 + lane < cnt ? road[i0 + lane] : 0u;
+      const int m = cnt - i0 < 64 ? cnt - i0 : 64;
+      for (int i = 0; i < m; ++i) {
+        const int c = (int)rdl(cv, i);
+        field = without(field, c);
+        rot = without(rot, c);
+      }
+    }
+  }
+
+  // One road onto the record (TDBoard.py:38-59): lane k < tot holds cell k (`cv`).
+  __device__ void stamp(uint32_t cv, int tot, int ri, uint32_t* maxdist) {
+    uint32_t* cw = rec + LAYOUT_HDR;
+    const int p = (int)cv;
+    const int pn = __shfl((int)cv, lane + 1 < 64 ? lane + 1 : 63);
+    wsync();
+    if (lane < tot) {
+      uint32_t w = cw[p] | 1u | (1u << (1 + ri));
+      w = (w & 0x00ffffffu) | (1u << 24);
+      w = (w & ~(0xffu << 16)) | ((uint32_t)(tot - 1 - lane) << 16);
+      if (lane < tot - 1) {
+        const int dr = pn / L - p / L, dc = pn % L - p % L;
+        const uint32_t dir = dr == 0 ? (dc == 1 ? 0u : 1u) : (dr == 1 ? 2u : 3u);
+        w = (w & ~(3u << 8)) | (dir << 8);
+      }
+      cw[p] = w;
+    }
+    if ((uint32_t)(tot - 1) > *maxdist) *maxdist = (uint32_t)(tot - 1);
+    wsync();
+  }
+
+  __device__ int fail(RoadResume& st, int status) {
+    wsync();
+    if (lane == 0) { rec[0] = 0; rec[1] = st.nr; rec[7] = (uint32_t)status; }
+    st.phase = RP_NEW;
+    return status;
+  }
+
+  static __device__ __forceinline__ int iabs(int x) { return x < 0 ? -x : x; }
+
+  // RoadGen::draw: the same state machine over the same RoadResume; st lives in
+  // registers (wave-uniform), the caller moves it from / to LDS.  pad holds road 1's
+  // last cell.
+  __device__ int draw(RoadResume& st, int budget, int max_attempts) {
+    if (st.phase == RP_NEW) {
+      st.nr = (uint32_t)np_randint(1, 4);  // TDGymBasic.reset :42
+      const int nr = (int)st.nr;
+      if (L < 4 || L > MAX_L || nr < 1 || nr > 3) return fail(st, ROAD_ERR_ARGS);
+      if (L / 4 <= L * 3 / 20) return fail(st, ROAD_ERR_RANDINT);  // segment randint raises (:41)
+      field = 0u; rot = 0u;
+      const int lo = L / 3, hi = (L * 2 + 2) / 3;
+      st.cr = (uint32_t)np_randint(lo, hi);
+      st.cc = (uint32_t)np_randint(lo, hi);
+      field = with(field, (int)(st.cr * L + st.cc));
+      st.d0 = (uint32_t)np_randint(0, 4);
+      st.phase = RP_ROAD1; st.att = 0;
+    }
+    const int cr = (int)st.cr, cc = (int)st.cc, d0 = (int)st.d0;
+    while (st.phase == RP_ROAD1) {  // center -> end, :128-137
+      if ((int)st.att >= max_attempts) return fail(st, ROAD_ERR_BOUND);
+      if (budget-- <= 0) return ROAD_PENDING;
+      ++st.att;
+      int n1 = 0, e1 = 0;
+      const int ok = walk(cr, cc, d0, r1, &n1, &e1);
+      if (!ok || n1 >= L) { erase(r1, n1); continue; }
+      st.n1 = (uint32_t)n1; st.pad = (uint32_t)e1; st.phase = RP_ROAD2; st.att = 0;
+    }
+    while (st.phase == RP_ROAD2) {  // center -> start, :141-155
+      if ((int)st.att >= max_attempts) return fail(st, ROAD_ERR_BOUND);
+      if (budget-- <= 0) return ROAD_PENDING;
+      ++st.att;
+      const int n1 = (int)st.n1;
+      int n2 = 0, e2 = 0;
+      const int ok = walk(cr, cc, (d0 + 2) % 4, r2, &n2, &e2);
+      if (!ok || n1 + n2 + 1 >= L * 2) { erase(r2, n2); continue; }
+      const int e1 = (int)st.pad;
+      if (iabs(e2 / L - e1 / L) + iabs(e2 % L - e1 % L) < L * 3 / 4) { erase(r2, n2); continue; }
+      // main = reversed(road2) + [center] + road1 (:157-158), one cell per lane (nm < 2L)
+      const int nm = n1 + n2 + 1;
+      wsync();
+      uint32_t mv = 0;
+      if (lane < n2) mv = r2[n2 - 1 - lane];
+      else if (lane == n2) mv = (uint32_t)(cr * L + cc);
+      else if (lane < nm) mv = r1[lane - n2 - 1];
+      if (lane < nm) mainr[lane] = (uint16_t)mv;
+      // branch points (:162-170): cells i with no turn at i and i + 1; a turn at i skips i + 1
+      int np = 0;
+      uint32_t pk = 0;
+      for (int i = 0; i < nm;) {
+        const int ci = (int)rdl(mv, i);
+        if (!bit(rot, ci)) {
+          if (i < nm - 1 && !bit(rot, (int)rdl(mv, i + 1))) {
+            if (lane == np) pk = ((uint32_t)i << 16) | (uint32_t)ci;
+            ++np;
+          }
+          i += 1;
+        } else {
+          i += 2;
+        }
+      }
+      if (lane < np) picks[lane] = pk;
+      // map planes from the main road first (roads[0])
+      for (int i = lane; i < L * L; i += 64) rec[LAYOUT_HDR + i] = 0u;
+      uint32_t maxdist = 0;
+      stamp(mv, nm, 0, &maxdist);
+      st.nm = (uint32_t)nm; st.np = (uint32_t)np; st.maxdist = maxdist;
+      st.start[0] = rdl(mv, 0); st.start[1] = st.start[2] = 0;
+      st.endc = rdl(mv, nm - 1);
+      st.phase = RP_BRANCH; st.ri = 1; st.att = 0;
+    }
+    while (st.phase == RP_BRANCH && (int)st.ri < (int)st.nr) {  // :174-197
+      if ((int)st.att >= max_attempts) return fail(st, ROAD_ERR_BOUND);
+      if (budget-- <= 0) return ROAD_PENDING;
+      ++st.att;
+      const int np = (int)st.np, nm = (int)st.nm, endc = (int)st.endc;
+      const int klo = np * 2 / 5, khi = np * 4 / 5;
+      if (khi <= klo) return fail(st, ROAD_ERR_RANDINT);
+      int k = np_randint(klo, khi);
+      const int nd = np_randint(0, 4);
+      wsync();
+      const uint32_t pkv = picks[k];
+      const int bcell = (int)(pkv & 0xffffu);
+      k = (int)(pkv >> 16);
+      int nb = 0, eb = 0;
+      const int ok = walk(bcell / L, bcell % L, nd, rb, &nb, &eb);
+      if (!ok) { erase(rb, nb); continue; }
+      if (nb + nm - k >= L * 2) { erase(rb, nb); continue; }
+      if (nb == 0) return fail(st, ROAD_ERR_EMPTY);
+      if (iabs(eb / L - endc / L) + iabs(eb % L - endc % L) < L * 3 / 4) { erase(rb, nb); continue; }
+      // road = reversed(branch) + main[k:], one cell per lane (< 2L)
+      wsync();
+      const int tot = nb + nm - k;
+      uint32_t cv = 0;
+      if (lane < nb) cv = rb[nb - 1 - lane];
+      else if (lane < tot) cv = mainr[k + lane - nb];
+      wsync();
+      if (lane < nb) rb[lane] = (uint16_t)cv;  // kept reversed, as RoadGen leaves it
+      uint32_t maxdist = st.maxdist;
+      stamp(cv, tot, (int)st.ri, &maxdist);
+      st.maxdist = maxdist;
+      if (st.ri == 1) st.start[1] = rdl(cv, 0);  // (no dynamic index: keeps st in registers)
+      else st.start[2] = rdl(cv, 0);
+      ++st.ri; st.att = 0;
+    }
+    const int nr = (int)st.nr;
+    uint32_t* cw = rec + LAYOUT_HDR;
+    wsync();
+    if (lane == 0) {
+      cw[st.start[0]] |= 1u << 5;
+      if (nr > 1) cw[st.start[1]] |= 1u << 6;
+      if (nr > 2) cw[st.start[2]] |= 1u << 7;
+      cw[st.endc] |= 1u << 4;
+      rec[0] = TD_LAYOUT_MAGIC;
+      rec[1] = (uint32_t)nr;
+      rec[2] = st.endc;
+      rec[3] = st.maxdist;
+      rec[4] = st.start[0];
+      rec[5] = nr > 1 ? st.start[1] : 0u;
+      rec[6] = nr > 2 ? st.start[2] : 0u;
+      rec[7] = ROAD_OK;
+    }
+    st.phase = RP_NEW;
+    return ROAD_OK;
+  }
 };
 
 // Layout draws are resumable (RoadGen::draw): a refill gives each board a budget of
@@ -1836,17 +2137,33 @@ __device__ int wave_layout(LayoutSmem<NC>& G, const StepArgs& a, int b, int retr
     __syncthreads();
   }
   int st = ROAD_ERR_BOUND;
-  if (lane == 0) {
-    LazyMt rng{G.mt, 0, 0};
-    rng.load();
-    RoadGen<LazyMt> g{rng, L, road_scratch_carve(G.scratch, L), kRoadAttempts};
+  {
+    WaveRoadGen<NC> g;
+    g.carve(G.scratch, L * L);
+    g.mt = G.mt; g.rec = G.rec; g.L = L; g.lane = lane;
+    // the stream position and the resume state are wave-uniform: SGPRs
+    g.pos = __builtin_amdgcn_readfirstlane(G.mt[MT_N]);
+    g.tw = __builtin_amdgcn_readfirstlane(G.mt[MT_N + 1]);
+    g.base = g.pos; g.n = 0; g.win = 0;
+    RoadResume res;
+    for (int i = 0; i < 16; ++i)
+      reinterpret_cast<uint32_t*>(&res)[i] = __builtin_amdgcn_readfirstlane(reinterpret_cast<const uint32_t*>(&G.res)[i]);
+    const int nw = (L * L + 31) / 32;
+    if (resumed) {  // the draw's field / turn bitmaps
+      g.field = lane < nw ? g.fieldw[lane] : 0u;
+      g.rot = lane < nw ? g.rotw[lane] : 0u;
+    } else {
+      g.field = g.rot = 0u;
+    }
+#pragma nounroll
     for (int t = 0; t <= retries; ++t) {
-      st = g.draw(G.res, budget, G.rec);
+      st = g.draw(res, budget, kRoadAttempts);
       if (st == ROAD_OK || st == ROAD_PENDING) break;
     }
-    rng.store();
+    __syncthreads();
+    if (lane < nw) { g.fieldw[lane] = g.field; g.rotw[lane] = g.rot; }
+    if (lane == 0) { G.mt[MT_N] = g.pos; G.mt[MT_N + 1] = g.tw; G.res = res; }
   }
-  st = __shfl(st, 0);
   __syncthreads();
   // every store below is write-through (st_relaxed = sc1): the claim release and the
   // tag store publish them without a release fence (see claim_board)
@@ -1991,6 +2308,7 @@ __global__ __launch_bounds__(64) void td_refill_kernel(StepArgs a) {
       if (!claim_board(a.lay_claim + bb, lane)) continue;  // another refill is drawing its layouts
       uint32_t t = ld_relaxed(a.lay_tail + bb);
       const uint32_t h = ld_relaxed(a.lay_head + bb);
+#pragma nounroll
       while (t - h < (uint32_t)NSLOT) {
         uint32_t* slot = a.nxt + ((size_t)bb * NSLOT + t % NSLOT) * a.slot_words;
         // an empty ring is urgent (the board needs this layout at its next episode end):
@@ -2119,7 +2437,8 @@ hipError_t launch_autoreset(const StepArgs& a, hipStream_t s) {
 template <int LT>
 static void launch_refill2(const StepArgs& a, hipStream_t s) {
   const int grp = a.refill_grp;
-  const int waves = (a.B + grp - 1) / grp;
+  const int groups = (a.B + grp - 1) / grp;  // a wave walks the groups grid-stride
+  const int waves = groups < a.refill_waves ? groups : a.refill_waves;
   hipLaunchKernelGGL(td_refill_kernel<LT>, dim3(waves), dim3(64), 0, s, a);
 }
 
