@@ -164,9 +164,8 @@ struct alignas(16) Smem {
 
 // Stage the constant block into LDS (16 bytes per lane).
 template <int NC>
-__device__ __forceinline__ void stage_cfg(Smem<NC>& S, const TdDevCfg* g) {
+__device__ __forceinline__ void stage_cfg(Smem<NC>& S, const TdDevCfg* g, int l = (int)(threadIdx.x & 63)) {
   static_assert(sizeof(TdDevCfg) % 16 == 0 && sizeof(TdDevCfg) <= 64 * 16, "cfg staging");
-  const int l = (int)threadIdx.x;
   if (l < (int)(sizeof(TdDevCfg) / 16))
     reinterpret_cast<uint4*>(&S.cfg)[l] = reinterpret_cast<const uint4*>(g)[l];
 }
