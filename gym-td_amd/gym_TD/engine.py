@@ -265,7 +265,9 @@ class TDEngine(object):
         return _lib.lib.td_state_bytes(self._h, count)
 
     def export_state(self, b0=0, count=None):
-        """Raw SoA state of boards [b0, b0+count) as numpy arrays."""
+        """Raw SoA state of boards [b0, b0+count) as numpy arrays (td_export_state).  The
+        numpy layout stream is not included: get_np_state / set_np_state carry it (with
+        random_agent=False it is the built-in opponent's stream too)."""
         count = self.B - b0 if count is None else count
         buf = np.zeros(self.state_bytes(count), dtype=np.uint8)
         torch.cuda.synchronize(self.device)

@@ -208,7 +208,10 @@ int td_layout_generate(uint32_t* np_state625, int map_size, int max_attempts, ui
  *   tw_cd f64[count][32], tw_inf u32[count][32] (cell | type<<12 | lv<<14 | build epoch<<16 |
  *   stats epoch<<24; imported entities take the current epoch), cells u32[count][L*L],
  *   opp_mt u32[count][626] (the opponent's CPython stream: 624 words, position, and the
- *   lazy-twist boundary -- words [w[625], 624) still hold the previous block).  Synchronous. */
+ *   lazy-twist boundary -- words [w[625], 624) still hold the previous block).  Synchronous.
+ *   The board's numpy layout stream is not part of the record (it belongs to the stream of
+ *   layouts, staged ahead under auto-reset): save / restore it with td_get_np_state /
+ *   td_set_np_state -- with random_agent=False it is also the built-in opponent's stream. */
 size_t td_state_bytes(td_handle* h, int count);
 int td_export_state(td_handle* h, int b0, int count, void* host_dst);
 int td_import_state(td_handle* h, int b0, int count, const void* host_src);
