@@ -1024,6 +1024,35 @@ constexpr uint64_t kChEnemy = 0xFFFFull << 25;
 constexpr uint64_t kChAll = (1ull << NCH) - 1;
 constexpr uint64_t kChConst = kChAll & ~(kChBin | kChD9 | kChEnemy);
 
+// The class of every observation window, by the board's misalignment `mis` (units of
+// the 128-B line before the board) and window k, as a compile-time table read with one
+// scalar load per 8 windows (instead of the window's channel range, channel mask and
+// edge test in ~20 SALU per window): bits 0-1 the channel class (0 binary planes only,
+// 1 broadcast channels only, 2 enemy planes only, 3 mixed), bit 2 the window holds a
+// line shared with a neighbouring board.
+template <int LT>
+struct ObsWinTab {
+  static constexpr int Q = LT * LT / 4, N4 = NCH * Q, K = (N4 + 7 + 63) / 64, W = (K + 7) / 8;
+  struct T { uint32_t w[8][W]; };
+  static constexpr uint32_t cls(int mis, int k) {
+    const int head = mis ? 8 - mis : 0, tail = ((N4 + mis) & ~7) - mis;
+    const int ulo = 64 * k - mis, uhi = ulo + 63;
+    const int clo = (ulo < 0 ? 0 : ulo) / Q, chi = (uhi > N4 - 1 ? N4 - 1 : uhi) / Q;
+    uint64_t chm = 0;
+    for (int c = clo; c <= chi; ++c) chm |= 1ull << c;
+    chm &= kChAll;
+    const uint32_t c = (chm & ~kChBin) == 0 ? 0u : (chm & ~kChConst) == 0 ? 1u : (chm & ~kChEnemy) == 0 ? 2u : 3u;
+    return c | ((ulo < head || uhi >= tail) ? 4u : 0u);
+  }
+  static constexpr T make() {
+    T t{};
+    for (int m = 0; m < 8; ++m)
+      for (int k = 0; k < K; ++k) t.w[m][k / 8] |= cls(m, k) << (4 * (k % 8));
+    return t;
+  }
+  static constexpr T tab = make();
+};
+
 // The (45, L, L) float32 observation of one board for compile-time L, into a
 // 16-B-aligned buffer: the 128-B-aligned 1-KB windows of write_obs (store k covers
 // stream units [A + 64k, A + 64k + 64), A = the board's first unit rounded down to a
@@ -1054,6 +1083,11 @@ __device__ __forceinline__ void write_obs_lines(const Smem<NC>& S, int lane, flo
   const int head = mis ? 8 - mis : 0, tail = ((N4 + mis) & ~7) - mis;   // [0, head), [tail, N4): shared lines
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(out, 0, N4 * 16, 0x00020000);
   const int i0 = lane - mis;
+  // the window's channel class and edge bit (wave-uniform, ObsWinTab)
+  auto wclass = [&](int k) { return (ObsWinTab<LT>::tab.w[mis][k >> 3] >> (4 * (k & 7))) & 7u; };
+  // only a window at either end of the board holds lanes outside it (i < 0, i >= N4):
+  // clamp there, so every lane reads LDS inside the board image
+  auto unit = [&](int i, uint32_t wc) { return (wc & 4u) ? (i < 0 ? 0 : (i > N4 - 1 ? N4 - 1 : i)) : i; };
   for (int k0 = KB; k0 < K; k0 += G) {
     uint4 A[G];
     uint32_t W[G];
@@ -1061,42 +1095,44 @@ __device__ __forceinline__ void write_obs_lines(const Smem<NC>& S, int lane, flo
     for (int j = 0; j < G; ++j) {
       const int k = k0 + j;
       if ((K - KB) % G == 0 || k < K) {
-        int i = i0 + 64 * k;
-        i = i < 0 ? 0 : (i > N4 - 1 ? N4 - 1 : i);
+        const uint32_t wc = wclass(k);
+        const int i = unit(i0 + 64 * k, wc);
         const int ch = i / Q, q = i - ch * Q;
-        const int e = ch - 25;
         A[j] = *reinterpret_cast<const uint4*>(sb + o_cell + 16 * q);
-        // enemy plane: the cell quad's group bytes; else the channel's broadcast value
-        // (bit select: a ternary here compiled to a divergent branch)
-        const int wa = o_grp + (e & 3) * NC + 4 * q, wb = o_chv + 4 * ch, m = -(int)((unsigned)e < 16u);
-        const int wo = wb ^ ((wa ^ wb) & m);
-        W[j] = *reinterpret_cast<const uint32_t*>(sb + wo);
+        if ((wc & 3u) == 1) {  // broadcast channels only: the channel's value
+          W[j] = *reinterpret_cast<const uint32_t*>(sb + o_chv + 4 * ch);
+        } else if ((wc & 3u) >= 2) {
+          // enemy plane: the cell quad's group bytes; else the channel's broadcast value
+          // (bit select: a ternary here compiled to a divergent branch)
+          const int e = ch - 25;
+          const int wa = o_grp + (e & 3) * NC + 4 * q, wb = o_chv + 4 * ch, m = -(int)((unsigned)e < 16u);
+          const int wo = wb ^ ((wa ^ wb) & m);
+          W[j] = *reinterpret_cast<const uint32_t*>(sb + wo);
+        } else {
+          W[j] = 0u;  // binary planes only: the cell quad is all
+        }
       }
     }
 #pragma unroll
     for (int j = 0; j < G; ++j) {
       const int k = k0 + j;
       if (!((K - KB) % G == 0 || k < K)) continue;
-      // the window's channels (wave-uniform)
-      const int ulo = 64 * k - mis, uhi = ulo + 63;
-      const int clo = (ulo < 0 ? 0 : ulo) / Q, chi = (uhi > N4 - 1 ? N4 - 1 : uhi) / Q;
-      const uint64_t chm = ((chi >= 63 ? ~0ull : ((1ull << (chi + 1)) - 1)) & ~((1ull << clo) - 1)) & kChAll;
-      const bool edge = ulo < head || uhi >= tail;  // the window holds a line shared with a neighbour
-      int i = i0 + 64 * k;
-      const int ic = i < 0 ? 0 : (i > N4 - 1 ? N4 - 1 : i);
-      const int ch = ic / Q;
+      const uint32_t wc = wclass(k);
+      const bool edge = (wc & 4u) != 0;  // the window holds a line shared with a neighbour
+      const int i = i0 + 64 * k;
+      const int ch = unit(i, wc) / Q;
       const int e = ch - 25;
       const bool isen = (unsigned)e < 16u, isd9 = ch == 9, isbin = ((kChBin >> ch) & 1ull) != 0;
       const uint32_t a4[4] = {A[j].x, A[j].y, A[j].z, A[j].w};
       float v[4];
-      if ((chm & ~kChBin) == 0) {
+      if ((wc & 3u) == 0) {
 #pragma unroll
         for (int c = 0; c < 4; ++c) v[c] = (float)((a4[c] >> ch) & 1u);
-      } else if ((chm & ~kChConst) == 0) {
+      } else if ((wc & 3u) == 1) {
         const float cv = __uint_as_float(W[j]);
 #pragma unroll
         for (int c = 0; c < 4; ++c) v[c] = cv;
-      } else if ((chm & ~kChEnemy) == 0 && !any_enemy) {
+      } else if ((wc & 3u) == 2 && !any_enemy) {
 #pragma unroll
         for (int c = 0; c < 4; ++c) v[c] = 0.0f;
       } else {
@@ -1121,15 +1157,16 @@ __device__ __forceinline__ void write_obs_lines(const Smem<NC>& S, int lane, flo
           for (int c = 0; c < 4; ++c) v[c] = cv;
         }
       }
-      const bool shared = i < head || i >= tail;  // a line shared with a neighbouring board
       const f32x4 val = f32x4{v[0], v[1], v[2], v[3]};
       const uint32_t off = (uint32_t)i * 16u;  // i < 0 or i >= N4: out of range already
       if (wt) {  // wave-uniform
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, val), rs, off, 0, 16 /* sc1 */);
+      } else if (!edge) {  // whole lines of this board only
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, val), rs, off, 0, 2 /* nt */);
       } else {
+        const bool shared = i < head || i >= tail;  // a line shared with a neighbouring board
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, val), rs, shared ? OOB : off, 0, 2 /* nt */);
-        if (edge)
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, val), rs, shared ? off : OOB, 0, 16 /* sc1 */);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, val), rs, shared ? off : OOB, 0, 16 /* sc1 */);
       }
     }
   }
@@ -2282,9 +2319,8 @@ __global__ __launch_bounds__(64) void td_autoreset_kernel(StepArgs a) {
 
 // Keep every board's ring of staged layouts full: lanes check G boards at once
 // (layouts drawn minus consumed < NSLOT), then the wave draws the missing layouts
-// of those boards one by one, lane 0 running the serial generator out of LDS.  Runs
-// on a side stream concurrently with the step grids; td_capi keeps at most one in
-// flight and never makes the step stream wait for it.
+// of those boards one by one with the whole-wave generator (WaveRoadGen).  Runs on a
+// side stream concurrently with the step grids; the step stream never waits for it.
 template <int LT>
 __global__ __launch_bounds__(64) void td_refill_kernel(StepArgs a) {
   constexpr int NC = LT ? LT * LT : MAX_KERNEL_L * MAX_KERNEL_L;
