@@ -1,6 +1,6 @@
 """Summarise a profile_session.sh run (gpurun_out/prof) into profiles/.
 
-  python scripts/pmc_summary.py ROUND [B] [WORKLOAD]
+  [PMC_PROF=dir] [PMC_OUT=dir] python scripts/pmc_summary.py ROUND [B] [WORKLOAD]
 
 writes profiles/<ROUND>_kernel_stats.csv (rocprofv3 --kernel-trace --stats),
 profiles/<ROUND>_pmc.json (per-launch counter means of the step kernel) and
@@ -17,7 +17,7 @@ import shutil
 import sys
 
 HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-PROF = os.path.join(HERE, "gpurun_out", "prof")
+PROF = os.environ.get("PMC_PROF", os.path.join(HERE, "gpurun_out", "prof"))
 
 
 def step_counters(name):
@@ -35,8 +35,8 @@ def main():
     B = int(sys.argv[2]) if len(sys.argv) > 2 else 65536
     wl = sys.argv[3] if len(sys.argv) > 3 else "def-small"
     L, mode = {"def-small": (10, "DEF"), "2p-middle-multi": (20, "2P"), "def-large": (30, "DEF")}[wl]
-    out = os.path.join(HERE, "profiles")
-    tag = rnd if wl == "def-small" else "%s_%s" % (rnd, wl)
+    out = os.environ.get("PMC_OUT", os.path.join(HERE, "profiles"))
+    tag = (rnd if wl == "def-small" else "%s_%s" % (rnd, wl)) + ("" if B == 65536 or wl != "def-small" else "_b%d" % B)
     shutil.copy(os.path.join(PROF, "kt", "kt_kernel_stats.csv"), os.path.join(out, "%s_kernel_stats.csv" % tag))
     pmc, launches = {}, {}
     for n in ("pmc_fetch", "pmc_write", "pmc_sq1", "pmc_sq2"):
@@ -56,6 +56,8 @@ def main():
     }
     json.dump(summary, open(os.path.join(out, "%s_pmc.json" % tag), "w"), indent=1)
     tp = os.path.join(out, "pmc_traffic.json")
+    if not os.path.exists(tp) and os.path.exists(os.path.join(HERE, "profiles", "pmc_traffic.json")):
+        shutil.copy(os.path.join(HERE, "profiles", "pmc_traffic.json"), tp)
     tj = json.load(open(tp)) if os.path.exists(tp) else {}
     sys.path.insert(0, HERE)
     import bench  # noqa: E402  (the kernel-source hash bench.py checks before quoting this record)
