@@ -378,6 +378,44 @@ def test_export_import_roundtrip():
         b_eng.close()
 
 
+def test_export_import_roundtrip_random_agent_false():
+    """With random_agent=False the built-in opponent draws from the board's numpy layout
+    stream, which td_export_state does not carry (include/tdstep.h): a snapshot is the
+    export plus get_np_state per board.  Restored into an engine with other seeds, the
+    boards continue bit-identically -- opponent moves, rewards, and the layouts of the
+    resets that follow."""
+    L, B = 10, 16
+    seeds, _ = _first_ok_seeds(L, B, 6100, "def", False, 1)
+    mk = lambda s, off: TDEngine(L, B, "def", False, 1, np_seeds=[x + off for x in s], py_seeds=[x + off for x in s],
+                                 autoreset=False, random_agent=False)
+    a_eng, b_eng = mk(seeds, 0), mk(seeds, 3)
+    try:
+        a_eng.reset()
+        b_eng.reset()
+        rng = np.random.RandomState(5)
+        for k in range(150):
+            a_eng.step(def_act=torch.from_numpy(rng.randint(0, 6 * L * L + 1, size=B).astype(np.int64)))
+        b_eng.import_state(a_eng.export_state())
+        for b in range(B):
+            b_eng.set_np_state(b, a_eng.get_np_state(b))
+            assert canon.state_digest(b_eng.board_state(b)) == canon.state_digest(a_eng.board_state(b))
+        for k in range(150):
+            act = torch.from_numpy(rng.randint(0, 6 * L * L + 1, size=B).astype(np.int64))
+            a_eng.step(def_act=act)
+            b_eng.step(def_act=act)
+            assert torch.equal(a_eng.obs, b_eng.obs) and torch.equal(a_eng.reward, b_eng.reward), k
+            assert torch.equal(a_eng.done, b_eng.done), k
+        # the next episodes' layouts come from the same restored streams
+        oa, fa = a_eng.reset()
+        ob, fb = b_eng.reset()
+        assert list(fa) == list(fb) and torch.equal(oa, ob)
+        for b in range(B):
+            assert a_eng.get_np_state(b).tolist() == b_eng.get_np_state(b).tolist()
+    finally:
+        a_eng.close()
+        b_eng.close()
+
+
 def test_paramconfig_reaches_live_engines():
     """paramConfig (TDParam.py:98-100) in the middle of episodes, twice, on a live engine.
     The reference reads most values live from `config`, but an Enemy / Tower keeps the
