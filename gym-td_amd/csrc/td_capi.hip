@@ -63,7 +63,6 @@ struct td_handle {
   int L = 0, NC = 0, B = 0, mode = 0, multi = 0, difficulty = 1, device = 0, autoreset = 1;
   int opp_np = 0;  // random_agent=False
   int small = 0, obs_wt = 0;  // small-batch step kernel, write-through observation stores (td_kernels.h)
-  int bpw = 1;                 // boards per wave of the small kernel (td_kernels.h)
   int lw = 0;  // layout record words
   size_t scratch_stride = 0;
   TdDevCfg dcfg;
@@ -174,7 +173,6 @@ StepArgs base_args(td_handle* h) {
   a.opp_np = h->opp_np;
   a.small = h->small;
   a.obs_wt = h->obs_wt;
-  a.bpw = h->bpw;
   a.hdr = h->d_hdr; a.en_lp = h->d_en_lp; a.en_mg = h->d_en_mg; a.en_inf = h->d_en_inf;
   a.tw_cd = h->d_tw_cd; a.tw_inf = h->d_tw_inf; a.cells = h->d_cells; a.opp_mt = h->d_opp; a.opp_hot = h->d_hot;
   a.np_mt = h->d_np; a.nxt = h->d_nxt; a.scratch = h->d_scratch; a.scratch_stride = h->scratch_stride;
@@ -393,10 +391,6 @@ td_handle* td_create(const td_config* cfg, int map_size, int n_boards, int mode,
     h->small = n_boards <= resident2 ? 2 : n_boards <= resident ? 1 : 0;
     h->obs_wt = h->small && obs_bytes <= 192.0 * 1024 * 1024 ? 1 : 0;
     auto ov = [](const char* name, int& v) { if (const char* e = std::getenv(name)) v = std::atoi(e) ? 1 : 0; };
-    if (const char* e = std::getenv("TD_BPW")) {  // A/B runs: boards per wave of the small kernel
-      h->bpw = std::max(1, std::atoi(e));
-      if (h->small != 2) h->small = (n_boards + h->bpw - 1) / h->bpw <= resident ? 1 : 0;
-    }
     if (const char* e = std::getenv("TD_SMALL")) h->small = std::max(0, std::min(2, std::atoi(e)));
     ov("TD_OBS_WT", h->obs_wt);
     if (const char* e = std::getenv("TD_REFILL_EVERY")) h->refill_every = std::max(0, std::atoi(e));  // A/B runs

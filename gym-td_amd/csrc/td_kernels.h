@@ -16,7 +16,6 @@ struct StepArgs {
   int opp_np;           // random_agent=False: the built-in opponents draw from np_mt (auto-reset off)
   int small;            // the batch fits one round of step waves: 1 td_step_kernel_small, 2 td_step_kernel_small2
   int obs_wt;           // small kernel: observation stores write-through (the batch's obs fits the MALL)
-  int bpw;              // small kernel: boards stepped one after another by each wave (>= 1)
   TdHdr* hdr;
   double* en_lp;
   double* en_mg;
