@@ -104,6 +104,18 @@ def metric_label(workload, global_batch, scaling):
     return "env-steps/sec (whole node), %s %dx%d board, batch=%d (%s scaling)" % (kind, L, L, global_batch, scaling)
 
 
+def step_kernel_name(L, mode, boards, cus):
+    """The step kernel td_create picks for this batch (td_capi.hip: the small kernel where
+    the batch is one round of waves, two waves per board up to half a round). Only the
+    10x10 build runs 8 waves per SIMD (5,072 B of LDS per board); TD_SMALL overrides."""
+    small = 0
+    if L == 10 and cus:
+        small = 2 if boards <= 16 * cus else 1 if boards <= 32 * cus else 0
+    if os.environ.get("TD_SMALL") is not None:
+        small = max(0, min(2, int(os.environ["TD_SMALL"])))
+    return "%s<%d, %s>" % (("td_step_kernel", "td_step_kernel_small", "td_step_kernel_small2")[small], L, mode.upper())
+
+
 def kernel_source_hash():
     """sha256 (16 hex) of the step kernel's sources: a PMC traffic record is quoted
     only for the build it was measured on."""
@@ -354,7 +366,8 @@ def main():
                        "map_size": L, "parallelism": "boards sharded per GPU (dp%d), no data-path collective" % world},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel": "td_step_kernel<%d, %s>" % (L, mode.upper()), "avg_kernel_us": avg_kernel_s * 1e6,
+                         "kernel": step_kernel_name(L, mode, B, torch.cuda.get_device_properties(dev).multi_processor_count),
+                         "avg_kernel_us": avg_kernel_s * 1e6,
                          "kernel_samples": len(kern_ms) * world,
                          "kernel_timing": {"dispatch": "dispatch-packet timestamps of every %dth timed launch "
                                                        "(td_kernel_timing)" % EVENT_EVERY,

@@ -33,3 +33,15 @@ def test_traffic_only_for_the_measured_build(tmp_path, monkeypatch):
     # a record measured on other kernel sources (or at another batch) is never quoted
     assert bench.measured_traffic("def-small", 12345) == (None, None)
     assert len(bench.kernel_source_hash()) == 16
+
+
+@pytest.mark.parametrize("world,kernel", [(1, "td_step_kernel<10, DEF>"), (2, "td_step_kernel<10, DEF>"),
+                                          (4, "td_step_kernel<10, DEF>"), (8, "td_step_kernel_small<10, DEF>")])
+def test_roofline_names_the_kernel_that_runs(world, kernel, monkeypatch):
+    # td_create's rule on a 256-CU MI355X: one round of waves (8 per SIMD) -> small kernel,
+    # half a round -> two waves per board
+    monkeypatch.delenv("TD_SMALL", raising=False)
+    B, _, _ = bench.partition("def-small", world)
+    assert bench.step_kernel_name(10, "def", B, 256) == kernel
+    assert bench.step_kernel_name(10, "def", 4096, 256) == "td_step_kernel_small2<10, DEF>"
+    assert bench.step_kernel_name(20, "2p", 16384, 256) == "td_step_kernel<20, 2P>"
