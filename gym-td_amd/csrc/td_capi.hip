@@ -226,10 +226,13 @@ int drop_all_staged(td_handle* h) {
 // steps ahead of the GPU, and a refill launched "when a stream looks free" from there
 // would leave the GPU without refills for as long.  A refill stuck on a draw the
 // reference never finishes (milliseconds) delays only its own stream's queue.
-int start_refill(td_handle* h, hipStream_t s) {
+// wait: the refill is ordered after the work on s so far.  Always after a reset kernel,
+// whose draws-now use the boards' numpy streams and ring slots without a claim;
+// TD_REFILL_NOWAIT (A/B runs) drops the order between steps only.
+int start_refill(td_handle* h, hipStream_t s, bool wait) {
   const int q = h->next_side;
   StepArgs a = base_args(h);
-  if (!h->refill_nowait) {
+  if (wait || !h->refill_nowait) {
     HIP_OK(hipEventRecord(h->ev_main, s));
     HIP_OK(hipStreamWaitEvent(h->side[q], h->ev_main, 0));
   }
@@ -245,7 +248,7 @@ int run_reset(td_handle* h, const std::vector<uint8_t>& mask, float* obs, hipStr
   a.obs = obs;
   a.reset_mask = h->d_mask;
   HIP_OK(launch_step(a, s, true));
-  if (h->autoreset && !h->opp_np && start_refill(h, s)) return -1;
+  if (h->autoreset && !h->opp_np && start_refill(h, s, true)) return -1;
   HIP_OK(hipDeviceSynchronize());
   return 0;
 }
@@ -633,7 +636,7 @@ int td_step(td_handle* h, const td_step_io* io, void* stream) {
   // random_agent=True: layouts are staged ahead by refills on the side streams.
   // random_agent=False: they are drawn in stream order right after the step (below).
   if (h->autoreset && !h->opp_np && h->refill_every > 0 && (h->steps % h->refill_every) == 0 &&
-      start_refill(h, s))
+      start_refill(h, s, false))
     return -1;
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (h->tev_n < h->tev_cap && (h->steps - h->tev_from) % h->tev_every == 0) {
