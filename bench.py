@@ -117,13 +117,14 @@ def step_kernel_name(L, mode, boards, cus):
 
 
 def kernel_source_hash():
-    """sha256 (16 hex) of the step kernel's sources: a PMC traffic record is quoted
-    only for the build it was measured on."""
+    """sha256 (16 hex) of the step kernel's sources (td_step.hip and the headers it
+    includes; not the host-side td_capi.hip, which launches it): a PMC traffic record of
+    the step kernel is quoted only for the build it was measured on."""
     import hashlib
     h = hashlib.sha256()
     d = os.path.join(HERE, "gym-td_amd", "csrc")
     for f in sorted(os.listdir(d)):
-        if f.endswith((".hip", ".h")):
+        if f == "td_step.hip" or f.endswith(".h"):
             h.update(open(os.path.join(d, f), "rb").read())
     return h.hexdigest()[:16]
 

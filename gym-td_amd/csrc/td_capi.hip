@@ -89,7 +89,8 @@ struct td_handle {
   int next_side = 0;
   int refill_every = kRefillEvery;  // 0: no refill launches (td_set_refill_interval)
   int refill_waves = kRefillWaves;  // waves per refill launch
-  int refill_nowait = 0, n_side = kSideStreams;  // A/B knobs (TD_REFILL_NOWAIT, TD_SIDE_STREAMS)
+  int refill_wait_every = 1, n_side = kSideStreams;  // A/B knobs (TD_REFILL_NOWAIT / _WAIT_EVERY, TD_SIDE_STREAMS)
+  long refill_launches = 0;
   int refill_walks = 0;  // walks per board per refill launch (0: 12 per step of interval; TD_REFILL_WALKS)
   // td_kernel_timing: event pairs bound to the next `tev_cap` step-kernel dispatches
   std::vector<hipEvent_t> tev;
@@ -228,11 +229,13 @@ int drop_all_staged(td_handle* h) {
 // reference never finishes (milliseconds) delays only its own stream's queue.
 // wait: the refill is ordered after the work on s so far.  Always after a reset kernel,
 // whose draws-now use the boards' numpy streams and ring slots without a claim;
-// TD_REFILL_NOWAIT (A/B runs) drops the order between steps only.
+// TD_REFILL_NOWAIT / TD_REFILL_WAIT_EVERY=k (A/B runs) drop the order between steps for
+// all launches / all but every k-th.
 int start_refill(td_handle* h, hipStream_t s, bool wait) {
   const int q = h->next_side;
   StepArgs a = base_args(h);
-  if (wait || !h->refill_nowait) {
+  const long n = h->refill_launches++;
+  if (wait || (h->refill_wait_every > 0 && n % h->refill_wait_every == 0)) {
     HIP_OK(hipEventRecord(h->ev_main, s));
     HIP_OK(hipStreamWaitEvent(h->side[q], h->ev_main, 0));
   }
@@ -398,7 +401,8 @@ td_handle* td_create(const td_config* cfg, int map_size, int n_boards, int mode,
     ov("TD_OBS_WT", h->obs_wt);
     if (const char* e = std::getenv("TD_REFILL_EVERY")) h->refill_every = std::max(0, std::atoi(e));  // A/B runs
     if (const char* e = std::getenv("TD_REFILL_WAVES")) h->refill_waves = std::max(1, std::atoi(e));
-    if (const char* e = std::getenv("TD_REFILL_NOWAIT")) h->refill_nowait = std::atoi(e) ? 1 : 0;
+    if (const char* e = std::getenv("TD_REFILL_NOWAIT")) h->refill_wait_every = std::atoi(e) ? 0 : 1;
+    if (const char* e = std::getenv("TD_REFILL_WAIT_EVERY")) h->refill_wait_every = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("TD_REFILL_WALKS")) h->refill_walks = std::max(1, std::atoi(e));
     if (const char* e = std::getenv("TD_SIDE_STREAMS")) h->n_side = std::min(kSideStreams, std::max(1, std::atoi(e)));
   }
