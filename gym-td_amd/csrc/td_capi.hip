@@ -46,7 +46,10 @@ int fail(const char* fmt, ...) {
 
 // Steps between refill launches (td_set_refill_interval).  At 65,536 boards every 4th
 // step and every 16th step per-step times are within 0.5 % (227.6 vs 228.5 us, 2,000
-// steps, no ring dry).
+// steps, no ring dry).  Every launch is ordered behind the step stream (start_refill):
+// refills left unordered between steps ran 4-8 % faster at 4,096 / 8,192 boards but
+// handed a board's draw between two concurrent refill kernels without the ordering its
+// stream state needs -- a wrong layout under load (test_autoreset_under_load, s43).
 constexpr int kRefillEvery = 4;
 constexpr int kRefillWaves = 1024;
 // A pending draw advances 3 walks per step of refill interval (12 per launch at 4): the
@@ -89,8 +92,7 @@ struct td_handle {
   int next_side = 0;
   int refill_every = kRefillEvery;  // 0: no refill launches (td_set_refill_interval)
   int refill_waves = kRefillWaves;  // waves per refill launch
-  int refill_wait_every = 1, n_side = kSideStreams;  // A/B knobs (TD_REFILL_NOWAIT / _WAIT_EVERY, TD_SIDE_STREAMS)
-  long refill_launches = 0;
+  int n_side = kSideStreams;  // A/B knob (TD_SIDE_STREAMS)
   int refill_walks = 0;  // walks per board per refill launch (0: 12 per step of interval; TD_REFILL_WALKS)
   // td_kernel_timing: event pairs bound to the next `tev_cap` step-kernel dispatches
   std::vector<hipEvent_t> tev;
@@ -227,18 +229,14 @@ int drop_all_staged(td_handle* h) {
 // steps ahead of the GPU, and a refill launched "when a stream looks free" from there
 // would leave the GPU without refills for as long.  A refill stuck on a draw the
 // reference never finishes (milliseconds) delays only its own stream's queue.
-// wait: the refill is ordered after the work on s so far.  Always after a reset kernel,
-// whose draws-now use the boards' numpy streams and ring slots without a claim;
-// TD_REFILL_NOWAIT / TD_REFILL_WAIT_EVERY=k (A/B runs) drop the order between steps for
-// all launches / all but every k-th.
-int start_refill(td_handle* h, hipStream_t s, bool wait) {
+// The refill is ordered after the work on s so far: after a reset kernel, whose
+// draws-now use the boards' numpy streams and ring slots without a claim, and after the
+// previous step (see kRefillEvery).
+int start_refill(td_handle* h, hipStream_t s) {
   const int q = h->next_side;
   StepArgs a = base_args(h);
-  const long n = h->refill_launches++;
-  if (wait || (h->refill_wait_every > 0 && n % h->refill_wait_every == 0)) {
-    HIP_OK(hipEventRecord(h->ev_main, s));
-    HIP_OK(hipStreamWaitEvent(h->side[q], h->ev_main, 0));
-  }
+  HIP_OK(hipEventRecord(h->ev_main, s));
+  HIP_OK(hipStreamWaitEvent(h->side[q], h->ev_main, 0));
   HIP_OK(launch_refill(a, h->side[q]));
   h->next_side = (q + 1) % h->n_side;
   return 0;
@@ -251,7 +249,7 @@ int run_reset(td_handle* h, const std::vector<uint8_t>& mask, float* obs, hipStr
   a.obs = obs;
   a.reset_mask = h->d_mask;
   HIP_OK(launch_step(a, s, true));
-  if (h->autoreset && !h->opp_np && start_refill(h, s, true)) return -1;
+  if (h->autoreset && !h->opp_np && start_refill(h, s)) return -1;
   HIP_OK(hipDeviceSynchronize());
   return 0;
 }
@@ -401,8 +399,6 @@ td_handle* td_create(const td_config* cfg, int map_size, int n_boards, int mode,
     ov("TD_OBS_WT", h->obs_wt);
     if (const char* e = std::getenv("TD_REFILL_EVERY")) h->refill_every = std::max(0, std::atoi(e));  // A/B runs
     if (const char* e = std::getenv("TD_REFILL_WAVES")) h->refill_waves = std::max(1, std::atoi(e));
-    if (const char* e = std::getenv("TD_REFILL_NOWAIT")) h->refill_wait_every = std::atoi(e) ? 0 : 1;
-    if (const char* e = std::getenv("TD_REFILL_WAIT_EVERY")) h->refill_wait_every = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("TD_REFILL_WALKS")) h->refill_walks = std::max(1, std::atoi(e));
     if (const char* e = std::getenv("TD_SIDE_STREAMS")) h->n_side = std::min(kSideStreams, std::max(1, std::atoi(e)));
   }
@@ -640,7 +636,7 @@ int td_step(td_handle* h, const td_step_io* io, void* stream) {
   // random_agent=True: layouts are staged ahead by refills on the side streams.
   // random_agent=False: they are drawn in stream order right after the step (below).
   if (h->autoreset && !h->opp_np && h->refill_every > 0 && (h->steps % h->refill_every) == 0 &&
-      start_refill(h, s, false))
+      start_refill(h, s))
     return -1;
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (h->tev_n < h->tev_cap && (h->steps - h->tev_from) % h->tev_every == 0) {
