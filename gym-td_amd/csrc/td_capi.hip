@@ -47,9 +47,9 @@ int fail(const char* fmt, ...) {
 // Steps between refill launches (td_set_refill_interval).  At 65,536 boards every 4th
 // step and every 16th step per-step times are within 0.5 % (227.6 vs 228.5 us, 2,000
 // steps, no ring dry).  Every launch is ordered behind the step stream (start_refill):
-// refills left unordered between steps ran 4-8 % faster at 4,096 / 8,192 boards but
-// handed a board's draw between two concurrent refill kernels without the ordering its
-// stream state needs -- a wrong layout under load (test_autoreset_under_load, s43).
+// refills left unordered between steps ran 4-8 % faster at 4,096 / 8,192 boards, but a
+// step that finds a ring empty then has no refill beside it to wait for: under load a
+// board missed its layout (test_autoreset_under_load, profiles/r02/s43_unordered).
 constexpr int kRefillEvery = 4;
 constexpr int kRefillWaves = 1024;
 // A pending draw advances 3 walks per step of refill interval (12 per launch at 4): the
