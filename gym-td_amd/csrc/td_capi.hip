@@ -44,17 +44,18 @@ int fail(const char* fmt, ...) {
     if (e_ != hipSuccess) return fail("%s: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, __LINE__); \
   } while (0)
 
-// Steps between refill launches (td_set_refill_interval).  At 65,536 boards every 4th
-// step and every 16th step per-step times are within 0.5 % (227.6 vs 228.5 us, 2,000
-// steps, no ring dry).  Every launch is ordered behind the step stream (start_refill):
+// Steps between refill launches (td_set_refill_interval).  Every 16th step instead of
+// every 4th: 23.7 / 36.3 / 208.3 vs 24.9 / 37.1 / 209.2 us per step at 4,096 / 8,192 /
+// 65,536 boards, no ring dry over 5,000 steps, the GPU suite green (profiles/r02/s44).
+// Every launch is ordered behind the step stream (start_refill):
 // refills left unordered between steps ran 4-8 % faster at 4,096 / 8,192 boards, but a
 // step that finds a ring empty then has no refill beside it to wait for: under load a
 // board missed its layout (test_autoreset_under_load, profiles/r02/s43_unordered).
-constexpr int kRefillEvery = 4;
+constexpr int kRefillEvery = 16;
 constexpr int kRefillWaves = 1024;
-// A pending draw advances 3 walks per step of refill interval (12 per launch at 4): the
+// A pending draw advances 3 walks per step of refill interval (48 per launch at 16): the
 // fewer walks a refill wave runs per launch, the less it holds a wave slot the next
-// step's waves need (8,192 boards: 37.9 us per step at 48 walks, 36.5 at 12, 36.6 at 4,
+// step's waves need (8,192 boards, a refill every 4th step: 37.9 us per step at 48 walks, 36.5 at 12, 36.6 at 4,
 // 36.9 at 1; 34.3 without refills, profiles/r02/s21_session.log).
 constexpr int kWalksPerStep = 3;
 constexpr int kSideStreams = 2;  // refill streams: one stuck on a long draw does not stall the next (the HIP
