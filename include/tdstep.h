@@ -158,7 +158,7 @@ int td_reset_layouts(td_handle* h, const uint32_t* recs, const int32_t* boards, 
 int td_step(td_handle* h, const td_step_io* io, void* stream);
 
 /* Steps between launches of the layout refill kernel on the side streams (auto-reset;
- * default 4, 0 = none: the staged rings then only drain).  A tuning / diagnostic knob. */
+ * default 16, 0 = none: the staged rings then only drain).  A tuning / diagnostic knob. */
 int td_set_refill_interval(td_handle* h, int steps);
 
 /* Kernel timing: every `every`-th td_step call from now on, up to max_launches of them,
