@@ -4,6 +4,10 @@
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
+``--gpus N`` with N > 1 and no WORLD_SIZE in the environment starts the N ranks itself
+(``torch.distributed.run`` as a child process, before anything touches the GPU) and
+exits with its status; under a launcher, WORLD_SIZE must equal ``--gpus``.
+
 Workload: TD-def-small (10x10), built-in lv1 opponent, uniform random defender
 actions over [0, 601) drawn on the device before the timed region, auto-reset on.
 Scaling is STRONG by default, as BASELINE.json's metric and configs[3] state it:
@@ -104,40 +108,32 @@ def metric_label(workload, global_batch, scaling):
     return "env-steps/sec (whole node), %s %dx%d board, batch=%d (%s scaling)" % (kind, L, L, global_batch, scaling)
 
 
-def step_kernel_name(L, mode, boards, cus):
-    """The step kernel td_create picks for this batch (td_capi.hip: the small kernel where
-    the batch is one round of waves, two waves per board up to half a round). Only the
-    10x10 build runs 8 waves per SIMD (5,072 B of LDS per board); TD_SMALL overrides."""
-    small = 0
-    if L == 10 and cus:
-        small = 2 if boards <= 16 * cus else 1 if boards <= 32 * cus else 0
-    if os.environ.get("TD_SMALL") is not None:
-        small = max(0, min(2, int(os.environ["TD_SMALL"])))
-    return "%s<%d, %s>" % (("td_step_kernel", "td_step_kernel_small", "td_step_kernel_small2")[small], L, mode.upper())
-
-
 def kernel_source_hash():
-    """sha256 (16 hex) of the step kernel's sources (td_step.hip and the headers it
-    includes; not the host-side td_capi.hip, which launches it): a PMC traffic record of
-    the step kernel is quoted only for the build it was measured on."""
+    """sha256 (16 hex) of the library's sources (td_step.hip, td_capi.hip -- which picks
+    the kernel, the store policy and the refill cadence -- and the headers): a PMC
+    traffic record of the step kernel is quoted only for the build it was measured on."""
     import hashlib
     h = hashlib.sha256()
     d = os.path.join(HERE, "gym-td_amd", "csrc")
     for f in sorted(os.listdir(d)):
-        if f == "td_step.hip" or f.endswith(".h"):
+        if f.endswith(".hip") or f.endswith(".h"):
             h.update(open(os.path.join(d, f), "rb").read())
+    h.update(open(os.path.join(HERE, "include", "tdstep.h"), "rb").read())
     return h.hexdigest()[:16]
 
 
-def measured_traffic(workload, boards):
+def measured_traffic(workload, boards, kernel=None):
     """(bytes per launch, source) from profiles/pmc_traffic.json when that file holds a
-    PMC measurement of this workload at these boards per GPU on this kernel build."""
+    PMC measurement of this workload at these boards per GPU on this build and, when the
+    record names one, this step kernel."""
     tp = os.path.join(HERE, "profiles", "pmc_traffic.json")
     try:
         rec = json.load(open(tp)).get("%s_B%d" % (workload, boards))
     except Exception:  # noqa: BLE001
         return None, None
     if not rec or rec.get("kernel_src") != kernel_source_hash():
+        return None, None
+    if kernel is not None and rec.get("kernel") not in (None, kernel):
         return None, None
     return rec["hbm_bytes_per_launch"], "profiles/pmc_traffic.json[%s_B%d] (%s, rocprofv3 --pmc FETCH_SIZE / " \
         "WRITE_SIZE passes of bench.py at the same boards per GPU, kernel sources %s)" % (
@@ -211,6 +207,37 @@ def host_cores():
     return max(1, min(16, n))
 
 
+# --------------------------------------------------------------------------- launch
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch_ranks(n, argv):
+    """Run this script on n ranks (one process per GPU) with torch.distributed.run as a
+    child process; returns its exit status.  Nothing here touches the GPU, so the ranks
+    start fresh (no exec from a process that has initialised HIP)."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__)] + list(argv)
+    return subprocess.call(cmd)
+
+
+def check_world(gpus, env):
+    """The rank count a run has: WORLD_SIZE under a launcher (which must equal --gpus),
+    else None when bench.py must start --gpus ranks itself, else 1."""
+    w = env.get("WORLD_SIZE")
+    if w is not None:
+        if int(w) != gpus:
+            raise SystemExit("bench.py: --gpus %d but the launcher started WORLD_SIZE=%s ranks" % (gpus, w))
+        return int(w)
+    if gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    return None if gpus > 1 else 1
+
+
 # --------------------------------------------------------------------------- main
 def main():
     ap = argparse.ArgumentParser()
@@ -234,11 +261,15 @@ def main():
                          "(td_kernel_timing, the dispatch-packet timestamps rocprofv3 reports); 'marker' = torch "
                          "event pairs around every %d-th launch (adds the marker packets' overhead); 'none' = "
                          "no kernel timing (diagnostic A/B of the step rate)" % (EVENT_EVERY, EVENT_EVERY))
+    ap.add_argument("--step-kernel", default="auto", choices=("auto", "large", "small", "small2"),
+                    help="diagnostic: force a step kernel (td_set_step_kernel); default td_create's rule")
     ap.add_argument("--refill-interval", type=int, default=None,
                     help="diagnostic: steps between layout-refill launches in the timed region (0 = none)")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world = check_world(args.gpus, os.environ)
+    if world is None:  # --gpus N > 1 without a launcher: start the N ranks here
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # TD_BENCH_DIST_BACKEND=gloo + TD_BENCH_SAME_DEVICE=1: rehearsal of the N > 1 control
@@ -269,7 +300,7 @@ def main():
     # its info dict (TDDefense.py:87, TDMulti.py:134-135 raise) and SURVEY 8(d) config 3
     # is the board-level step
     eng = TDEngine(L, B, mode, multi, 1, device=dev, np_seeds=seeds, py_seeds=seeds, autoreset=bool(args.autoreset),
-                   info=not multi)
+                   info=not multi, step_kernel=args.step_kernel)
     obs, _ = eng.reset_all()  # failing road draws (the reference raises/hangs) are redrawn
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
 
@@ -346,16 +377,18 @@ def main():
     # the per-board payload (16 B per board: last episode's return, length, win)
     recs = shard.gather_episode_records(*[t.to(coll) for t in eng.episode_records()])
     elapsed, avg_kernel_s = float(t[0]), float(t[1])
+    reported_world = dist.get_world_size() if world > 1 else 1  # what the process group (RCCL) reports
 
     if rank == 0:
         total_steps = world * B * K
         value = total_steps / elapsed
         bpe = algorithmic_bytes(L, mode, multi)
         achieved = B * bpe / avg_kernel_s / 1e9
-        traffic, traffic_src = measured_traffic(args.workload, B)
+        traffic, traffic_src = measured_traffic(args.workload, B, eng.step_kernel_name)
         out = {
             "metric": metric,
-            "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": K, "warmup": W,
+            "value": value, "unit": "env-steps/s", "n_gpus": world, "world_size_reported": reported_world,
+            "steps": K, "warmup": W,
             "ms_per_step": elapsed / K * 1e3, "higher_is_better": True, "scaling": scaling,
             "vs_baseline": None, "dtype": "f64",
             "data": DATA[mode, multi],
@@ -367,7 +400,7 @@ def main():
                        "map_size": L, "parallelism": "boards sharded per GPU (dp%d), no data-path collective" % world},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel": step_kernel_name(L, mode, B, torch.cuda.get_device_properties(dev).multi_processor_count),
+                         "kernel": eng.step_kernel_name,
                          "avg_kernel_us": avg_kernel_s * 1e6,
                          "kernel_samples": len(kern_ms) * world,
                          "kernel_timing": {"dispatch": "dispatch-packet timestamps of every %dth timed launch "

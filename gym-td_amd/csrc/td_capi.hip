@@ -66,7 +66,9 @@ constexpr int kSideStreams = 2;  // refill streams: one stuck on a long draw doe
 struct td_handle {
   int L = 0, NC = 0, B = 0, mode = 0, multi = 0, difficulty = 1, device = 0, autoreset = 1;
   int opp_np = 0;  // random_agent=False
-  int small = 0, obs_wt = 0;  // small-batch step kernel, write-through observation stores (td_kernels.h)
+  int small = 0, obs_wt = 0;  // the step kernel (0 large, 1 small, 2 small2), write-through observation stores
+  int small_auto = 0;         // td_create's choice (TD_KERNEL_AUTO)
+  std::string kernel_name;    // td_step_kernel_name
   int lw = 0;  // layout record words
   size_t scratch_stride = 0;
   TdDevCfg dcfg;
@@ -200,6 +202,21 @@ void parallel_for(int n, F fn) {
       for (int i = w; i < n; i += nt) fn(i);
     });
   for (auto& t : pool) t.join();
+}
+
+// The step kernel (td_set_step_kernel): small = 0 large, 1 small, 2 small2.  Write-through
+// observation stores go with the small kernels where the batch's observation fits the
+// 256-MiB Infinity Cache (scripts/storepol.hip: 21.8 vs 30.0 us at 8,192 boards).
+void apply_kernel(td_handle* h, int small) {
+  h->small = small;
+  const double obs_bytes = (double)h->B * NCH * h->NC * 4.0;
+  h->obs_wt = h->small && obs_bytes <= 192.0 * 1024 * 1024 ? 1 : 0;
+  if (const char* e = std::getenv("TD_OBS_WT")) h->obs_wt = std::atoi(e) ? 1 : 0;  // A/B runs
+  const bool has_small = h->L == 10 || h->L == 20 || h->L == 30;
+  const char* k = !has_small || small == 0 ? "td_step_kernel" : small == 1 ? "td_step_kernel_small" : "td_step_kernel_small2";
+  char buf[96];
+  std::snprintf(buf, sizeof buf, "%s<%d, %d, %s>", k, has_small ? h->L : 0, h->mode, h->multi ? "true" : "false");
+  h->kernel_name = buf;
 }
 
 // Drop staged layouts: they were drawn from a stream that has been replaced.
@@ -385,19 +402,14 @@ td_handle* td_create(const td_config* cfg, int map_size, int n_boards, int mode,
   }
   if (!rc && hipEventCreateWithFlags(&h->ev_main, hipEventDisableTiming) != hipSuccess) rc = fail("event");
   if (rc) { std::string e = g_err; td_destroy(h); g_err = e; return nullptr; }
-  {  // the small-batch kernel where the whole batch is one round of waves, and
-     // write-through observation stores where the batch's observation fits the 256-MiB
-     // Infinity Cache (TD_SMALL / TD_OBS_WT = 0|1 override, for A/B runs)
+  {  // TD_KERNEL_AUTO: the small-batch kernel where the whole batch is one round of waves,
+     // two waves per board up to half a round (td_set_step_kernel overrides)
     int cus = 0;
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
     const int resident = step_resident_boards(base_args(h), cus, 1);
     const int resident2 = step_resident_boards(base_args(h), cus, 2);
-    const double obs_bytes = (double)n_boards * NCH * h->NC * 4.0;
-    h->small = n_boards <= resident2 ? 2 : n_boards <= resident ? 1 : 0;
-    h->obs_wt = h->small && obs_bytes <= 192.0 * 1024 * 1024 ? 1 : 0;
-    auto ov = [](const char* name, int& v) { if (const char* e = std::getenv(name)) v = std::atoi(e) ? 1 : 0; };
-    if (const char* e = std::getenv("TD_SMALL")) h->small = std::max(0, std::min(2, std::atoi(e)));
-    ov("TD_OBS_WT", h->obs_wt);
+    h->small_auto = n_boards <= resident2 ? 2 : n_boards <= resident ? 1 : 0;
+    apply_kernel(h, h->small_auto);
     if (const char* e = std::getenv("TD_REFILL_EVERY")) h->refill_every = std::max(0, std::atoi(e));  // A/B runs
     if (const char* e = std::getenv("TD_REFILL_WAVES")) h->refill_waves = std::max(1, std::atoi(e));
     if (const char* e = std::getenv("TD_REFILL_WALKS")) h->refill_walks = std::max(1, std::atoi(e));
@@ -629,6 +641,7 @@ int td_step(td_handle* h, const td_step_io* io, void* stream) {
   a.def_act = io->def_act; a.atk_act = io->atk_act; a.obs = io->obs; a.reward = io->reward; a.done = io->done;
   a.real_def = io->real_def; a.real_atk = io->real_atk; a.fail_def = io->fail_def; a.fail_atk = io->fail_atk;
   a.win = io->win; a.allow_next = io->allow_next; a.ep_return = io->ep_return; a.ep_len = io->ep_len;
+  a.cooldowns = io->cooldowns;
   a.stamps = h->d_stamps;
   a.ep_stats = h->d_epstats;
   a.last_ep = h->d_lastep;
@@ -650,6 +663,20 @@ int td_step(td_handle* h, const td_step_io* io, void* stream) {
   h->steps += 1;
   return 0;
 }
+
+int td_set_step_kernel(td_handle* h, int kind) {
+  if (!h) return fail("NULL handle");
+  if (kind < TD_KERNEL_AUTO || kind > TD_KERNEL_SMALL2) return fail("td_set_step_kernel: unknown kernel kind %d", kind);
+  if (kind >= TD_KERNEL_SMALL && h->L != 10 && h->L != 20 && h->L != 30)
+    return fail("td_set_step_kernel: L = %d has no small-batch step kernel (only L = 10 / 20 / 30)", h->L);
+  HIP_OK(hipDeviceSynchronize());  // launches already queued keep the kernel they were enqueued with
+  apply_kernel(h, kind == TD_KERNEL_AUTO ? h->small_auto : kind - 1);
+  return 0;
+}
+
+int td_step_kernel(td_handle* h) { return h ? h->small + 1 : fail("NULL handle"); }
+
+const char* td_step_kernel_name(td_handle* h) { return h ? h->kernel_name.c_str() : ""; }
 
 int td_set_refill_interval(td_handle* h, int steps) {
   if (!h || steps < 0) return fail("td_set_refill_interval: bad arguments");
@@ -785,7 +812,25 @@ static int state_copy(td_handle* h, int b0, int count, void* host, bool to_host)
 
 int td_export_state(td_handle* h, int b0, int count, void* host_dst) { return state_copy(h, b0, count, host_dst, true); }
 
+// A record whose board has a layout must carry the captured max_cost / max_base_LP the
+// step divides by (TdHdr.format: header format 2); a record of another format, or a
+// hand-built one with zeros there, would silently clamp every cost to 0 and divide the
+// observation's scalar channels by zero.
 int td_import_state(td_handle* h, int b0, int count, const void* host_src) {
+  if (!h || !host_src || b0 < 0 || count < 0 || b0 + count > h->B) return fail("td_import_state: bad arguments");
+  const TdHdr* hdr = static_cast<const TdHdr*>(host_src);
+  for (int i = 0; i < count; ++i) {
+    const TdHdr& x = hdr[i];
+    if (x.num_roads < 1 || x.num_roads > 3) continue;  // a board never reset: nothing is stepped
+    if (x.format != kHdrFormat)
+      return fail("td_import_state: board %d: header format 0x%x, expected 0x%x (a record of another build?)",
+                  b0 + i, (unsigned)x.format, (unsigned)kHdrFormat);
+    if (!(x.max_cost > 0.0) || x.max_base_LP < 1)
+      return fail("td_import_state: board %d: max_cost %g / max_base_LP %d (must be > 0 / >= 1)", b0 + i, x.max_cost,
+                  x.max_base_LP);
+    if (x.n_en < 0 || x.n_en > ECAP || x.n_tw < 0 || x.n_tw > TCAP)
+      return fail("td_import_state: board %d: %d enemies / %d towers exceed the capacity", b0 + i, x.n_en, x.n_tw);
+  }
   return state_copy(h, b0, count, const_cast<void*>(host_src), false);
 }
 

@@ -45,8 +45,10 @@ struct alignas(16) TdHdr {  // 96 bytes
   int32_t start_cell[3], maxdist;
   int32_t flags, episodes;
   double max_cost;             // captured at reset (TDBoard.py:70, passed by TDGymBasic.reset :43-53)
-  int32_t max_base_LP, pad;    // :72
+  int32_t max_base_LP;         // :72
+  int32_t format;              // kHdrFormat on every board a kernel has reset (td_import_state checks it)
 };
+constexpr int32_t kHdrFormat = 0x54440002;  // "TD", header format 2 (max_cost / max_base_LP captured)
 static_assert(sizeof(TdHdr) == 96, "TdHdr layout");
 
 // Device constant block (built on the host from paramConfig-style values).  The device

@@ -59,6 +59,7 @@ struct StepArgs {
   int32_t* fail_atk;
   int8_t* win;
   uint8_t* allow_next;
+  uint8_t* cooldowns;
   double* ep_return;
   int32_t* ep_len;
   double* ep_stats;  // [2]: finished episodes, sum of their returns (accumulated by the step kernel)

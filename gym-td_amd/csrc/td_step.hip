@@ -1328,7 +1328,7 @@ __device__ __forceinline__ void store_board(const Smem<NC>& S, const U& u, const
     h.n_en = u.n; h.n_tw = u.nt; h.num_roads = u.num_roads; h.end_cell = u.end_cell;
     h.start_cell[0] = u.start(0); h.start_cell[1] = u.start(1); h.start_cell[2] = u.start(2);
     h.maxdist = u.maxdist; h.flags = u.flags; h.episodes = u.episodes;
-    h.max_cost = u.max_cost; h.max_base_LP = u.max_base_LP; h.pad = 0;
+    h.max_cost = u.max_cost; h.max_base_LP = u.max_base_LP; h.format = kHdrFormat;
     a.hdr[b] = h;
   }
   const size_t tb = (size_t)b * TCAP;
@@ -1599,10 +1599,11 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
     if (MODE == MODE_ATK) win = u.base_LP <= 0 ? 1 : 0;
     else win = u.base_LP > 0 ? 1 : 0;
   }
-  // info['AllowNextMove'] bits 0-1; bits 2-4 / 5-7: the cool-downs themselves, saturated at 7
-  // (TDGymBasic's attacker_cd / defender_cd attributes after the step)
-  const int acd = u.atk_cd < 7 ? u.atk_cd : 7, dcd = u.def_cd < 7 ? u.def_cd : 7;
-  const uint8_t allow = (uint8_t)((u.atk_cd <= 1 ? 1 : 0) | (u.def_cd <= 1 ? 2 : 0) | (acd << 2) | (dcd << 5));
+  // info['AllowNextMove'] (bits 0-1), and the env's attacker_cd / defender_cd attributes
+  // after the step, saturated at 15 (td_step_io.cooldowns)
+  const uint8_t allow = (uint8_t)((u.atk_cd <= 1 ? 1 : 0) | (u.def_cd <= 1 ? 2 : 0));
+  const int acd = u.atk_cd < 15 ? u.atk_cd : 15, dcd = u.def_cd < 15 ? u.def_cd : 15;
+  const uint8_t cool = (uint8_t)(acd | (dcd << 4));
   const double ep_ret = u.ep_ret;
 
   if (done) u.episodes += 1;
@@ -1659,6 +1660,7 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
     sst(&a.done[b], (uint8_t)(done ? 1 : 0));
     if (a.win) sst(&a.win[b], win);
     if (a.allow_next) sst(&a.allow_next[b], allow);
+    if (a.cooldowns) sst(&a.cooldowns[b], cool);
     if (a.fail_def) sst(&a.fail_def[b], (int32_t)fail_def);
     if (a.real_def && !a.multi) sst(&a.real_def[b], real_def);
     if (a.ep_return) sst(&a.ep_return[b], ep_ret);
@@ -2299,14 +2301,18 @@ __global__ __launch_bounds__(64) void td_reset_kernel(StepArgs a) {
 // finished boards in turn, drawing each layout from the board's stream now, exactly
 // where the reference's reset() would -- failing draws skipped as in every auto-reset.
 // The step kernel left those boards finished (no staged layout is consumed in this
-// mode); their observation is overwritten with the new episode's first one.
+// mode); their observation is overwritten with the new episode's first one.  Boards
+// flagged FLAG_NO_LAYOUT are skipped: a board never reset (its first road generation
+// failed, done every step) or whose auto-reset already failed 65 draws in a row stays
+// as it is until an explicit reset, as under random_agent=True -- it neither stalls
+// the step stream with 65 draws every step nor consumes its stream.
 template <int LT>
 __global__ __launch_bounds__(64) void td_autoreset_kernel(StepArgs a) {
   constexpr int NC = LT ? LT * LT : MAX_KERNEL_L * MAX_KERNEL_L;
   __shared__ ResetSmem<NC> sh;
   const int lane = (int)threadIdx.x;
   const int b0 = (int)blockIdx.x * 64;
-  const bool mine = b0 + lane < a.B && a.done[b0 + lane] != 0;
+  const bool mine = b0 + lane < a.B && a.done[b0 + lane] != 0 && !(a.hdr[b0 + lane].flags & FLAG_NO_LAYOUT);
   uint64_t m = ballot(mine);
   while (m) {
     const int b = b0 + ctz64(m);

@@ -17,6 +17,8 @@ ECAP, TCAP, NCH = 128, 32, 45
 MT_WORDS = 625
 OPP_WORDS = 626
 HDR_BYTES = 96
+ABI_VERSION = 2  # include/tdstep.h TD_ABI_VERSION
+STEP_KERNELS = {"auto": 0, "large": 1, "small": 2, "small2": 3}  # enum td_step_kernel_kind
 
 c_u32p = ctypes.POINTER(ctypes.c_uint32)
 c_i32p = ctypes.POINTER(ctypes.c_int32)
@@ -43,7 +45,7 @@ class TdStepIO(ctypes.Structure):
     """struct td_step_io (tdstep.h): device pointers."""
     _fields_ = [(n, c_vp) for n in (
         "def_act", "atk_act", "obs", "reward", "done", "real_def", "real_atk", "fail_def", "fail_atk",
-        "win", "allow_next", "ep_return", "ep_len")]
+        "win", "allow_next", "ep_return", "ep_len", "cooldowns")]
 
 
 def _load():
@@ -81,6 +83,9 @@ def _load():
         "td_episode_records": (ctypes.c_int, [c_vp, c_vp, c_vp]),
         "td_opponent": (ctypes.c_int, [c_vp, ctypes.c_int, ctypes.c_int, c_u8p, c_vp]),
         "td_set_refill_interval": (ctypes.c_int, [c_vp, ctypes.c_int]),
+        "td_set_step_kernel": (ctypes.c_int, [c_vp, ctypes.c_int]),
+        "td_step_kernel": (ctypes.c_int, [c_vp]),
+        "td_step_kernel_name": (ctypes.c_char_p, [c_vp]),
         "td_config_epoch": (ctypes.c_int, [c_vp]),
         "td_kernel_timing": (ctypes.c_int, [c_vp, ctypes.c_int, ctypes.c_int]),
         "td_kernel_times": (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_float), ctypes.c_int]),
@@ -94,7 +99,7 @@ def _load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.td_abi_version() != 1:
+    if lib.td_abi_version() != ABI_VERSION:
         raise ImportError("libtdstep.so ABI version mismatch")
     return lib
 

@@ -20,7 +20,7 @@ HDR_DTYPE = np.dtype([
     ("cost_def", "<f8"), ("cost_atk", "<f8"), ("ep_return", "<f8"), ("steps", "<i4"), ("base_LP", "<i4"),
     ("atk_cd", "<i4"), ("def_cd", "<i4"), ("n_en", "<i4"), ("n_tw", "<i4"), ("num_roads", "<i4"),
     ("end_cell", "<i4"), ("start_cell", "<i4", (3,)), ("maxdist", "<i4"), ("flags", "<i4"), ("episodes", "<i4"),
-    ("max_cost", "<f8"), ("max_base_LP", "<i4"), ("pad", "<i4")])
+    ("max_cost", "<f8"), ("max_base_LP", "<i4"), ("format", "<i4")])
 assert HDR_DTYPE.itemsize == _lib.HDR_BYTES
 
 
@@ -48,11 +48,13 @@ class TDEngine(object):
     random_agent: TDGymBasic's random_agent (False: the built-in opponent draws from
           each board's layout stream; with auto-reset the next layout is then drawn
           right after the step that ends the episode, in stream order).
+    step_kernel: 'auto' (td_create's rule by batch size), 'large', 'small' or 'small2'
+          (td_set_step_kernel; the three give the same results).
     """
 
     def __init__(self, map_size, n_boards, mode="def", multi_action=None, difficulty=1, device=None,
                  np_seeds=None, py_seeds=None, autoreset=True, info=True, cfg=None, hp=None, host_io=False,
-                 random_agent=True):
+                 random_agent=True, step_kernel="auto"):
         hp = hp or P.hyper_parameters
         if multi_action is None:
             multi_action = bool(hp.allow_multiple_actions)
@@ -84,11 +86,12 @@ class TDEngine(object):
         self.reward = zeros(B, torch.float64)
         self.done = zeros(B, torch.uint8)
         self.info_enabled = bool(info)
-        self.win = self.allow_next = self.ep_return = self.ep_len = None
+        self.win = self.allow_next = self.cooldowns = self.ep_return = self.ep_len = None
         self.real_def = self.fail_def = self.real_atk = self.fail_atk = None
         if info:
             self.win = zeros(B, torch.int8)
             self.allow_next = zeros(B, torch.uint8)
+            self.cooldowns = zeros(B, torch.uint8)
             self.ep_return = zeros(B, torch.float64)
             self.ep_len = zeros(B, torch.int32)
             if mode != "atk":
@@ -106,7 +109,7 @@ class TDEngine(object):
         # conversion or a scalar read through torch costs microseconds per step)
         self.np = types.SimpleNamespace()
         for name in ("obs", "reward", "done", "real_def", "real_atk", "fail_def", "fail_atk", "win",
-                     "allow_next", "ep_return", "ep_len"):
+                     "allow_next", "cooldowns", "ep_return", "ep_len"):
             t = getattr(self, name)
             setattr(self._io, name, t.data_ptr() if t is not None else None)
             if self.host_io:
@@ -116,6 +119,8 @@ class TDEngine(object):
             self._atk_np = self._atk_in.numpy() if self._atk_in is not None else None
         if np_seeds is not None or py_seeds is not None:
             self.seed(np_seeds, py_seeds)
+        if step_kernel != "auto":
+            self.set_step_kernel(step_kernel)
         P._live.add(self)
 
     # ------------------------------------------------------------------ setup
@@ -304,6 +309,23 @@ class TDEngine(object):
             m = np.ascontiguousarray(np.asarray(mask, dtype=np.uint8).reshape(self.B))
         _lib.check(_lib.lib.td_opponent(self._h, {"enemy": 0, "tower": 1}[side], int(level),
                                         _lib.ptr(m, _lib.ctypes.c_uint8) if m is not None else None, self._stream()))
+
+    def set_step_kernel(self, kind):
+        """Select the step kernel: 'auto', 'large', 'small' or 'small2' (td_set_step_kernel)."""
+        if kind not in _lib.STEP_KERNELS:
+            raise ValueError("step kernel must be one of %s" % sorted(_lib.STEP_KERNELS))
+        _lib.check(_lib.lib.td_set_step_kernel(self._h, _lib.STEP_KERNELS[kind]))
+
+    @property
+    def step_kernel(self):
+        """The step kernel td_step launches: 'large', 'small' or 'small2'."""
+        k = _lib.check(_lib.lib.td_step_kernel(self._h))
+        return {v: n for n, v in _lib.STEP_KERNELS.items()}[k]
+
+    @property
+    def step_kernel_name(self):
+        """Its name as rocprofv3 reports it, e.g. 'td_step_kernel_small<10, 0, false>'."""
+        return _lib.lib.td_step_kernel_name(self._h).decode()
 
     def set_refill_interval(self, steps):
         """Steps between layout-refill launches (auto-reset; 0 = none, rings only drain)."""

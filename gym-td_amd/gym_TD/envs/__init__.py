@@ -164,12 +164,13 @@ class _TDBasic(object):
         win = int(n.win[0])
         an = int(n.allow_next[0])
         # TDGymBasic's cool-down attributes (TDDefense.py:38-39,75; TDAttack.py:31-32,44):
-        # allow_next carries them saturated at 7, the board header holds them exactly
-        self.attacker_cd, self.defender_cd = (an >> 2) & 7, (an >> 5) & 7
-        if self.attacker_cd == 7 or self.defender_cd == 7:
+        # the cooldowns output carries them saturated at 15, the board header holds them exactly
+        cd = int(n.cooldowns[0])
+        self.attacker_cd, self.defender_cd = cd & 15, cd >> 4
+        if self.attacker_cd == 15 or self.defender_cd == 15:
             h = e.export_state(0, 1)["hdr"][0]
             self.attacker_cd, self.defender_cd = int(h["atk_cd"]), int(h["def_cd"])
-        return self._obs.copy(), reward, done, (None if win < 0 else bool(win)), an & 3
+        return self._obs.copy(), reward, done, (None if win < 0 else bool(win)), an
 
     def render(self, mode="human"):
         raise NotImplementedError("rendering (TDBoard.render, pyglet) is out of scope for the device engine")
@@ -345,7 +346,7 @@ class TDVecEnv(object):
         e = self.engine
         infos = {}
         if e.info_enabled:
-            infos = {"Win": e.win, "AllowNextMove": e.allow_next & 3, "episode_return": e.ep_return,
+            infos = {"Win": e.win, "AllowNextMove": e.allow_next, "episode_return": e.ep_return,
                      "episode_length": e.ep_len}
             if e.real_def is not None:
                 infos["RealAction"] = e.real_def

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define TD_ABI_VERSION 1
+#define TD_ABI_VERSION 2
 
 enum td_mode { TD_MODE_DEF = 0, TD_MODE_ATK = 1, TD_MODE_2P = 2 };
 
@@ -77,9 +77,12 @@ typedef struct td_config {
  *   fail_def  int32 [B]   fail_atk int32 [B][3] (-1 = no entry)       info['FailCode']
  *   win       int8 [B] (-1 = None)                                     info['Win']
  *   allow_next uint8 [B] (bit0 attacker_cd<=1, bit1 defender_cd<=1)   info['AllowNextMove']
- *             bits 2-4 / 5-7: attacker_cd / defender_cd after the step, saturated at 7
+ *             (bits 2-7 are always 0)
  *   ep_return double [B], ep_len int32 [B]: running episode return / length after this
- *             step (the finished episode's totals when done[b]). */
+ *             step (the finished episode's totals when done[b]).
+ *   cooldowns uint8 [B]: the env's attacker_cd (bits 0-3) and defender_cd (bits 4-7) after the
+ *             step (TDDefense.py:38-39,75, TDAttack.py:31-32,44), each saturated at 15
+ *             (ABI 2; ABI 1 packed them into allow_next bits 2-7). */
 typedef struct td_step_io {
   const int64_t* def_act;
   const int64_t* atk_act;
@@ -94,6 +97,7 @@ typedef struct td_step_io {
   uint8_t* allow_next;
   double* ep_return;
   int32_t* ep_len;
+  uint8_t* cooldowns;
 } td_step_io;
 
 typedef struct td_handle td_handle;
@@ -156,6 +160,26 @@ int td_reset_layouts(td_handle* h, const uint32_t* recs, const int32_t* boards, 
  * and real-action arrays) takes the line-aligned 16-B store path, any other the
  * per-element one (same bytes, slower). */
 int td_step(td_handle* h, const td_step_io* io, void* stream);
+
+/* Which step kernel td_step launches (one wave per board in all three; they differ in
+ * occupancy and load schedule, not in results):
+ *   TD_KERNEL_LARGE  td_step_kernel        several rounds of waves (7 per SIMD), live slots
+ *                                          loaded once the header's counts are in;
+ *   TD_KERNEL_SMALL  td_step_kernel_small  one round (8 waves per SIMD), 16 enemy + 16 tower
+ *                                          slots prefetched with the header;
+ *   TD_KERNEL_SMALL2 td_step_kernel_small2 as SMALL, plus a second wave per board that
+ *                                          writes half of the observation;
+ *   TD_KERNEL_AUTO   td_create's rule: SMALL2 up to half a round of boards, SMALL up to one
+ *                    round, else LARGE (L = 10 / 20 / 30; other L only have LARGE).
+ * The small kernels need a 16-B-aligned observation buffer; a td_step with any other
+ * buffer runs LARGE.  td_set_step_kernel fails (and changes nothing) for a small kernel
+ * at an L without one.  td_step_kernel returns the resolved kind, td_step_kernel_name the
+ * kernel's name as rocprofv3 shows it ("td_step_kernel_small<10, 0, false>": L, mode,
+ * multi-action scan). */
+enum td_step_kernel_kind { TD_KERNEL_AUTO = 0, TD_KERNEL_LARGE = 1, TD_KERNEL_SMALL = 2, TD_KERNEL_SMALL2 = 3 };
+int td_set_step_kernel(td_handle* h, int kind);
+int td_step_kernel(td_handle* h);
+const char* td_step_kernel_name(td_handle* h);
 
 /* Steps between launches of the layout refill kernel on the side streams (auto-reset;
  * default 16, 0 = none: the staged rings then only drain).  A tuning / diagnostic knob. */

@@ -1,0 +1,27 @@
+#!/bin/bash
+# Round-3 GPU sessions: bash scripts/r03.sh <session>.  Every GPU step runs under its own
+# time limit; the session stops at the first crash / timeout (pytest's 1 = failures
+# is reported and the session goes on only where noted).
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+export TMPDIR=/tmp
+S=$1
+O=gpurun_out/r03_$S
+mkdir -p $O
+run() { local name=$1 secs=$2; shift 2; echo "== $name $(date +%T)"; timeout -k 10 "$secs" "$@" > "$O/$name.log" 2>&1; local rc=$?; echo "== $name rc=$rc"; [ $rc -ne 0 ] && tail -25 "$O/$name.log"; return $rc; }
+line() { grep -h '^{' "$O/$1.log" | python3 -c "import json,sys
+for l in sys.stdin: d=json.loads(l); r=d['roofline']; print('   %-18s' % '$1', round(d['value']/1e6,1), 'M/s  step', round(d['ms_per_step']*1e3,2), 'us  kernel', round(r['avg_kernel_us'],2), 'frac', round(r['frac'],3), r['kernel'], 'n', d['n_gpus'], d.get('world_size_reported'), 'B/gpu', d['config']['boards_per_gpu'], 'flags', d.get('board_flags'), 'eps', d['episodes']['finished'])"; }
+case $S in
+s1)  # the kernel-parametrised parity suite, smoke, default line, N = 2 self-launch rehearsal
+  run pytest_gpu 700 python -u -m pytest tests -m gpu -q --timeout 400 --timeout-method thread -p no:cacheprovider
+  rc=$?; tail -3 $O/pytest_gpu.log; [ $rc -le 1 ] || exit $rc
+  run smoke 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" || exit 1
+  run bench_default 300 python bench.py || exit 1
+  grep '^{' $O/bench_default.log; line bench_default
+  export TD_BENCH_DIST_BACKEND=gloo TD_BENCH_SAME_DEVICE=1
+  run bench_n2 300 python bench.py --gpus 2 --no-cpu-baseline --steps 200 || exit 1
+  unset TD_BENCH_DIST_BACKEND TD_BENCH_SAME_DEVICE
+  line bench_n2
+  ;;
+*) echo "unknown session $S"; exit 2 ;;
+esac
+echo "session $S rc=0"

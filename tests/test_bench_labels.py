@@ -35,13 +35,40 @@ def test_traffic_only_for_the_measured_build(tmp_path, monkeypatch):
     assert len(bench.kernel_source_hash()) == 16
 
 
-@pytest.mark.parametrize("world,kernel", [(1, "td_step_kernel<10, DEF>"), (2, "td_step_kernel<10, DEF>"),
-                                          (4, "td_step_kernel<10, DEF>"), (8, "td_step_kernel_small<10, DEF>")])
-def test_roofline_names_the_kernel_that_runs(world, kernel, monkeypatch):
-    # td_create's rule on a 256-CU MI355X: one round of waves (8 per SIMD) -> small kernel,
-    # half a round -> two waves per board
-    monkeypatch.delenv("TD_SMALL", raising=False)
-    B, _, _ = bench.partition("def-small", world)
-    assert bench.step_kernel_name(10, "def", B, 256) == kernel
-    assert bench.step_kernel_name(10, "def", 4096, 256) == "td_step_kernel_small2<10, DEF>"
-    assert bench.step_kernel_name(20, "2p", 16384, 256) == "td_step_kernel<20, 2P>"
+def test_world_must_match_gpus():
+    # under a launcher, WORLD_SIZE must equal --gpus; without one, --gpus N > 1 launches N ranks
+    assert bench.check_world(1, {}) == 1
+    assert bench.check_world(8, {}) is None
+    assert bench.check_world(8, {"WORLD_SIZE": "8"}) == 8
+    with pytest.raises(SystemExit):
+        bench.check_world(1, {"WORLD_SIZE": "2"})
+
+
+def test_mismatched_world_exits_nonzero():
+    """bench.py under a launcher that started another rank count than --gpus says exits
+    non-zero before it touches a GPU."""
+    import os
+    import subprocess
+    import sys
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, bench.__file__, "--gpus", "1"], env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert p.returncode != 0
+    assert "WORLD_SIZE=2" in p.stderr
+
+
+def test_gpus_n_starts_n_ranks(monkeypatch):
+    """--gpus N > 1 with no launcher: torch.distributed.run with N processes on 127.0.0.1,
+    started as a child (never an exec of this process), its status returned."""
+    import subprocess
+    seen = {}
+
+    def fake_call(cmd):
+        seen["cmd"] = cmd
+        return 3
+    monkeypatch.setattr(subprocess, "call", fake_call)
+    assert bench.launch_ranks(4, ["--gpus", "4", "--steps", "5"]) == 3
+    cmd = seen["cmd"]
+    assert cmd[1:3] == ["-m", "torch.distributed.run"]
+    assert cmd[cmd.index("--nproc-per-node") + 1] == "4" and cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert cmd[-4:] == [bench.os.path.abspath(bench.__file__), "--gpus", "4", "--steps", "5"][-4:]

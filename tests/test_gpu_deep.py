@@ -9,8 +9,9 @@ finishes its episode and auto-resets onto its next staged layout (failing draws
 skipped on both sides).  The two shapes are chosen so that boards carry more than
 64 live enemies (10x10, an idle defender against a fast attacker) and more than 16
 towers (20x20, a builder defender): the step kernel prefetches 16 enemy and 16 tower
-slots with the header and loads the rest afterwards, and lanes hold enemies l and
-l + 64 (td_step.hip prefetch_issue / load_board / board_step)."""
+slots with the header and loads the rest afterwards (the large kernel loads exactly the
+live slots once the header is in), and lanes hold enemies l and l + 64 (td_step.hip
+prefetch_issue / load_board / board_step).  Each shape runs on all three step kernels."""
 import copy
 
 import numpy as np
@@ -61,10 +62,11 @@ def _reset_skipping(env):
 # 10x10: an idle defender against a fast attacker (cost rates 4 -> 8 per step): 25-65 live
 # enemies per board late in the episode, past the 16 prefetched slots and past lane 63.
 # 20x20: a builder defender: up to ~24 towers per board.
+@pytest.mark.parametrize("kernel", ("large", "small", "small2"))
 @pytest.mark.parametrize("L,B,p_build,over", [
     (10, 128, 0.0, dict(attacker_cost_init_rate=4, attacker_cost_final_rate=8)),
     (20, 64, 0.8, {})])
-def test_deep_batched_autoreset_vs_c_oracle(L, B, p_build, over):
+def test_deep_batched_autoreset_vs_c_oracle(L, B, p_build, over, kernel):
     steps, every = 1300, 25
     over = dict(over, base_LP=10 ** 6)
     cfg = O.Config(**over)
@@ -80,8 +82,10 @@ def test_deep_batched_autoreset_vs_c_oracle(L, B, p_build, over):
     dcfg = copy.deepcopy(P.config)
     for key, v in over.items():
         setattr(dcfg, key, v)
-    eng = TDEngine(L, B, "def", False, 1, np_seeds=seeds, py_seeds=seeds, autoreset=True, cfg=dcfg)
+    eng = TDEngine(L, B, "def", False, 1, np_seeds=seeds, py_seeds=seeds, autoreset=True, cfg=dcfg,
+                   step_kernel=kernel)
     try:
+        assert eng.step_kernel == kernel
         obs, failed = eng.reset()
         assert not failed
         ob = obs.cpu().numpy()

@@ -46,7 +46,7 @@ def _fc_list(row):
     return [int(v) for v in row if v >= 0]
 
 
-@pytest.mark.parametrize("L,B,mode,multi,difficulty,steps,random_agent", [
+_MODE_CASES = [
     (10, 24, "atk", False, 0, 150, True),
     (10, 24, "atk", False, 1, 150, True),
     (10, 24, "atk", False, 2, 150, True),
@@ -66,14 +66,20 @@ def _fc_list(row):
     (10, 24, "atk", False, 1, 150, False),
     (20, 12, "atk", False, 2, 100, False),
     (30, 6, "def", False, 1, 80, False),
-])
-def test_batched_modes_vs_oracle(L, B, mode, multi, difficulty, steps, random_agent):
+]
+
+
+@pytest.mark.parametrize("L,B,mode,multi,difficulty,steps,random_agent,kernel", [
+    c + (k,) for c in _MODE_CASES for k in (("large", "small", "small2") if c[0] in (10, 20, 30) else ("large",))])
+def test_batched_modes_vs_oracle(L, B, mode, multi, difficulty, steps, random_agent, kernel):
     """B boards of one mode in one launch vs B oracle envs: reward bits, done,
-    state digest, observation bytes and the info tensors of every board."""
+    state digest, observation bytes and the info tensors of every board, on every step
+    kernel the map size has."""
     seeds, orc = _first_ok_seeds(L, B, 3000 + 97 * difficulty, mode, multi, difficulty, random_agent=random_agent)
     eng = TDEngine(L, B, mode, multi, difficulty, np_seeds=seeds, py_seeds=seeds, autoreset=False,
-                   random_agent=random_agent)
+                   random_agent=random_agent, step_kernel=kernel)
     try:
+        assert eng.step_kernel == kernel
         _, failed = eng.reset()
         assert not failed
         rng = np.random.RandomState(L * 31 + difficulty)
@@ -90,6 +96,8 @@ def test_batched_modes_vs_oracle(L, B, mode, multi, difficulty, steps, random_ag
                      atk_act=None if aa is None else torch.from_numpy(aa))
             ob, rw, dn = eng.obs.cpu().numpy(), eng.reward.cpu().numpy(), eng.done.cpu().numpy()
             win, an = eng.win.cpu().numpy(), eng.allow_next.cpu().numpy()
+            cdn = eng.cooldowns.cpu().numpy()
+            assert (an & ~3 == 0).all()  # AllowNextMove bits only (ABI 2: cool-downs have their own output)
             rd = eng.real_def.cpu().numpy() if eng.real_def is not None else None
             fd = eng.fail_def.cpu().numpy() if eng.fail_def is not None else None
             ra = eng.real_atk.cpu().numpy() if eng.real_atk is not None else None
@@ -109,6 +117,7 @@ def test_batched_modes_vs_oracle(L, B, mode, multi, difficulty, steps, random_ag
                 if isinstance(w, dict):
                     w = w["Defender"] if mode != "atk" else w["Attacker"]
                 assert (int(win[b]) if win[b] >= 0 else None) == (None if w is None else int(w)), tag
+                assert (int(cdn[b]) & 15, int(cdn[b]) >> 4) == (min(o.attacker_cd, 15), min(o.defender_cd, 15)), tag
                 anm = info["AllowNextMove"]
                 if mode == "2p":
                     assert bool(an[b] & 1) == anm["Attacker"] and bool(an[b] & 2) == anm["Defender"], tag
@@ -378,6 +387,137 @@ def test_export_import_roundtrip():
         b_eng.close()
 
 
+def test_step_kernel_selector():
+    """td_set_step_kernel: every kind at L = 10 / 20 / 30, named as rocprofv3 names the
+    kernel; a small kernel at an L without one is refused and changes nothing."""
+    from gym_TD import _lib
+    for L in (10, 20, 30):
+        eng = TDEngine(L, 4, "def", False, 1, np_seeds=[1, 2, 3, 4], py_seeds=[1, 2, 3, 4])
+        try:
+            for k, name in (("large", "td_step_kernel<"), ("small", "td_step_kernel_small<"),
+                            ("small2", "td_step_kernel_small2<")):
+                eng.set_step_kernel(k)
+                assert eng.step_kernel == k and eng.step_kernel_name == "%s%d, 0, false>" % (name, L)
+            eng.set_step_kernel("auto")
+            assert eng.step_kernel == "small2"  # 4 boards: half a round of waves or less
+        finally:
+            eng.close()
+    eng = TDEngine(12, 4, "2p", True, 1, np_seeds=[1, 2, 3, 4], py_seeds=[1, 2, 3, 4])
+    try:
+        assert eng.step_kernel == "large" and eng.step_kernel_name == "td_step_kernel<0, 2, true>"
+        with pytest.raises(_lib.TDError, match="no small-batch"):
+            eng.set_step_kernel("small")
+        assert eng.step_kernel == "large"
+    finally:
+        eng.close()
+
+
+def test_import_refuses_records_without_captured_fields():
+    """A state record whose max_cost / max_base_LP (TdHdr, captured at reset: TDBoard.py:66-72)
+    are zero -- a record of an older header format, or a hand-built one -- would clamp every
+    cost to 0 and divide the scalar observation channels by zero: td_import_state refuses
+    it and changes nothing.  Boards never reset (no layout) carry no such fields."""
+    from gym_TD import _lib
+    L, B = 10, 8
+    seeds, _ = _first_ok_seeds(L, B, 6100, "def", False, 1)
+    eng = TDEngine(L, B, "def", False, 1, np_seeds=seeds, py_seeds=seeds, autoreset=False)
+    try:
+        eng.reset()
+        good = eng.export_state()
+        before = [canon.state_digest(eng.board_state(b)) for b in range(B)]
+        for field, value in (("max_cost", 0.0), ("max_base_LP", 0), ("format", 0), ("n_en", 129)):
+            st = {k: np.array(v, copy=True) for k, v in good.items()}
+            st["hdr"][3][field] = value
+            with pytest.raises(_lib.TDError, match="board 3"):
+                eng.import_state(st)
+            assert [canon.state_digest(eng.board_state(b)) for b in range(B)] == before, field
+        # a never-reset board (zero header, num_roads 0) imports as it is
+        st = {k: np.array(v, copy=True) for k, v in good.items()}
+        st["hdr"][5] = np.zeros(1, dtype=st["hdr"].dtype)[0]
+        eng.import_state(st)
+        assert eng.board_state(5)["num_roads"] == 0
+        eng.import_state(good)
+        assert [canon.state_digest(eng.board_state(b)) for b in range(B)] == before
+    finally:
+        eng.close()
+
+
+def test_config_epochs_recycled_past_256():
+    """paramConfig every step for 300 steps (a curriculum): the device has 256 constant
+    blocks, so after 255 changes td_set_config recycles blocks no live enemy or tower
+    refers to (td_cfg_usage_kernel).  Every entity must keep the values it captured
+    (TDElements.py:4-43, 134-170) -- bit-exact against the oracle through the recycling.
+    Then, with 256 epochs each held by a live tower, one more td_set_config fails cleanly
+    and leaves the current config in place."""
+    from gym_TD import _lib
+    from gym_TD import params as P
+    L, B = 10, 16
+    base = dict(tower_distance=0, defender_init_cost=400, max_cost=400, defender_cost_rate=2)
+
+    def cfg_at(k, into):
+        for key, v in base.items():
+            setattr(into, key, copy.deepcopy(v))
+        into.reward_time = 0.001 + k * 1e-6  # every step's config is distinct
+        into.enemy_LP = [[820 + 10 * (k % 11), 1700], [2050, 3000 + 7 * (k % 5)], [6000, 8000], [8000 - 3 * (k % 9), 12000]]
+        into.enemy_defense = [[k % 3, 0], [200 + k % 7, 250], [600, 800], [80, 100]]
+        into.enemy_speed = [[.25, .25], [.13 + .01 * (k % 2), .13], [.1, .1], [.1, .1]]
+        into.tower_attack = [[454 + k % 13, 540], [651, 771 + k % 4], [566 + k % 6, 691], [358, 424]]
+        into.tower_range = [[3 + k % 2, 3], [2, 2], [4, 4], [3, 3]]
+        return into
+
+    cfg0 = cfg_at(0, O.Config())
+    seeds, orc = _first_ok_seeds(L, B, 6200, "def", False, 1, cfg0)
+    dcfg = cfg_at(0, copy.deepcopy(P.config))
+    eng = TDEngine(L, B, "def", False, 1, np_seeds=seeds, py_seeds=seeds, autoreset=False, cfg=dcfg)
+    try:
+        eng.reset()
+        rng = np.random.RandomState(31)
+        seen = []
+        for k in range(1, 301):
+            eng.set_config(cfg_at(k, copy.deepcopy(P.config)))
+            seen.append(_lib.lib.td_config_epoch(eng._h))
+            for o in orc:
+                cfg_at(k, o.cfg)
+            acts = np.array([policies.discrete_def(rng, L, o._board.map[0], 0.7) for o in orc], dtype=np.int64)
+            eng.step(def_act=torch.from_numpy(acts))
+            ob, rw = eng.obs.cpu().numpy(), eng.reward.cpu().numpy()
+            st = eng.export_state()
+            for b, o in enumerate(orc):
+                if o._board.done():
+                    continue
+                wo, wr, _, _ = o.step(int(acts[b]))
+                assert canon.fhex(rw[b]) == canon.fhex(wr), (k, b)
+                assert canon.state_digest(eng.board_state(b, st)) == canon.state_digest(canon.oracle_state(o)), (k, b)
+                assert np.array_equal(ob[b], wo), (k, b, np.argwhere(ob[b] != wo)[:5].tolist())
+        assert len(set(seen)) == 256 and len(seen) == 300  # blocks were recycled
+    finally:
+        eng.close()
+    # all 256 blocks held by live towers: one tower per config epoch, board k % 16 building at step k
+    eng = TDEngine(L, B, "def", False, 1, np_seeds=seeds, py_seeds=seeds, autoreset=False, cfg=dcfg)
+    try:
+        eng.reset()
+        st = eng.export_state()
+        free = [[c for c in range(L * L) if (int(st["cells"][b][c]) >> 24) == 0] for b in range(B)]
+        empty = 6 * L * L
+        for k in range(256):
+            eng.set_config(cfg_at(1000 + k, copy.deepcopy(P.config)))
+            acts = np.full(B, empty, dtype=np.int64)
+            acts[k % B] = free[k % B][k // B]  # op 0 (arrow) at a free cell
+            eng.step(def_act=torch.from_numpy(acts))
+            assert int(eng.fail_def[k % B]) == 0, k
+        st = eng.export_state()
+        held = {(int(u) >> 16) & 0xFF for b in range(B) for u in st["tw_inf"][b][:int(st["hdr"][b]["n_tw"])]}
+        assert len(held) == 256
+        ep = _lib.lib.td_config_epoch(eng._h)
+        with pytest.raises(_lib.TDError, match="still referenced"):
+            eng.set_config(cfg_at(5000, copy.deepcopy(P.config)))
+        assert _lib.lib.td_config_epoch(eng._h) == ep
+        eng.step(def_act=torch.full((B,), empty, dtype=torch.int64))  # the engine keeps stepping
+        assert (eng.flags() == 0).all()
+    finally:
+        eng.close()
+
+
 def test_export_import_roundtrip_random_agent_false():
     """With random_agent=False the built-in opponent draws from the board's numpy layout
     stream, which td_export_state does not carry (include/tdstep.h): a snapshot is the
@@ -416,7 +556,8 @@ def test_export_import_roundtrip_random_agent_false():
         b_eng.close()
 
 
-def test_paramconfig_reaches_live_engines():
+@pytest.mark.parametrize("kernel", ("large", "small", "small2"))
+def test_paramconfig_reaches_live_engines(kernel):
     """paramConfig (TDParam.py:98-100) in the middle of episodes, twice, on a live engine.
     The reference reads most values live from `config`, but an Enemy / Tower keeps the
     stats it was created or upgraded with (TDElements.py:4-69, 134-170: maxLP, speed,
@@ -437,7 +578,7 @@ def test_paramconfig_reaches_live_engines():
                max_cost=150, attacker_cost_final_rate=1.5)
     seeds, orc = _first_ok_seeds(L, B, 7000, "def", False, 1)
     saved = {k: copy.deepcopy(getattr(P.config, k)) for k in set(ov1) | set(ov2)}
-    eng = TDEngine(L, B, "def", False, 1, np_seeds=seeds, py_seeds=seeds, autoreset=False)
+    eng = TDEngine(L, B, "def", False, 1, np_seeds=seeds, py_seeds=seeds, autoreset=False, step_kernel=kernel)
     try:
         eng.reset()
         rng = np.random.RandomState(8)
@@ -568,7 +709,8 @@ def test_autoreset_under_load_matches_explicit_reset(B, steps):
         eb.close()
 
 
-def test_many_towers_vs_oracle():
+@pytest.mark.parametrize("kernel", ("large", "small", "small2"))
+def test_many_towers_vs_oracle(kernel):
     """Boards with more towers than the step prefetches up front (16): tower distance
     1, rich defender.  Same bit-exact comparison as the batched tests."""
     from test_gpu_parity import reference_settings
@@ -577,7 +719,7 @@ def test_many_towers_vs_oracle():
     cfg = O.Config(**ov)
     seeds, orc = _first_ok_seeds(L, B, 9000, "def", False, 1, cfg)
     with reference_settings(ov, False):
-        eng = TDEngine(L, B, "def", False, 1, np_seeds=seeds, py_seeds=seeds, autoreset=False)
+        eng = TDEngine(L, B, "def", False, 1, np_seeds=seeds, py_seeds=seeds, autoreset=False, step_kernel=kernel)
     try:
         eng.reset()
         rng = np.random.RandomState(12)

@@ -22,6 +22,11 @@ from gym_TD.engine import TDEngine  # noqa: E402
 
 from test_oracle_golden import _info_view  # noqa: E402
 
+# The three step kernels (td_set_step_kernel): the large-batch kernel of the metric's
+# 65,536 boards, the one-round kernel of the N = 8 share (8,192 boards), the two-wave
+# kernel of configs[1] (4,096 boards).  Every parity test below runs each of them.
+KERNELS = ("large", "small", "small2")
+
 
 @contextlib.contextmanager
 def reference_settings(overrides, multi):
@@ -46,13 +51,16 @@ def _make_env(tr):
     return cls(tr["L"], **kw)
 
 
+@pytest.mark.parametrize("kernel", KERNELS)
 @pytest.mark.parametrize("name", G.traj_names())
-def test_device_replays_golden(name):
+def test_device_replays_golden(name, kernel):
     tr = G.load_traj(name)
     L = tr["L"]
     with reference_settings(tr["overrides"], tr["multi"]):
         env = _make_env(tr)
         try:
+            env._engine.set_step_kernel(kernel)
+            assert env._engine.step_kernel == kernel
             rep = G.replay_oracle(tr)
             _, init, _ = next(rep)
             st = env._engine.board_state(0)
@@ -101,8 +109,9 @@ def _oracle_envs(L, seeds, mode="def", multi=False, difficulty=1):
     return [O.Env(L, G.MODES[mode], difficulty, int(s), int(s), O.Config(), hp, road_attempts=20000) for s in seeds]
 
 
+@pytest.mark.parametrize("kernel", KERNELS)
 @pytest.mark.parametrize("L,B,steps", [(10, 96, 260), (20, 32, 160), (30, 16, 120)])
-def test_batched_vs_oracle(L, B, steps):
+def test_batched_vs_oracle(L, B, steps, kernel):
     """B boards in one launch vs B oracle envs, random + smart defender actions."""
     seeds = [s for s in range(1000, 1000 + 3 * B) if L > 10 or s not in (1045,)]
     orc, ok = [], []
@@ -114,8 +123,9 @@ def test_batched_vs_oracle(L, B, steps):
             pass
         if len(ok) == B:
             break
-    eng = TDEngine(L, B, "def", False, 1, np_seeds=ok, py_seeds=ok, autoreset=False)
+    eng = TDEngine(L, B, "def", False, 1, np_seeds=ok, py_seeds=ok, autoreset=False, step_kernel=kernel)
     try:
+        assert eng.step_kernel == kernel
         obs, failed = eng.reset()
         assert not failed
         rng = np.random.RandomState(L)
@@ -198,24 +208,44 @@ def test_autoreset_matches_explicit_reset():
         eb.close()
 
 
-@pytest.mark.parametrize("L,B,mode,multi", [(10, 4096, "def", False), (10, 65536, "def", False),
-                                            (20, 16384, "2p", True), (30, 16384, "def", False)])
-def test_full_size_properties(L, B, mode, multi):
-    """BASELINE.json configs[1]-[4] sizes per GPU (4,096 and 65,536 x 10x10 TD-def,
-    16,384 x 20x20 TD-2p multi-action, 16,384 x 30x30 TD-def = one GPU's share of
-    configs[4]): invariants over every board, bit-exact spot checks vs the oracle."""
-    seeds = np.arange(B, dtype=np.int64) + 7000
-    eng = TDEngine(L, B, mode, multi, 1, np_seeds=seeds, py_seeds=seeds, autoreset=True)
+# BASELINE.json configs[1]-[4] per GPU: 4,096 and 65,536 x 10x10 TD-def (configs[1], the
+# metric at N = 1), 8,192 (the N = 8 share of configs[3]), 16,384 x 20x20 TD-2p multi-action
+# (configs[2]) and 16,384 x 30x30 TD-def (one GPU's share of configs[4]), on the kernel
+# td_create picks for each (and the 8,192 share also on the large kernel).  10x10 runs past a
+# full episode (1,300 steps: every board reaches the 0.75 enemy upgrade and auto-resets at
+# least once, on the staged-layout rings the refill kernel fills).
+@pytest.mark.parametrize("L,B,mode,multi,steps,kernel", [
+    (10, 4096, "def", False, 1300, "auto"), (10, 8192, "def", False, 1300, "auto"),
+    (10, 8192, "def", False, 1300, "large"), (10, 65536, "def", False, 1300, "auto"),
+    (20, 16384, "2p", True, 300, "auto"), (30, 16384, "def", False, 300, "auto")])
+def test_full_size_properties(L, B, mode, multi, steps, kernel):
+    """Invariants over every board every 50 steps, and 12 boards per batch bit-exact
+    against the C restatement (oracle/td_cpu.c) at every step: reward bits, done, every
+    observation byte (the next episode's first one after an auto-reset, failing layout
+    draws skipped on both sides), the canonical state every 100 steps."""
+    from oracle import td_cpu as C
+    from test_gpu_deep import _reset_skipping, ROAD_ATTEMPTS
+    seeds = np.arange(B, dtype=np.int64) + 7000 + 100000 * (B == 8192)
+    eng = TDEngine(L, B, mode, multi, 1, np_seeds=seeds, py_seeds=seeds, autoreset=True, info=not multi,
+                   step_kernel=kernel)
+    orc = []
     try:
+        if kernel == "auto" and torch.cuda.get_device_properties(0).multi_processor_count == 256 and L == 10:
+            # td_create's rule on a 256-CU MI355X: one round of waves (8 per SIMD) -> small kernel
+            assert eng.step_kernel == {4096: "small2", 8192: "small", 65536: "large"}[B], eng.step_kernel_name
         obs, failed = eng.reset()
         good = np.ones(B, bool)
         good[failed] = False
-        picks = [b for b in np.random.RandomState(1).choice(B, 24, replace=False) if good[b]][:12]
-        orc = _oracle_envs(L, [int(seeds[b]) for b in picks], mode, multi)
+        picks = [int(b) for b in np.random.RandomState(1).choice(B, 24, replace=False) if good[b]][:12]
+        orc = [C.Env(L, mode, 1, int(seeds[b]), int(seeds[b]), multi=multi, road_attempts=ROAD_ATTEMPTS) for b in picks]
+        ob = obs[picks].cpu().numpy()
+        for j, o in enumerate(orc):
+            assert np.array_equal(ob[j], o.obs())
         # boards whose first draw failed (the reference raises) stay unstepped: flagged, zero obs
         assert len(failed) < B // 10
         g = torch.Generator(device="cuda").manual_seed(5)
-        for k in range(40):
+        resets = 0
+        for k in range(steps):
             if multi:
                 d = torch.randint(0, 3, (B, 6, L, L), device="cuda", generator=g, dtype=torch.int64)
             else:
@@ -223,23 +253,37 @@ def test_full_size_properties(L, B, mode, multi):
             a = torch.randint(0, 5, (B, 3, 8), device="cuda", generator=g, dtype=torch.int64) if mode == "2p" else None
             eng.step(def_act=d, atk_act=a)
             ob = eng.obs
-            assert float(ob.min()) >= 0.0 and float(ob.max()) <= 1.0
-            assert torch.equal(ob[:, 0], (ob[:, 1:4].sum(1) > 0).float())
-            if failed:
-                assert float(ob[failed].abs().max()) == 0.0
+            if k % 50 == 0 or k == steps - 1:
+                assert float(ob.min()) >= 0.0
+                assert torch.equal(ob[:, 0], (ob[:, 1:4].sum(1) > 0).float())
+                if failed:
+                    assert float(ob[failed].abs().max()) == 0.0
             dh = d[picks].cpu().numpy()
             ah = a[picks].cpu().numpy() if a is not None else [None] * len(picks)
             obh = ob[picks].cpu().numpy()
             rwh = eng.reward[picks].cpu().numpy()
+            dnh = eng.done[picks].cpu().numpy()
+            st = eng.export_state() if k % 100 == 99 else None
             for j, o in enumerate(orc):
-                wo, wr, wd, _ = o.step(dh[j] if multi else int(dh[j]), ah[j])
-                assert canon.fhex(rwh[j]) == canon.fhex(wr)
-                assert np.array_equal(obh[j], wo)
+                wo, wr, wd = o.step(dh[j] if multi else int(dh[j]), ah[j])
+                assert canon.fhex(rwh[j]) == canon.fhex(wr), (k, picks[j])
+                assert bool(dnh[j]) == wd, (k, picks[j])
+                if wd:
+                    wo = _reset_skipping(o)
+                    resets += 1
+                assert np.array_equal(obh[j], wo), (k, picks[j], np.argwhere(obh[j] != wo)[:5].tolist())
+                if st is not None:
+                    assert canon.state_digest(eng.board_state(picks[j], st)) == canon.digest(o.state_bytes()), \
+                        (k, picks[j])
+        if steps > 1200:
+            assert resets >= len(picks)  # every checked board finished an episode and auto-reset
         fl = eng.flags()
-        assert (fl[good] == 0).all()
+        assert (fl[good] == 0).all(), np.unique(fl[good], return_counts=True)
         assert (fl[~good] == 8).all()  # TD_FLAG_NO_LAYOUT
     finally:
         eng.close()
+        for o in orc:
+            o.close()
 
 
 def test_reference_kat_on_device():
