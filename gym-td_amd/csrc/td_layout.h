@@ -8,6 +8,20 @@
 // :178, IndexError at :189); here every loop is bounded and each failure mode is
 // a status code.
 //
+// Hopeless branch loops.  About 1 % of L = 10 draws reach a branch loop (:177) that no
+// attempt can ever finish: the reference spins there forever, and a bounded loop
+// burns its whole bound (1,000 walks -- 69 % of all generator walks at L = 10).  The
+// loop's field is static (a failed walk is erased), so on its first attempt a
+// breadth-first search from every candidate branch point over the free cells decides
+// whether ANY walk could end on a border cell at Manhattan distance >= 3L/4 from the
+// main road's end within the length bound (a walk moves one cell per appended cell and
+// stops on the first border cell, so the search's distance is a lower bound on every
+// walk's length).  If none can, the draw fails at once with ROAD_ERR_BOUND, before the
+// attempt draws anything (branch_hopeless).  Draws the reference finishes are never
+// affected: a search can only prove a failure every attempt would have had.  The
+// stream position after such a failed draw is the loop's entry (the bounded loop's
+// was 1,000 attempts later); both are restatements of a reference that never returns.
+//
 // Layout record (uint32 words), the unit the device resets a board from:
 //   [0] TD_LAYOUT_MAGIC   [1] num_roads   [2] end cell   [3] max dist
 //   [4..6] start cell of road 0..2 (row*L+col)  [7] status
@@ -134,6 +148,36 @@ struct RoadGen {
     for (int i = 0; i < n; ++i) { s.field[road[i]] = 0; s.rot[road[i]] = 0; }
   }
 
+  // The branch loop's first attempt (see the file comment): 1 when no candidate branch
+  // point picks[klo, khi) can start a walk that ends on a border cell at Manhattan
+  // distance >= 3L/4 from endc with fewer than 2L - (nm - index) cells.  BFS over the
+  // free cells: s.r1 (free in the branch phase) is the queue, s.r2 the distances.
+  TD_HD int branch_hopeless(int klo, int khi, int nm, int endc) {
+    const int NC = L * L, dmin = L * 3 / 4;
+    const int DR[4] = {1, 0, -1, 0}, DC[4] = {0, -1, 0, 1};
+    for (int k = klo; k < khi; ++k) {
+      const int bc = (int)(s.picks[k] & 0xffffu), lim = 2 * L - (nm - (int)(s.picks[k] >> 16));
+      if (lim <= 0) continue;                              // every walk from here is too long
+      if (!inner(bc / L, bc % L)) return 0;                // an empty branch: IndexError (:189), not a hang
+      for (int i = 0; i < NC; ++i) s.r2[i] = 0xffffu;
+      int qh = 0, qt = 0;
+      s.r1[qt++] = (uint16_t)bc;
+      s.r2[bc] = 0;
+      while (qh < qt) {
+        const int u = s.r1[qh++], du = s.r2[u];
+        if (du + 1 >= lim) break;                          // BFS order: every later cell is as far
+        for (int d = 0; d < 4; ++d) {
+          const int r = u / L + DR[d], c = u % L + DC[d], v = r * L + c;
+          if (s.field[v] || s.r2[v] != 0xffffu) continue;  // u is inner: v is on the board
+          s.r2[v] = (uint16_t)(du + 1);
+          if (inner(r, c)) s.r1[qt++] = (uint16_t)v;
+          else if (iabs(r - endc / L) + iabs(c - endc % L) >= dmin) return 0;  // a walk could end here
+        }
+      }
+    }
+    return 1;
+  }
+
   static TD_HD int iabs(int x) { return x < 0 ? -x : x; }
 
   // TDGymBasic.reset's draws (num_roads, :42) + create_road_v2 (TDRoadGen.py:4-199)
@@ -209,6 +253,7 @@ struct RoadGen {
       const int np = (int)st.np, nm = (int)st.nm, endc = (int)st.endc;
       const int klo = np * 2 / 5, khi = np * 4 / 5;
       if (khi <= klo) return fail(st, ROAD_ERR_RANDINT, rec);
+      if (st.att == 1 && branch_hopeless(klo, khi, nm, endc)) return fail(st, ROAD_ERR_BOUND, rec);
       int k = (int)rng.np_randint(klo, khi);
       const int nd = (int)rng.np_randint(0, 4);
       const int bcell = s.picks[k] & 0xffffu;

@@ -1967,6 +1967,52 @@ struct WaveRoadGen {
     return loop >= 100 ? 0 : 1;
   }
 
+  // Bitmap shifts across the lanes' words: cell c -> c + sh (up) / c - sh (down), 0 < sh <= 32.
+  __device__ __forceinline__ uint32_t up(uint32_t x, int sh) const {
+    const uint32_t b = lane > 0 ? (uint32_t)__shfl((int)x, lane - 1) : 0u;
+    return sh == 32 ? b : (x << sh) | (b >> (32 - sh));
+  }
+  __device__ __forceinline__ uint32_t down(uint32_t x, int sh) const {
+    const uint32_t a = lane < 63 ? (uint32_t)__shfl((int)x, lane + 1) : 0u;
+    return sh == 32 ? a : (x >> sh) | (a << (32 - sh));
+  }
+
+  // td_layout.h RoadGen::branch_hopeless on the register bitmaps: a breadth-first search
+  // from each candidate branch point picks[klo, khi) over the free cells, one frontier
+  // bitmap step per walk length; true when no candidate reaches a border cell at
+  // Manhattan distance >= 3L/4 from endc in fewer than 2L - (nm - index) cells.
+  __device__ bool hopeless(int klo, int khi, int nm, int endc) {
+    const int ncells = L * L, dmin = L * 3 / 4;
+    uint32_t valid = 0, first = 0, last = 0, inn = 0, qual = 0;
+    for (int i = 0; i < 32; ++i) {
+      const int c = 32 * lane + i, r = c / L, cc = c - r * L;
+      if (c >= ncells) break;
+      const uint32_t m = 1u << i;
+      valid |= m;
+      if (cc == 0) first |= m;
+      if (cc == L - 1) last |= m;
+      if (inner(r, cc)) inn |= m;
+      else if (iabs(r - endc / L) + iabs(cc - endc % L) >= dmin) qual |= m;
+    }
+    wsync();
+    for (int k = klo; k < khi; ++k) {
+      const uint32_t pk = picks[k];
+      const int bc = (int)(pk & 0xffffu), lim = 2 * L - (nm - (int)(pk >> 16));
+      if (lim <= 0) continue;                      // every walk from here is too long
+      if (!inner(bc / L, bc % L)) return false;    // an empty branch: IndexError (:189), not a hang
+      uint32_t F = lane == (bc >> 5) ? 1u << (bc & 31) : 0u;
+      uint32_t V = F | field;
+      for (int d = 1; d < lim; ++d) {
+        const uint32_t N = (up(F & ~last, 1) | down(F & ~first, 1) | up(F, L) | down(F, L)) & valid & ~V;
+        if (ballot((N & qual) != 0u)) return false;  // a walk could end here
+        V |= N;
+        F = N & inn;
+        if (!ballot(F != 0u)) break;
+      }
+    }
+    return true;
+  }
+
   // clean_up (TDRoadGen.py:121-124): field and turn marks of the road's cells cleared
   __device__ void erase(const uint16_t* road, int cnt) {
     wsync();
@@ -2088,6 +2134,7 @@ struct WaveRoadGen {
       const int np = (int)st.np, nm = (int)st.nm, endc = (int)st.endc;
       const int klo = np * 2 / 5, khi = np * 4 / 5;
       if (khi <= klo) return fail(st, ROAD_ERR_RANDINT);
+      if (st.att == 1 && hopeless(klo, khi, nm, endc)) return fail(st, ROAD_ERR_BOUND);  // RoadGen::branch_hopeless
       int k = np_randint(klo, khi);
       const int nd = np_randint(0, 4);
       wsync();

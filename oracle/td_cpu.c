@@ -210,6 +210,43 @@ static void g_erase(Gen* g, const Road* rd) {
 
 static int iabs(int x) { return x < 0 ? -x : x; }
 
+/* The branch loop's first attempt: 1 when no candidate branch point main[pick_i[k]],
+ * k in [klo, khi), can start a walk ending on a border cell at Manhattan distance
+ * >= 3L/4 from the main road's end within the length bound -- the loop would never
+ * finish (TDRoadGen.py:177; the rule of td_layout.h branch_hopeless, restated).  BFS
+ * over the free cells; a walk stops on its first border cell. */
+static int branch_hopeless(const Gen* g, const Road* mainr, const int* pick_i, int klo, int khi) {
+  const int L = g->L, dmin = L * 3 / 4;
+  const int er = mainr->p[mainr->n - 1][0], ec = mainr->p[mainr->n - 1][1];
+  static __thread int16_t dist[MAXL][MAXL];
+  static __thread int16_t q[MAXL * MAXL][2];
+  for (int k = klo; k < khi; ++k) {
+    const int idx = pick_i[k], lim = 2 * L - (mainr->n - idx);
+    const int br = mainr->p[idx][0], bcc = mainr->p[idx][1];
+    if (lim <= 0) continue;
+    if (!g_inner(g, br, bcc)) return 0;  /* an empty branch raises IndexError (:189) */
+    for (int r = 0; r < L; ++r)
+      for (int c = 0; c < L; ++c) dist[r][c] = -1;
+    int qh = 0, qt = 0;
+    q[qt][0] = (int16_t)br; q[qt][1] = (int16_t)bcc; ++qt;
+    dist[br][bcc] = 0;
+    while (qh < qt) {
+      const int ur = q[qh][0], uc = q[qh][1];
+      ++qh;
+      const int du = dist[ur][uc];
+      if (du + 1 >= lim) break;
+      for (int d = 0; d < 4; ++d) {
+        const int r = ur + STEP[d][0], c = uc + STEP[d][1];
+        if (g->field[r][c] || dist[r][c] >= 0) continue;
+        dist[r][c] = (int16_t)(du + 1);
+        if (g_inner(g, r, c)) { q[qt][0] = (int16_t)r; q[qt][1] = (int16_t)c; ++qt; }
+        else if (iabs(r - er) + iabs(c - ec) >= dmin) return 0;
+      }
+    }
+  }
+  return 1;
+}
+
 /* roads[i] as cell lists; returns 0 or an error (1 randint ValueError, 2 IndexError, 3 bound) */
 static int create_road(Env* e, int num_roads, Road* roads) {
   Gen g;
@@ -259,6 +296,8 @@ static int create_road(Env* e, int num_roads, Road* roads) {
     int k = 0;
     for (att = 0;; ++att) {
       if (att >= e->road_attempts) return 3;
+      if (np * 4 / 5 <= np * 2 / 5) return 1;  /* randint's ValueError (:178) */
+      if (att == 0 && branch_hopeless(&g, mainr, pick_i, np * 2 / 5, np * 4 / 5)) return 3;
       k = np_randint(m, np * 2 / 5, np * 4 / 5, &g.err);
       if (g.err) return 1;
       const int nd = np_randint(m, 0, 4, &g.err);

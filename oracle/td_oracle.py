@@ -83,11 +83,17 @@ class RoadGenError(Exception):
     """The reference raises (IndexError/ValueError) or never terminates."""
 
 
-def create_road(rng, L, num_roads, max_attempts=None):
+def create_road(rng, L, num_roads, max_attempts=None, prove_hopeless=True):
     """Restates create_road_v2 (TDRoadGen.py:4-199) call for call on ``rng``.
 
     ``max_attempts`` bounds each ``while not succ`` loop (the reference's are
     unbounded, TDRoadGen.py:129,142,177); exceeding it raises RoadGenError.
+    ``prove_hopeless``: a branch loop (:174-197) that no attempt can finish -- no
+    candidate branch point has a path over the free cells to a border cell at
+    Manhattan distance >= 3L/4 from the main road's end short enough for the length
+    bound -- raises RoadGenError on its first attempt, before any draw, where the
+    reference spins forever (the build's rule, gym-td_amd/csrc/td_layout.h
+    branch_hopeless; False: burn the attempts, for the test that pins the rule).
     """
     assert 1 <= num_roads <= 3
 
@@ -202,10 +208,43 @@ def create_road(rng, L, num_roads, max_attempts=None):
             i += 1
         else:
             i += 2
+    def hopeless(klo, khi):
+        """No walk from any candidate branch point can be accepted (BFS lower bound)."""
+        end = main[-1]
+        for kk in range(klo, khi):
+            (br, bc), idx = picks[kk]
+            lim = 2 * L - (len(main) - idx)
+            if lim <= 0:
+                continue
+            if not inner((br, bc)):
+                return False  # an empty branch raises IndexError (:189), not a hang
+            dist = {(br, bc): 0}
+            queue = [(br, bc)]
+            for u in queue:
+                du = dist[u]
+                if du + 1 >= lim:
+                    break
+                for dx, dy in step:
+                    v = (u[0] + dx, u[1] + dy)
+                    if field[v] or v in dist:
+                        continue
+                    dist[v] = du + 1
+                    if inner(v):
+                        queue.append(v)
+                    elif abs(v[0] - end[0]) + abs(v[1] - end[1]) >= L * 3 // 4:
+                        return False
+        return True
+
     for _r in range(1, num_roads):  # :174-197
+        first = True
         for _ in bounded():
+            klo, khi = len(picks) * 2 // 5, len(picks) * 4 // 5
+            if first:
+                first = False
+                if prove_hopeless and khi > klo and hopeless(klo, khi):
+                    raise RoadGenError("no branch point can reach an accepted end (the reference loops forever)")
             try:
-                k = rng.randint(low=len(picks) * 2 // 5, high=len(picks) * 4 // 5)
+                k = rng.randint(low=klo, high=khi)
             except ValueError as ex:
                 raise RoadGenError("randint: %s" % ex)
             nd = rng.randint(4)

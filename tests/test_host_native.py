@@ -133,3 +133,86 @@ def test_create_without_gpu_fails_cleanly():
     h = lib.td_create(c, 10, 4, 0, 0, 1, 0)
     assert not h
     assert lib.td_last_error()
+
+
+def _digest_of_roads(roads, L):
+    m, start, end = O.layout_from_roads(roads, L)
+    return canon.layout_digest(m, start, end)
+
+
+def test_hopeless_branch_rule_is_pinned():
+    """The hopeless-branch rule (td_layout.h branch_hopeless) against the bounded loops it
+    replaces, on auto-reset sequences of L = 10 draws: every draw the rule fails at once is
+    one whose branch loop burns the whole 1,000-attempt bound (the reference never
+    returns), and every other draw -- layout, error kind, stream position after it -- is
+    the bounded loops' own.  The native host restatement follows the rule draw for draw."""
+    L, hopeless, draws = 10, 0, 0
+    for seed in range(200):
+        rs = np.random.RandomState(seed)
+        w = np.zeros(625, np.uint32)
+        lib.td_np_seed(_p(w), seed)
+        for _ in range(8):
+            draws += 1
+            old = np.random.RandomState()
+            old.set_state(rs.get_state())
+            nr = rs.randint(1, 4)
+            assert old.randint(1, 4) == nr
+            try:
+                roads, err = O.create_road(rs, L, nr, max_attempts=1000), None
+            except O.RoadGenError as ex:
+                roads, err = None, str(ex)
+            try:
+                roads_old, err_old = O.create_road(old, L, nr, max_attempts=1000, prove_hopeless=False), None
+            except O.RoadGenError as ex:
+                roads_old, err_old = None, str(ex)
+            st, rec = generate_layout(w, L, 1000)
+            if err is not None and "loops forever" in err:
+                hopeless += 1
+                assert err_old == "retry bound exceeded", (seed, err_old)
+                assert st == 3, (seed, st)  # ROAD_ERR_BOUND, at the loop's entry
+            else:
+                assert err == err_old and (roads == roads_old), (seed, err, err_old)
+                assert old.get_state()[2] == rs.get_state()[2] and (old.get_state()[1] == rs.get_state()[1]).all()
+                if err is None:
+                    assert st == 0
+                    m, start, end, nr2 = layout_planes(rec, L)
+                    assert nr2 == nr and canon.layout_digest(m, start, end) == _digest_of_roads(roads, L)
+                else:
+                    assert st != 0
+            # the native stream is where the Python restatement's is
+            st_py = rs.get_state()
+            assert list(w[:624]) == list(st_py[1]) and int(w[624]) == st_py[2], seed
+    assert hopeless >= 3, (hopeless, draws)
+
+
+def test_cpu_oracle_follows_the_hopeless_rule():
+    """The C restatement's auto-reset sequence (failing draws skipped) equals the native
+    host sequence under the same rule, over boards whose sequences hold hopeless draws."""
+    from oracle import td_cpu as C
+    L, checked = 10, 0
+    for seed in range(60):
+        try:
+            env = C.Env(L, "def", 1, seed, seed, road_attempts=1000)
+        except C.RoadGenError:
+            continue
+        w = np.zeros(625, np.uint32)
+        lib.td_np_seed(_p(w), seed)
+        st, rec = generate_layout(w, L, 1000)
+        assert st == 0
+        try:
+            for _ in range(10):
+                m, start, end, _ = layout_planes(rec, L)
+                m2, s2, e2 = env.layout()
+                assert canon.layout_digest(m, start, end) == canon.layout_digest(m2.astype(np.int32), s2, e2), seed
+                while True:  # next layout of both, failing draws skipped
+                    st, rec = generate_layout(w, L, 1000)
+                    try:
+                        env.reset()
+                        assert st == 0, seed
+                        break
+                    except C.RoadGenError:
+                        assert st != 0, seed
+                        checked += st == 3
+        finally:
+            env.close()
+    assert checked >= 1
