@@ -1968,12 +1968,16 @@ struct WaveRoadGen {
   }
 
   // Bitmap shifts across the lanes' words: cell c -> c + sh (up) / c - sh (down), 0 < sh <= 32.
+  // (The shuffles run in every lane: a lane reading a lane that is switched off by a
+  // branch around the shuffle would read garbage.)
   __device__ __forceinline__ uint32_t up(uint32_t x, int sh) const {
-    const uint32_t b = lane > 0 ? (uint32_t)__shfl((int)x, lane - 1) : 0u;
+    const uint32_t t = (uint32_t)__shfl((int)x, lane > 0 ? lane - 1 : 0);
+    const uint32_t b = lane > 0 ? t : 0u;
     return sh == 32 ? b : (x << sh) | (b >> (32 - sh));
   }
   __device__ __forceinline__ uint32_t down(uint32_t x, int sh) const {
-    const uint32_t a = lane < 63 ? (uint32_t)__shfl((int)x, lane + 1) : 0u;
+    const uint32_t t = (uint32_t)__shfl((int)x, lane < 63 ? lane + 1 : 63);
+    const uint32_t a = lane < 63 ? t : 0u;
     return sh == 32 ? a : (x >> sh) | (a << (32 - sh));
   }
 

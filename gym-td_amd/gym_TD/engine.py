@@ -128,6 +128,7 @@ class TDEngine(object):
         if getattr(self, "_h", None):
             _lib.lib.td_destroy(self._h)
             self._h = None
+        P._live.discard(self)  # paramConfig reaches live engines only
 
     def __del__(self):
         try:

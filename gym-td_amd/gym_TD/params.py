@@ -53,7 +53,8 @@ def paramConfig(**kwargs):
     for key, val in kwargs.items():
         setattr(config, key, val)
     for eng in list(_live):
-        eng.set_config(config)
+        if getattr(eng, "_h", None):  # closed engines are gone
+            eng.set_config(config)
 
 
 def getConfig():

@@ -22,6 +22,10 @@ s1)  # the kernel-parametrised parity suite, smoke, default line, N = 2 self-lau
   unset TD_BENCH_DIST_BACKEND TD_BENCH_SAME_DEVICE
   line bench_n2
   ;;
+s2)  # the failures of s1 after the fixes, and the new reset-sequence test
+  run pytest_gpu 700 python -u -m pytest tests/test_gpu_roadgen.py tests/test_gpu_envs.py tests/test_gpu_deep.py -q --timeout 400 --timeout-method thread -p no:cacheprovider
+  rc=$?; grep -E "^(FAILED|E  )" $O/pytest_gpu.log | head -40; tail -3 $O/pytest_gpu.log; [ $rc -le 1 ] || exit $rc
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "session $S rc=0"

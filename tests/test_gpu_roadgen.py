@@ -130,3 +130,37 @@ def test_refill_kernel_layouts_match_host_sequence():
     finally:
         eng.close()
 
+
+
+@pytest.mark.parametrize("L,B,resets", [(10, 512, 10), (20, 128, 4)])
+def test_reset_sequence_matches_host(L, B, resets):
+    """Explicit resets one after another (each draws the board's next layout, failing
+    draws leaving the board as it was): the reset kernel's draws -- including the
+    hopeless branch loops failed at once (td_layout.h branch_hopeless; ~1 % of L = 10
+    draws) -- equal the host restatement's, failure for failure, with the stream left
+    at the same position after every draw."""
+    seeds = list(range(50000, 50000 + B))
+    eng = TDEngine(L, B, "def", False, 1, np_seeds=seeds, py_seeds=seeds, autoreset=False)
+    host = []
+    for s in seeds:
+        w = np.zeros(625, np.uint32)
+        _lib.lib.td_np_seed(_lib.ptr(w, _lib.ctypes.c_uint32), s)
+        host.append(w)
+    try:
+        bound = 0
+        for r in range(resets):
+            _, failed = eng.reset()
+            st = eng.export_state()
+            for b in range(B):
+                hst, rec = generate_layout(host[b], L, ROAD_ATTEMPTS)
+                bound += hst == 3
+                assert (b in failed) == (hst != 0), (r, b, hst)
+                assert eng.get_np_state(b).tolist() == host[b].tolist(), (r, b)
+                if hst == 0:
+                    m, start, end, nr = layout_planes(rec, L)
+                    m2, s2, e2 = eng.map_planes(b, st)
+                    assert canon.layout_digest(m, start, end) == canon.layout_digest(m2, s2, e2), (r, b)
+        if L == 10:
+            assert bound >= 10, bound  # hopeless draws were among them
+    finally:
+        eng.close()
