@@ -26,6 +26,16 @@ s2)  # the failures of s1 after the fixes, and the new reset-sequence test
   run pytest_gpu 700 python -u -m pytest tests/test_gpu_roadgen.py tests/test_gpu_envs.py tests/test_gpu_deep.py -q --timeout 400 --timeout-method thread -p no:cacheprovider
   rc=$?; grep -E "^(FAILED|E  )" $O/pytest_gpu.log | head -40; tail -3 $O/pytest_gpu.log; [ $rc -le 1 ] || exit $rc
   ;;
+s3)  # full suite, then every workload line on this build, refills off as the bound
+  run pytest_gpu 700 python -u -m pytest tests -m gpu -q --timeout 400 --timeout-method thread -p no:cacheprovider
+  rc=$?; grep -E "^(FAILED|E  )" $O/pytest_gpu.log | head -20; tail -1 $O/pytest_gpu.log; [ $rc -le 1 ] || exit $rc
+  for bb in 32768 16384 8192 4096; do
+    run b$bb 200 python bench.py --global-batch $bb --no-cpu-baseline --steps 2000 || exit 1; line b$bb
+    run b${bb}_norefill 200 python bench.py --global-batch $bb --no-cpu-baseline --steps 2000 --refill-interval 0 || exit 1; line b${bb}_norefill
+  done
+  run p2 300 python bench.py --workload 2p-middle-multi --no-cpu-baseline --steps 1000 || exit 1; line p2
+  run large 300 python bench.py --workload def-large --no-cpu-baseline --steps 300 || exit 1; line large
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "session $S rc=0"

@@ -452,7 +452,10 @@ def test_config_epochs_recycled_past_256():
     from gym_TD import _lib
     from gym_TD import params as P
     L, B = 10, 16
-    base = dict(tower_distance=0, defender_init_cost=400, max_cost=400, defender_cost_rate=2)
+    # phase 1: a builder defender that stays under the 32-tower cap ((150 + 0.5 * 300) / 10 = 30 towers
+    # at most); phase 2: explicit builds, one tower per board every 16 steps
+    rich = dict(tower_distance=0, defender_init_cost=400, max_cost=400, defender_cost_rate=2)
+    base = dict(rich, defender_init_cost=150, defender_cost_rate=0.5)
 
     def cfg_at(k, into):
         for key, v in base.items():
@@ -491,8 +494,10 @@ def test_config_epochs_recycled_past_256():
                 assert canon.state_digest(mine) == canon.state_digest(want), (k, b, mine, want)
                 assert np.array_equal(ob[b], wo), (k, b, np.argwhere(ob[b] != wo)[:5].tolist())
         assert len(set(seen)) == 256 and len(seen) == 300  # blocks were recycled
+        assert (eng.flags() == 0).all()  # no board reached the tower / enemy caps
     finally:
         eng.close()
+    base = rich
     # all 256 blocks held by live towers: one tower per config epoch, board k % 16 building at step k
     eng = TDEngine(L, B, "def", False, 1, np_seeds=seeds, py_seeds=seeds, autoreset=False, cfg=dcfg)
     try:
