@@ -23,6 +23,8 @@
 #include "td_kernels.h"
 #include "td_layout.h"
 #include "td_rng.h"
+#include "td_wave.h"
+#include "td_wavegen.h"
 
 #include <type_traits>
 #include <utility>
@@ -41,92 +43,6 @@ namespace td {
 constexpr int MAX_KERNEL_L = 32;  // generic-L kernels: L <= 32
 
 enum : int { FC_OK = 0, FC_COST = 1, FC_POS = 2, FC_LVMAX = 3, FC_TARGET = 4, FC_CAP = 6 };  // utils/fail_code.py
-
-// ---------------------------------------------------------------------------
-// exact-rounding helpers (Python float / numpy float32 semantics)
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ double dadd(double a, double b) { return __dadd_rn(a, b); }
-__device__ __forceinline__ double dsub(double a, double b) { return __dsub_rn(a, b); }
-__device__ __forceinline__ double dmul(double a, double b) { return __dmul_rn(a, b); }
-__device__ __forceinline__ double ddiv(double a, double b) { return __ddiv_rn(a, b); }
-__device__ __forceinline__ double pymin(double a, double b) { return b < a ? b : a; }  // min(a, b)
-__device__ __forceinline__ float f32(double x) { return __double2float_rn(x); }
-
-__device__ __forceinline__ int ctz64(uint64_t m) { return __builtin_ctzll(m); }
-__device__ __forceinline__ int popc64(uint64_t m) { return __popcll(m); }
-__device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
-// Lane l's value (l wave-uniform): a scalar broadcast, no LDS traffic.
-__device__ __forceinline__ uint32_t rdl(uint32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }
-__device__ __forceinline__ float rdl(float v, int l) { return __int_as_float((int)rdl((uint32_t)__float_as_int(v), l)); }
-__device__ __forceinline__ double rdl(double v, int l) {
-  return __hiloint2double((int)rdl((uint32_t)__double2hiint(v), l), (int)rdl((uint32_t)__double2loint(v), l));
-}
-
-// Agent-scope relaxed accesses through the global address space (global_load /
-// global_store ... sc1, never flat): the words two concurrently running grids
-// hand over (layout tags, ring counters).
-typedef __attribute__((address_space(1))) uint32_t gu32;
-__device__ __forceinline__ uint32_t ld_relaxed(const uint32_t* p) {
-  return __hip_atomic_load((gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_relaxed(uint32_t* p, uint32_t v) {
-  __hip_atomic_store((gu32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// A board's layout stream (np_mt) and its ring tail are written only by the refill
-// wave holding the board's claim word (several refills may be in flight on side
-// streams).  Take it with an agent-scope CAS + acquire; give it back after the
-// wave's stores have drained.  Everything the claim protects is stored write-through
-// (sc1, st_relaxed), so no release fence is needed (MI355X_MICROARCH.md, publish
-// recipe R1): a release fence writes back the XCD's whole L2, full of the step
-// kernel's dirty observation lines, and ~490 of them per refill launch cost the
-// 20x20 multi-action step 3.6 % (335.5 -> 323.7 us per step without them).
-__device__ __forceinline__ bool claim_board(uint32_t* claim, int lane) {
-  uint32_t got = 0;
-  if (lane == 0) got = atomicCAS(claim, 0u, 1u) == 0u ? 1u : 0u;
-  got = __builtin_amdgcn_readfirstlane(got);
-  if (got) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  return got != 0;
-}
-__device__ __forceinline__ void release_board(uint32_t* claim, int lane) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (lane == 0) st_relaxed(claim, 0u);
-}
-
-// Per-board state and output stores.  TD_SST selects the cache policy (A/B builds):
-// 0 plain, 1 non-temporal, 2 write-through (sc1).  Plain is the product: these arrays
-// hold a few bytes per board, so a line is shared by boards on several XCDs and the
-// XCD L2s merge the plain stores; 65,536 boards at L = 10 measured 224 us plain,
-// 227 us sc1 and 287 us non-temporal (partial-line writes to HBM).
-#ifndef TD_SST
-#define TD_SST 0
-#endif
-template <class T>
-__device__ __forceinline__ void sst(T* p, T v) {
-  if constexpr (TD_SST == 1) {
-    __builtin_nontemporal_store(v, p);
-  } else if constexpr (TD_SST == 2) {
-    using W = std::conditional_t<sizeof(T) == 8, uint64_t,
-              std::conditional_t<sizeof(T) == 4, uint32_t, std::conditional_t<sizeof(T) == 2, uint16_t, uint8_t>>>;
-    __hip_atomic_store(reinterpret_cast<W*>(p), __builtin_bit_cast(W, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  } else {
-    *p = v;
-  }
-}
-
-// The step of one board runs in one wave: its LDS hand-offs between lanes need the
-// wave's LDS operations drained and the compiler kept from moving memory accesses
-// across, not a workgroup barrier -- so the small-batch kernel can give a board a
-// second wave that waits at one real barrier for the observation (td_step_kernel_small2).
-__device__ __forceinline__ void wsync() {
-#ifdef TD_WSYNC_BARRIER  // A/B builds: a workgroup barrier (one-wave workgroups only)
-  __syncthreads();
-#else
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_wave_barrier();
-#endif
-}
 
 // ---------------------------------------------------------------------------
 // per-board LDS image
@@ -1499,6 +1415,10 @@ __device__ __forceinline__ void attacker_actions(Smem<NC>& S, U& u, const Ctx& x
 // the observation lines are stored write-through (write_obs_lines).  (Storing the
 // layout and tower planes at the start of the step, before the step logic, was
 // measured slower at 4,096 and 8,192 boards: 36.3 / 53.1 vs 25.7 / 38.3 us.)
+// A board whose ring of staged layouts is empty at its episode end (td_step.hip below).
+template <int NC, bool SMALL>
+__device__ __forceinline__ bool take_dry_ring(const StepArgs& a, int b, uint32_t head, int lane);
+
 // Observation windows written by the stepping wave of a two-wave board (the first half).
 template <int LT>
 __host__ __device__ constexpr int obs_half() { return ((NCH * LT * LT / 4 + 7 + 63) / 64 + 1) / 2; }
@@ -1618,26 +1538,14 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
     const uint32_t* rec = a.nxt + ((size_t)b * NSLOT + lay_head % NSLOT) * a.slot_words;
     const uint32_t want = slot_tag(lay_head);
     bool ready = ld_relaxed(rec) == want;
-#ifndef TD_NO_SPIN
-    if (!ready && ld_relaxed(a.lay_claim + b) != 0u) {
-      // the ring ran dry while a refill wave holds the board: it is drawing exactly
-      // this layout (typically one the reference never finishes, 2-5 ms of one lane
-      // at the 1,000-attempt bound); wait for its tag, bounded
-      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      while (!ready && ld_relaxed(a.lay_claim + b) != 0u &&
-             __builtin_amdgcn_s_memrealtime() - t0 < kTakeSpinTicks) {
-        __builtin_amdgcn_s_sleep(64);
-        ready = ld_relaxed(rec) == want;
-      }
-      ready = ready || ld_relaxed(rec) == want;
-    }
-#endif
+    // a dry ring: wait for the refill drawing this layout, or draw it now
+    if (!ready) ready = take_dry_ring<NC, SMALL>(a, b, lay_head, x.lane);
     if (ready) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       reset_board(S, u, x, rec);
       was_reset = true;
     } else {
-      u.flags |= FLAG_NO_LAYOUT;  // no layout staged or being drawn: the board keeps stepping its finished episode
+      u.flags |= FLAG_NO_LAYOUT;  // 65 failing draws in a row (the reference raises): the board keeps its finished episode
     }
   }
   STAMP(5);
@@ -1723,8 +1631,15 @@ __device__ __forceinline__ void step_kernel_body(const StepArgs& a) {
 
 // Large batches (several rounds of waves, HBM-write bound): 6 waves per SIMD at
 // L = 10 (106 SGPRs), no register pressure beyond the step's own.
+template <int LT>
+constexpr int large_waves() { return LT == 10 ? 7 : LT == 20 ? 5 : 3; }  // LDS-bound residency per SIMD
+#ifdef TD_DRY_DRAW
+#define TD_LARGE_ATTR __attribute__((amdgpu_waves_per_eu(large_waves<LT>())))
+#else
+#define TD_LARGE_ATTR
+#endif
 template <int LT, int MODE, bool SCAN>
-__global__ __launch_bounds__(64) void td_step_kernel(StepArgs a) {
+__global__ __launch_bounds__(64) TD_LARGE_ATTR void td_step_kernel(StepArgs a) {
   step_kernel_body<LT, MODE, SCAN, false>(a);
 }
 
@@ -1733,8 +1648,18 @@ __global__ __launch_bounds__(64) void td_step_kernel(StepArgs a) {
 // limit for 8 resident waves (MI355X_MICROARCH.md, residency), so 8,192 boards -- 8
 // GPUs' share of BASELINE's 65,536 -- run as ONE round instead of 6,144 + 2,048.  At
 // 65,536 boards the same build is 7 % slower (SGPR spill code), hence two kernels.
-#ifndef TD_SMALL_ATTR
+// (TD_DRY_DRAW A/B builds: per-L residency, which bounds the registers of the dry-ring
+// draw the kernels then call -- see take_dry_ring.)
+template <int LT>
+constexpr int small_waves() { return LT == 10 ? 8 : LT == 20 ? 5 : 3; }
+template <int LT>
+constexpr int small2_waves() { return LT == 30 ? 6 : 8; }
+#ifdef TD_DRY_DRAW
+#define TD_SMALL_ATTR __attribute__((amdgpu_waves_per_eu(small_waves<LT>(), small_waves<LT>())))
+#define TD_SMALL2_ATTR __attribute__((amdgpu_waves_per_eu(small2_waves<LT>(), small2_waves<LT>())))
+#else
 #define TD_SMALL_ATTR __attribute__((amdgpu_waves_per_eu(8, 8)))
+#define TD_SMALL2_ATTR __attribute__((amdgpu_waves_per_eu(8, 8)))
 #endif
 template <int LT, int MODE, bool SCAN>
 __global__ __launch_bounds__(64) TD_SMALL_ATTR void td_step_kernel_small(StepArgs a) {
@@ -1746,7 +1671,7 @@ __global__ __launch_bounds__(64) TD_SMALL_ATTR void td_step_kernel_small(StepArg
 // of the observation windows beside it, which shortens a board's critical path where the
 // batch leaves issue slots free (4,096 boards: 8,192 waves, 8 per SIMD).
 template <int LT, int MODE, bool SCAN>
-__global__ __launch_bounds__(128) TD_SMALL_ATTR void td_step_kernel_small2(StepArgs a) {
+__global__ __launch_bounds__(128) TD_SMALL2_ATTR void td_step_kernel_small2(StepArgs a) {
   constexpr int NC = LT * LT;
   __shared__ Smem<NC> S;
   const int b = blockIdx.x;
@@ -1816,377 +1741,15 @@ static hipError_t launch_opponent2(const StepArgs& a, int side, int level, hipSt
 hipError_t launch_opponent(const StepArgs& a, int side, int level, hipStream_t s) {
   switch (a.L) {
     case 10: return launch_opponent2<10>(a, side, level, s);
+#ifndef TD_L10_ONLY  // diagnostic register-usage compiles (scripts/kernel_resources.sh)
     case 20: return launch_opponent2<20>(a, side, level, s);
     case 30: return launch_opponent2<30>(a, side, level, s);
     default: return launch_opponent2<0>(a, side, level, s);
+#else
+    default: return hipErrorInvalidValue;
+#endif
   }
 }
-
-// ---------------------------------------------------------------------------
-// episode layouts on the device
-// ---------------------------------------------------------------------------
-// LDS image of one layout draw: the board's numpy stream, the output record,
-// create_road_v2's scratch and the draw's resume state (WaveRoadGen runs on it).
-template <int NC>
-struct LayoutSmem {
-  uint32_t mt[OPP_WORDS];
-  uint32_t rec[LAYOUT_HDR + NC];
-  uint8_t scratch[14 * NC + 64];
-  RoadResume res;
-};
-
-// create_road_v2 (TDRoadGen.py:4-199) and TDGymBasic.reset's num_roads draw (:42) run by
-// a whole wave: the device form of td_layout.h RoadGen::draw, draw for draw the same
-// (both are pinned against the reference's road table).  RoadGen on one lane waited on
-// LDS for every stream draw (three dependent words of the lazy twist) and for every
-// move (the field byte); here the stream is a window of 64 tempered outputs in a
-// register, one per lane, refilled 64 at a time with one LDS round trip, and the field
-// / turn maps are bitmaps in registers (lane j holds cells [32j, 32j + 32)), read with
-// v_readlane.  Control flow is wave-uniform.  The road lists stay in LDS (the resumable
-// state); the main road, its branch points and the stamping of a road onto the record
-// run one cell per lane (an accepted road is shorter than 2L <= 64 cells).
-template <int NC>
-struct WaveRoadGen {
-  static constexpr int NW = (NC + 31) / 32;  // bitmap words (at most)
-  uint32_t* mt;   // LDS stream words (LazyMt format: [624] position, [625] lazy-twist boundary)
-  uint32_t* rec;  // LDS record
-  uint32_t* picks;
-  uint16_t *r1, *r2, *rb, *mainr;
-  uint32_t *fieldw, *rotw;  // the bitmaps' resumable copies in the scratch
-  int L, lane;
-  uint32_t pos, tw, base, n, win;
-  uint32_t field, rot;
-
-  // scratch carve for L*L = nc cells: picks u32[nc], r1 / r2 / rb / mainr u16[nc], field / rot
-  // u32[(nc + 31) / 32] -- 12 nc + 8 (nc + 31) / 32 <= road_scratch_bytes(L) bytes
-  __device__ void carve(uint8_t* sc, int nc) {
-    picks = reinterpret_cast<uint32_t*>(sc);
-    r1 = reinterpret_cast<uint16_t*>(sc + 4 * nc);
-    r2 = r1 + nc; rb = r2 + nc; mainr = rb + nc;
-    fieldw = reinterpret_cast<uint32_t*>(sc + 12 * nc);
-    rotw = fieldw + (nc + 31) / 32;
-  }
-
-  // ---- the numpy-legacy stream (LazyMt semantics, 64 words per refill) ----
-  __device__ void refill() {
-    if (pos >= (uint32_t)MT_N) { pos = 0; tw = 0; }
-    base = pos;
-    n = (uint32_t)MT_N - pos < 64u ? (uint32_t)MT_N - pos : 64u;
-    const uint32_t q = base + (uint32_t)lane;
-    const bool mine = (uint32_t)lane < n, lazy = mine && q >= tw;
-    uint32_t y = 0;
-    if (mine) {
-      y = mt[q];
-      if (lazy) {  // new[q] from old[q], old[q + 1] and old[q + 397] / new[q - 227] (< base: done)
-        const uint32_t nb = mt[q == MT_N - 1 ? 0u : q + 1u];
-        const uint32_t far = mt[q < (uint32_t)(MT_N - MT_M) ? q + MT_M : q - (MT_N - MT_M)];
-        const uint32_t yy = (y & 0x80000000u) | (nb & 0x7fffffffu);
-        y = far ^ (yy >> 1) ^ ((yy & 1u) ? 0x9908b0dfu : 0u);
-      }
-    }
-    wsync();  // every lane's old words are read before any new word is stored
-    if (lazy) mt[q] = y;
-    if (base + n > tw) tw = base + n;
-    win = mt_temper(y);
-  }
-  __device__ __forceinline__ uint32_t next() {
-    if (pos - base >= n) refill();
-    const uint32_t r = rdl(win, (int)(pos - base));
-    ++pos;
-    return r;
-  }
-  __device__ int np_randint(int lo, int hi) {  // numpy legacy masked rejection (hi exclusive)
-    if (hi <= lo) return lo;
-    const uint32_t rng = (uint32_t)(hi - lo - 1);
-    if (rng == 0) return lo;
-    uint32_t mask = rng;
-    mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4; mask |= mask >> 8; mask |= mask >> 16;
-    uint32_t v = next() & mask;
-    while (v > rng) v = next() & mask;
-    return lo + (int)v;
-  }
-
-  // ---- field / turn bitmaps ----
-  __device__ __forceinline__ bool bit(uint32_t m, int c) const { return (rdl(m, c >> 5) >> (c & 31)) & 1u; }
-  __device__ __forceinline__ uint32_t with(uint32_t m, int c) const {
-    return m | (lane == (c >> 5) ? 1u << (c & 31) : 0u);
-  }
-  __device__ __forceinline__ uint32_t without(uint32_t m, int c) const {
-    return m & ~(lane == (c >> 5) ? 1u << (c & 31) : 0u);
-  }
-  __device__ __forceinline__ bool inner(int r, int c) const { return r > 0 && r < L - 1 && c > 0 && c < L - 1; }
-
-  // generate_road (TDRoadGen.py:31-119), as RoadGen::walk; *last = the last cell appended
-  __device__ int walk(int r0, int c0, int d, uint16_t* out, int* len, int* last) {
-    int pr = r0, pc = c0, cnt = 0, pending = 0, loop = 0;
-    while (inner(pr, pc) && loop < 100) {
-      ++loop;
-      const int shape = np_randint(0, 2);
-      const int seg = np_randint(L * 3 / 20, L / 4);
-      bool cross = false;
-      auto run = [&](int k_max, int dd, bool reset_cross) {
-        const int dr = dd == 0 ? 1 : dd == 2 ? -1 : 0, dc = dd == 1 ? -1 : dd == 3 ? 1 : 0;  // :15
-        for (int k = 0; k < k_max; ++k) {
-          pr += dr; pc += dc;
-          const int cell = pr * L + pc;
-          if (bit(field, cell)) { pr -= dr; pc -= dc; cross = true; return; }
-          if (reset_cross) cross = false;
-          if (lane == 0) out[cnt] = (uint16_t)cell;
-          ++cnt;
-          field = with(field, cell);
-          if (!inner(pr, pc)) return;
-        }
-      };
-      if (shape <= 0) {
-        run(seg * 2, d, false);
-      } else {
-        run(seg, d, false);
-        if (!inner(pr, pc)) break;
-        int rd;
-        if (pending != 0) { rd = pending; pending = 0; }
-        else { rd = np_randint(0, 2) * 2 - 1; pending = -rd; }
-        rot = with(rot, pr * L + pc);
-        d = (d + 4 + rd) % 4;
-        run(seg, d, true);
-      }
-      if (cross) {  // the free neighbours in direction order, one picked at random
-        const uint32_t fm = (bit(field, (pr + 1) * L + pc) ? 0u : 1u) | (bit(field, pr * L + pc - 1) ? 0u : 2u) |
-                            (bit(field, (pr - 1) * L + pc) ? 0u : 4u) | (bit(field, pr * L + pc + 1) ? 0u : 8u);
-        const int nf = __popc(fm);
-        if (nf == 0) { *len = cnt; *last = pr * L + pc; return 0; }
-        int pick = np_randint(0, nf);
-        uint32_t m = fm;
-        while (pick-- > 0) m &= m - 1;
-        d = __builtin_ctz(m);
-        pending = 0;
-        rot = with(rot, pr * L + pc);
-      }
-    }
-    *len = cnt;
-    *last = pr * L + pc;
-    return loop >= 100 ? 0 : 1;
-  }
-
-  // Bitmap shifts across the lanes' words: cell c -> c + sh (up) / c - sh (down), 0 < sh <= 32.
-  // (The shuffles run in every lane: a lane reading a lane that is switched off by a
-  // branch around the shuffle would read garbage.)
-  __device__ __forceinline__ uint32_t up(uint32_t x, int sh) const {
-    const uint32_t t = (uint32_t)__shfl((int)x, lane > 0 ? lane - 1 : 0);
-    const uint32_t b = lane > 0 ? t : 0u;
-    return sh == 32 ? b : (x << sh) | (b >> (32 - sh));
-  }
-  __device__ __forceinline__ uint32_t down(uint32_t x, int sh) const {
-    const uint32_t t = (uint32_t)__shfl((int)x, lane < 63 ? lane + 1 : 63);
-    const uint32_t a = lane < 63 ? t : 0u;
-    return sh == 32 ? a : (x >> sh) | (a << (32 - sh));
-  }
-
-  // td_layout.h RoadGen::branch_hopeless on the register bitmaps: a breadth-first search
-  // from each candidate branch point picks[klo, khi) over the free cells, one frontier
-  // bitmap step per walk length; true when no candidate reaches a border cell at
-  // Manhattan distance >= 3L/4 from endc in fewer than 2L - (nm - index) cells.
-  __device__ bool hopeless(int klo, int khi, int nm, int endc) {
-    const int ncells = L * L, dmin = L * 3 / 4;
-    uint32_t valid = 0, first = 0, last = 0, inn = 0, qual = 0;
-    for (int i = 0; i < 32; ++i) {
-      const int c = 32 * lane + i, r = c / L, cc = c - r * L;
-      if (c >= ncells) break;
-      const uint32_t m = 1u << i;
-      valid |= m;
-      if (cc == 0) first |= m;
-      if (cc == L - 1) last |= m;
-      if (inner(r, cc)) inn |= m;
-      else if (iabs(r - endc / L) + iabs(cc - endc % L) >= dmin) qual |= m;
-    }
-    wsync();
-    for (int k = klo; k < khi; ++k) {
-      const uint32_t pk = picks[k];
-      const int bc = (int)(pk & 0xffffu), lim = 2 * L - (nm - (int)(pk >> 16));
-      if (lim <= 0) continue;                      // every walk from here is too long
-      if (!inner(bc / L, bc % L)) return false;    // an empty branch: IndexError (:189), not a hang
-      uint32_t F = lane == (bc >> 5) ? 1u << (bc & 31) : 0u;
-      uint32_t V = F | field;
-      for (int d = 1; d < lim; ++d) {
-        const uint32_t N = (up(F & ~last, 1) | down(F & ~first, 1) | up(F, L) | down(F, L)) & valid & ~V;
-        if (ballot((N & qual) != 0u)) return false;  // a walk could end here
-        V |= N;
-        F = N & inn;
-        if (!ballot(F != 0u)) break;
-      }
-    }
-    return true;
-  }
-
-  // clean_up (TDRoadGen.py:121-124): field and turn marks of the road's cells cleared
-  __device__ void erase(const uint16_t* road, int cnt) {
-    wsync();
-    for (int i0 = 0; i0 < cnt; i0 += 64) {
-      const uint32_t cv = i0 + lane < cnt ? road[i0 + lane] : 0u;
-      const int m = cnt - i0 < 64 ? cnt - i0 : 64;
-      for (int i = 0; i < m; ++i) {
-        const int c = (int)rdl(cv, i);
-        field = without(field, c);
-        rot = without(rot, c);
-      }
-    }
-  }
-
-  // One road onto the record (TDBoard.py:38-59): lane k < tot holds cell k (`cv`).
-  __device__ void stamp(uint32_t cv, int tot, int ri, uint32_t* maxdist) {
-    uint32_t* cw = rec + LAYOUT_HDR;
-    const int p = (int)cv;
-    const int pn = __shfl((int)cv, lane + 1 < 64 ? lane + 1 : 63);
-    wsync();
-    if (lane < tot) {
-      uint32_t w = cw[p] | 1u | (1u << (1 + ri));
-      w = (w & 0x00ffffffu) | (1u << 24);
-      w = (w & ~(0xffu << 16)) | ((uint32_t)(tot - 1 - lane) << 16);
-      if (lane < tot - 1) {
-        const int dr = pn / L - p / L, dc = pn % L - p % L;
-        const uint32_t dir = dr == 0 ? (dc == 1 ? 0u : 1u) : (dr == 1 ? 2u : 3u);
-        w = (w & ~(3u << 8)) | (dir << 8);
-      }
-      cw[p] = w;
-    }
-    if ((uint32_t)(tot - 1) > *maxdist) *maxdist = (uint32_t)(tot - 1);
-    wsync();
-  }
-
-  __device__ int fail(RoadResume& st, int status) {
-    wsync();
-    if (lane == 0) { rec[0] = 0; rec[1] = st.nr; rec[7] = (uint32_t)status; }
-    st.phase = RP_NEW;
-    return status;
-  }
-
-  static __device__ __forceinline__ int iabs(int x) { return x < 0 ? -x : x; }
-
-  // RoadGen::draw: the same state machine over the same RoadResume; st lives in
-  // registers (wave-uniform), the caller moves it from / to LDS.  pad holds road 1's
-  // last cell.
-  __device__ int draw(RoadResume& st, int budget, int max_attempts) {
-    if (st.phase == RP_NEW) {
-      st.nr = (uint32_t)np_randint(1, 4);  // TDGymBasic.reset :42
-      const int nr = (int)st.nr;
-      if (L < 4 || L > MAX_L || nr < 1 || nr > 3) return fail(st, ROAD_ERR_ARGS);
-      if (L / 4 <= L * 3 / 20) return fail(st, ROAD_ERR_RANDINT);  // segment randint raises (:41)
-      field = 0u; rot = 0u;
-      const int lo = L / 3, hi = (L * 2 + 2) / 3;
-      st.cr = (uint32_t)np_randint(lo, hi);
-      st.cc = (uint32_t)np_randint(lo, hi);
-      field = with(field, (int)(st.cr * L + st.cc));
-      st.d0 = (uint32_t)np_randint(0, 4);
-      st.phase = RP_ROAD1; st.att = 0;
-    }
-    const int cr = (int)st.cr, cc = (int)st.cc, d0 = (int)st.d0;
-    while (st.phase == RP_ROAD1) {  // center -> end, :128-137
-      if ((int)st.att >= max_attempts) return fail(st, ROAD_ERR_BOUND);
-      if (budget-- <= 0) return ROAD_PENDING;
-      ++st.att;
-      int n1 = 0, e1 = 0;
-      const int ok = walk(cr, cc, d0, r1, &n1, &e1);
-      if (!ok || n1 >= L) { erase(r1, n1); continue; }
-      st.n1 = (uint32_t)n1; st.pad = (uint32_t)e1; st.phase = RP_ROAD2; st.att = 0;
-    }
-    while (st.phase == RP_ROAD2) {  // center -> start, :141-155
-      if ((int)st.att >= max_attempts) return fail(st, ROAD_ERR_BOUND);
-      if (budget-- <= 0) return ROAD_PENDING;
-      ++st.att;
-      const int n1 = (int)st.n1;
-      int n2 = 0, e2 = 0;
-      const int ok = walk(cr, cc, (d0 + 2) % 4, r2, &n2, &e2);
-      if (!ok || n1 + n2 + 1 >= L * 2) { erase(r2, n2); continue; }
-      const int e1 = (int)st.pad;
-      if (iabs(e2 / L - e1 / L) + iabs(e2 % L - e1 % L) < L * 3 / 4) { erase(r2, n2); continue; }
-      // main = reversed(road2) + [center] + road1 (:157-158), one cell per lane (nm < 2L)
-      const int nm = n1 + n2 + 1;
-      wsync();
-      uint32_t mv = 0;
-      if (lane < n2) mv = r2[n2 - 1 - lane];
-      else if (lane == n2) mv = (uint32_t)(cr * L + cc);
-      else if (lane < nm) mv = r1[lane - n2 - 1];
-      if (lane < nm) mainr[lane] = (uint16_t)mv;
-      // branch points (:162-170): cells i with no turn at i and i + 1; a turn at i skips i + 1
-      int np = 0;
-      uint32_t pk = 0;
-      for (int i = 0; i < nm;) {
-        const int ci = (int)rdl(mv, i);
-        if (!bit(rot, ci)) {
-          if (i < nm - 1 && !bit(rot, (int)rdl(mv, i + 1))) {
-            if (lane == np) pk = ((uint32_t)i << 16) | (uint32_t)ci;
-            ++np;
-          }
-          i += 1;
-        } else {
-          i += 2;
-        }
-      }
-      if (lane < np) picks[lane] = pk;
-      // map planes from the main road first (roads[0])
-      for (int i = lane; i < L * L; i += 64) rec[LAYOUT_HDR + i] = 0u;
-      uint32_t maxdist = 0;
-      stamp(mv, nm, 0, &maxdist);
-      st.nm = (uint32_t)nm; st.np = (uint32_t)np; st.maxdist = maxdist;
-      st.start[0] = rdl(mv, 0); st.start[1] = st.start[2] = 0;
-      st.endc = rdl(mv, nm - 1);
-      st.phase = RP_BRANCH; st.ri = 1; st.att = 0;
-    }
-    while (st.phase == RP_BRANCH && (int)st.ri < (int)st.nr) {  // :174-197
-      if ((int)st.att >= max_attempts) return fail(st, ROAD_ERR_BOUND);
-      if (budget-- <= 0) return ROAD_PENDING;
-      ++st.att;
-      const int np = (int)st.np, nm = (int)st.nm, endc = (int)st.endc;
-      const int klo = np * 2 / 5, khi = np * 4 / 5;
-      if (khi <= klo) return fail(st, ROAD_ERR_RANDINT);
-      if (st.att == 1 && hopeless(klo, khi, nm, endc)) return fail(st, ROAD_ERR_BOUND);  // RoadGen::branch_hopeless
-      int k = np_randint(klo, khi);
-      const int nd = np_randint(0, 4);
-      wsync();
-      const uint32_t pkv = picks[k];
-      const int bcell = (int)(pkv & 0xffffu);
-      k = (int)(pkv >> 16);
-      int nb = 0, eb = 0;
-      const int ok = walk(bcell / L, bcell % L, nd, rb, &nb, &eb);
-      if (!ok) { erase(rb, nb); continue; }
-      if (nb + nm - k >= L * 2) { erase(rb, nb); continue; }
-      if (nb == 0) return fail(st, ROAD_ERR_EMPTY);
-      if (iabs(eb / L - endc / L) + iabs(eb % L - endc % L) < L * 3 / 4) { erase(rb, nb); continue; }
-      // road = reversed(branch) + main[k:], one cell per lane (< 2L)
-      wsync();
-      const int tot = nb + nm - k;
-      uint32_t cv = 0;
-      if (lane < nb) cv = rb[nb - 1 - lane];
-      else if (lane < tot) cv = mainr[k + lane - nb];
-      wsync();
-      if (lane < nb) rb[lane] = (uint16_t)cv;  // kept reversed, as RoadGen leaves it
-      uint32_t maxdist = st.maxdist;
-      stamp(cv, tot, (int)st.ri, &maxdist);
-      st.maxdist = maxdist;
-      if (st.ri == 1) st.start[1] = rdl(cv, 0);  // (no dynamic index: keeps st in registers)
-      else st.start[2] = rdl(cv, 0);
-      ++st.ri; st.att = 0;
-    }
-    const int nr = (int)st.nr;
-    uint32_t* cw = rec + LAYOUT_HDR;
-    wsync();
-    if (lane == 0) {
-      cw[st.start[0]] |= 1u << 5;
-      if (nr > 1) cw[st.start[1]] |= 1u << 6;
-      if (nr > 2) cw[st.start[2]] |= 1u << 7;
-      cw[st.endc] |= 1u << 4;
-      rec[0] = TD_LAYOUT_MAGIC;
-      rec[1] = (uint32_t)nr;
-      rec[2] = st.endc;
-      rec[3] = st.maxdist;
-      rec[4] = st.start[0];
-      rec[5] = nr > 1 ? st.start[1] : 0u;
-      rec[6] = nr > 2 ? st.start[2] : 0u;
-      rec[7] = ROAD_OK;
-    }
-    st.phase = RP_NEW;
-    return ROAD_OK;
-  }
-};
 
 // Layout draws are resumable (RoadGen::draw): a refill gives each board a budget of
 // walks per launch, and a draw that runs out (in practice one the reference never
@@ -2244,11 +1807,7 @@ __device__ int wave_layout(LayoutSmem<NC>& G, const StepArgs& a, int b, int retr
     } else {
       g.field = g.rot = 0u;
     }
-#pragma nounroll
-    for (int t = 0; t <= retries; ++t) {
-      st = g.draw(res, budget, kRoadAttempts);
-      if (st == ROAD_OK || st == ROAD_PENDING) break;
-    }
+    st = g.draw(res, budget, kRoadAttempts, retries);
     __syncthreads();
     if (lane < nw) { g.fieldw[lane] = g.field; g.rotw[lane] = g.rot; }
     if (lane == 0) { G.mt[MT_N] = g.pos; G.mt[MT_N + 1] = g.tw; G.res = res; }
@@ -2269,6 +1828,90 @@ __device__ int wave_layout(LayoutSmem<NC>& G, const StepArgs& a, int b, int retr
     if (lane == 0) st_relaxed(slot, slot_tag(n));
   }
   return st;
+}
+
+// TDGymBasic.reset's draws (:42-51) for board b as layout number n of its stream, run by
+// the step wave that found the board's ring empty at its episode end (TD_DRY_DRAW A/B
+// builds, see take_dry_ring): the same draws as
+// wave_layout (a pending draw continues; failing draws skipped up to kLayoutRetries
+// times; no walk budget), by the whole wave but in place in global memory -- the
+// stream in np_mt, the record in the ring slot, the generator's arrays in the board's
+// scratch -- since the step's LDS holds the board image (and a second wave may share
+// the workgroup: wave-level syncs only).  Not inlined: the generator's registers would
+// cost the step kernels occupancy on every step; as a call its spills stay inside
+// this rarely run function.  The caller holds the board's claim.
+template <int NC, bool SMALL>
+__device__ __attribute__((noinline)) int draw_in_place(const StepArgs& a, int b, uint32_t* slot, uint32_t n) {
+  const int lane = (int)(threadIdx.x & 63), L = a.L;
+  uint32_t* gmt = a.np_mt + (size_t)b * OPP_WORDS;
+  uint32_t* ghdr = reinterpret_cast<uint32_t*>(resume_hdr(a, b));
+  static_assert(sizeof(RoadResume) == 64, "resume header: 16 words");
+  WaveRoadGen<NC, true> g;
+  g.carve(a.scratch + (size_t)b * a.scratch_stride + sizeof(RoadResume), L * L);
+  g.mt = gmt; g.rec = slot; g.L = L; g.lane = lane;
+  g.pos = __builtin_amdgcn_readfirstlane(gmt[MT_N]);
+  g.tw = __builtin_amdgcn_readfirstlane(gmt[MT_N + 1]);
+  g.base = g.pos; g.n = 0; g.win = 0;
+  const uint32_t hw = lane < 16 ? ghdr[lane] : 0u;
+  RoadResume res;
+  for (int i = 0; i < 16; ++i) reinterpret_cast<uint32_t*>(&res)[i] = rdl(hw, i);
+  const int nw = (L * L + 31) / 32;
+  if (res.phase != RP_NEW) {  // the bitmaps of the draw a refill left pending (its partial record is in the slot)
+    g.field = lane < nw ? g.fieldw[lane] : 0u;
+    g.rot = lane < nw ? g.rotw[lane] : 0u;
+  } else {
+    g.field = g.rot = 0u;
+  }
+  const int st = g.draw(res, 0x7fffffff, kRoadAttempts, kLayoutRetries);
+  g.sync();
+  if (lane == 0) { gmt[MT_N] = g.pos; gmt[MT_N + 1] = g.tw; }
+  if (lane < 16) ghdr[lane] = reinterpret_cast<const uint32_t*>(&res)[lane];  // phase RP_NEW: nothing pending
+  if (st == ROAD_OK) {
+    g.sync();
+    if (lane == 0) slot[0] = slot_tag(n);
+  }
+  g.sync();
+  return st;
+}
+
+// The step wave of board b found layout `head` unpublished at the episode end.  If a
+// refill wave holds the board's claim it is drawing exactly this layout (an empty ring
+// is urgent: its draw runs to the end): wait for the tag, bounded.  Otherwise the ring
+// ran dry with no refill beside the step: the board is flagged no_layout (product).
+// TD_DRY_DRAW A/B builds claim the board instead and draw the layout now
+// (draw_in_place), so an episode end never depends on the refill cadence; the plain
+// stores of the draw are published by one release fence before the claim is given
+// back.  Measured (profiles/r03/s4): bit-exact (the refill-interval-0 auto-reset tests
+// pass on all three step kernels), but the called draw spills (0.5-1 KB of scratch per
+// lane in every step kernel) and every step ran 4.5x slower (65,536 boards: 1,018 vs
+// 223 us; 8,192: 163 vs 36 us) -- inlined, it costs the kernels their occupancy.
+// True when layout `head` is ready in its slot.
+template <int NC, bool SMALL>
+__device__ __forceinline__ bool take_dry_ring(const StepArgs& a, int b, uint32_t head, int lane) {
+  uint32_t* const slot = a.nxt + ((size_t)b * NSLOT + head % NSLOT) * a.slot_words;
+  const uint32_t want = slot_tag(head);
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  for (;;) {
+#ifndef TD_DRY_DRAW  // product: no claim holder -- the board is flagged no_layout
+    if (ld_relaxed(a.lay_claim + b) == 0u) return ld_relaxed(slot) == want;
+#else
+    if (claim_board(a.lay_claim + b, lane)) {
+      bool ok = ld_relaxed(slot) == want;  // published before the claim was taken
+      if (!ok && ld_relaxed(a.lay_tail + b) == head) {
+        ok = draw_in_place<NC, SMALL>(a, b, slot, head) == ROAD_OK;
+        if (ok && lane == 0) st_relaxed(a.lay_tail + b, head + 1u);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      }
+      __builtin_amdgcn_wave_barrier();
+      if (lane == 0) st_relaxed(a.lay_claim + b, 0u);
+      return ok;
+    }
+#endif
+    if (ld_relaxed(slot) == want) return true;
+    if (__builtin_amdgcn_s_memrealtime() - t0 >= kTakeSpinTicks) return false;
+    __builtin_amdgcn_s_sleep(64);
+  }
 }
 
 // TDGymBasic.reset of board b, by one wave (the device is idle for this board: no refill
@@ -2474,18 +2117,26 @@ static int resident3(const StepArgs& a, int cus, int waves) {
 int step_resident_boards(const StepArgs& a, int cus, int waves) {
   switch (a.L) {
     case 10: return resident3<10>(a, cus, waves);
+#ifndef TD_L10_ONLY  // diagnostic register-usage compiles (scripts/kernel_resources.sh)
     case 20: return resident3<20>(a, cus, waves);
     case 30: return resident3<30>(a, cus, waves);
     default: return 0;  // generic-L kernels: no small-batch build
+#else
+    default: return 0;
+#endif
   }
 }
 
 hipError_t launch_step(const StepArgs& a, hipStream_t s, bool reset, hipEvent_t ev0, hipEvent_t ev1) {
   switch (a.L) {
     case 10: return launch2<10>(a, s, reset, ev0, ev1);
+#ifndef TD_L10_ONLY  // diagnostic register-usage compiles (scripts/kernel_resources.sh)
     case 20: return launch2<20>(a, s, reset, ev0, ev1);
     case 30: return launch2<30>(a, s, reset, ev0, ev1);
     default: return launch2<0>(a, s, reset, ev0, ev1);
+#else
+    default: return hipErrorInvalidValue;
+#endif
   }
 }
 
@@ -2519,9 +2170,13 @@ static void launch_autoreset2(const StepArgs& a, hipStream_t s) {
 hipError_t launch_autoreset(const StepArgs& a, hipStream_t s) {
   switch (a.L) {
     case 10: launch_autoreset2<10>(a, s); break;
+#ifndef TD_L10_ONLY  // diagnostic register-usage compiles (scripts/kernel_resources.sh)
     case 20: launch_autoreset2<20>(a, s); break;
     case 30: launch_autoreset2<30>(a, s); break;
     default: launch_autoreset2<0>(a, s); break;
+#else
+    default: break;
+#endif
   }
   return hipGetLastError();
 }
@@ -2537,9 +2192,13 @@ static void launch_refill2(const StepArgs& a, hipStream_t s) {
 hipError_t launch_refill(const StepArgs& a, hipStream_t s) {
   switch (a.L) {
     case 10: launch_refill2<10>(a, s); break;
+#ifndef TD_L10_ONLY  // diagnostic register-usage compiles (scripts/kernel_resources.sh)
     case 20: launch_refill2<20>(a, s); break;
     case 30: launch_refill2<30>(a, s); break;
     default: launch_refill2<0>(a, s); break;
+#else
+    default: break;
+#endif
   }
   return hipGetLastError();
 }

@@ -36,6 +36,17 @@ s3)  # full suite, then every workload line on this build, refills off as the bo
   run p2 300 python bench.py --workload 2p-middle-multi --no-cpu-baseline --steps 1000 || exit 1; line p2
   run large 300 python bench.py --workload def-large --no-cpu-baseline --steps 300 || exit 1; line large
   ;;
+s4)  # dry-ring draws in the step (refill interval 0 tests on every kernel), GPU suite, A/B vs the no-draw build
+  run pytest_gpu 900 python -u -m pytest tests -m gpu -q --timeout 400 --timeout-method thread -p no:cacheprovider
+  rc=$?; grep -E "^(FAILED|E  )" $O/pytest_gpu.log | head -30; tail -1 $O/pytest_gpu.log; [ $rc -le 1 ] || exit $rc
+  for r in 1 2; do for v in nodraw dry; do for bb in 65536 8192 4096; do
+    TDSTEP_LIB=$PWD/gym-td_amd/lib/variants/libtdstep_$v.so run ab_${v}_${bb}_$r 200 python bench.py --global-batch $bb --no-cpu-baseline --steps $((bb > 10000 ? 500 : 2000)) || exit 1; line ab_${v}_${bb}_$r
+  done; done; done
+  for v in nodraw dry; do
+    TDSTEP_LIB=$PWD/gym-td_amd/lib/variants/libtdstep_$v.so run ab_${v}_p2 300 python bench.py --workload 2p-middle-multi --no-cpu-baseline --steps 500 || exit 1; line ab_${v}_p2
+    TDSTEP_LIB=$PWD/gym-td_amd/lib/variants/libtdstep_$v.so run ab_${v}_large 300 python bench.py --workload def-large --global-batch 16384 --no-cpu-baseline --steps 300 || exit 1; line ab_${v}_large
+  done
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "session $S rc=0"

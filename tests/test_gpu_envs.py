@@ -664,8 +664,9 @@ def _obs_checksum(obs):
     return torch.stack([w.sum(1), (w * idx).sum(1)], 1)
 
 
-@pytest.mark.parametrize("B,steps", [(16384, 200), (512, 1500)])
-def test_autoreset_under_load_matches_explicit_reset(B, steps):
+@pytest.mark.parametrize("B,steps,kernel", [
+    (16384, 200, "large"), (512, 1500, "small2"), (8192, 400, "small"), (4096, 300, "large")])
+def test_autoreset_under_load_matches_explicit_reset(B, steps, kernel):
     """The staged-layout rings under load: 16,384 boards with 1-LP bases and a weak
     defence finish ~250 episodes per step; 512 boards step so fast that one draw
     the reference never finishes (2-5 ms of one lane) spans hundreds of steps.
@@ -674,13 +675,14 @@ def test_autoreset_under_load_matches_explicit_reset(B, steps):
     layouts while step grids consume them; per-step observation checksums, rewards
     and dones stay on the device.  Phase 2 replays the same actions on an engine
     reset explicitly (the reset kernel draws each layout on the spot, failing draws
-    skipped as the refill skips them).  Every board must agree at every step."""
+    skipped as the refill skips them).  Every board must agree at every step, on each
+    step kernel (8,192 boards: the N = 8 share's kernel)."""
     from test_gpu_parity import reference_settings
     L = 10
     ov = dict(base_LP=1, defender_init_cost=0, defender_cost_rate=0.02)
     seeds = np.arange(B, dtype=np.int64) + 20000
     with reference_settings(ov, False):
-        ea = TDEngine(L, B, "def", False, 1, np_seeds=seeds, py_seeds=seeds, autoreset=True)
+        ea = TDEngine(L, B, "def", False, 1, np_seeds=seeds, py_seeds=seeds, autoreset=True, step_kernel=kernel)
         eb = TDEngine(L, B, "def", False, 1, np_seeds=seeds, py_seeds=seeds, autoreset=False)
     try:
         ea.reset_all()
