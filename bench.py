@@ -70,9 +70,18 @@ ENV_ID = {"def-small": "TD-def-small-v0", "2p-middle-multi": "TD-2p-middle-v0 (a
 DATA = {("def", False): "synthetic: uniform random defender actions, built-in lv1 opponent, seeded boards",
         ("2p", True): "synthetic: defender flags uniform in {0,1,2} (6,L,L), attacker clusters uniform in {0..4} (3,8), "
                       "seeded boards"}
-N_ACTION_BUFS = 8
+N_ACTION_BUFS = 8  # distinct pre-drawn action batches cycled through the timed steps (multi-action shapes)
 EVENT_EVERY = 8  # timed steps per sampled kernel duration (an event pair per launch costs ~10 % of the step rate at 8,192 boards)
-FLAG_BITS = (("enemy_overflow", 1), ("tower_overflow", 2), ("bad_action", 4), ("no_layout", 8), ("bad_move", 16))  # distinct pre-drawn action batches cycled through the timed steps (multi-action shapes)
+
+FLAG_BITS = (("enemy_overflow", 1), ("tower_overflow", 2), ("bad_action", 4), ("no_layout", 8), ("bad_move", 16))
+
+
+def event_every(steps, override=None):
+    """Timed launches per sampled kernel duration: every 8th over long runs, every launch
+    over short ones (the driver's 20-step line would otherwise average 3 launches)."""
+    if override:
+        return max(1, int(override))
+    return EVENT_EVERY if steps >= 8 * 16 else 1
 
 
 def algorithmic_bytes(L, mode="def", multi=False):
@@ -257,12 +266,14 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--autoreset", type=int, default=1, help="diagnostic: 0 keeps finished boards stepping (not the metric)")
     ap.add_argument("--timing", default="dispatch", choices=("dispatch", "marker", "none"),
-                    help="step-kernel durations: 'dispatch' = events bound to every %d-th timed launch "
-                         "(td_kernel_timing, the dispatch-packet timestamps rocprofv3 reports); 'marker' = torch "
-                         "event pairs around every %d-th launch (adds the marker packets' overhead); 'none' = "
-                         "no kernel timing (diagnostic A/B of the step rate)" % (EVENT_EVERY, EVENT_EVERY))
+                    help="step-kernel durations: 'dispatch' = events bound to every k-th timed launch "
+                         "(td_kernel_timing, the dispatch-packet timestamps rocprofv3 reports; k: --event-every); "
+                         "'marker' = torch event pairs around every k-th launch (adds the marker packets' "
+                         "overhead); 'none' = no kernel timing (diagnostic A/B of the step rate)")
     ap.add_argument("--step-kernel", default="auto", choices=("auto", "large", "small", "small2"),
                     help="diagnostic: force a step kernel (td_set_step_kernel); default td_create's rule")
+    ap.add_argument("--event-every", type=int, default=None,
+                    help="timed launches per sampled kernel duration (default: 8 from 128 steps, else 1)")
     ap.add_argument("--refill-interval", type=int, default=None,
                     help="diagnostic: steps between layout-refill launches in the timed region (0 = none)")
     args = ap.parse_args()
@@ -332,16 +343,17 @@ def main():
         eng.step(def_act=d, atk_act=a)
     acts = pool if multi else draw(K)
     stream = torch.cuda.current_stream(dev)
-    # HIP events bracket every EVENT_EVERY-th step kernel on its stream: the kernel's
+    # HIP events bracket every `every`-th step kernel on its stream: the kernel's
     # duration is sampled live over the timed region without a timing event pair
     # (and its cache flush) behind every launch
-    sampled = set(range(0, K, EVENT_EVERY)) if args.timing == "marker" else set()
+    every = event_every(K, args.event_every)
+    sampled = set(range(0, K, every)) if args.timing == "marker" else set()
     ev = {k: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for k in sampled}
     eng.episode_stats(clear=True)  # the device accumulates finished episodes of the timed steps
     if args.refill_interval is not None:
         eng.set_refill_interval(args.refill_interval)
     if args.timing == "dispatch":
-        eng.kernel_timing((K + EVENT_EVERY - 1) // EVENT_EVERY, EVENT_EVERY)  # timestamped by their own dispatch
+        eng.kernel_timing((K + every - 1) // every, every)  # timestamped by their own dispatch
 
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -404,8 +416,8 @@ def main():
                          "avg_kernel_us": avg_kernel_s * 1e6,
                          "kernel_samples": len(kern_ms) * world,
                          "kernel_timing": {"dispatch": "dispatch-packet timestamps of every %dth timed launch "
-                                                       "(td_kernel_timing)" % EVENT_EVERY,
-                                           "marker": "torch event pairs around every %dth launch" % EVENT_EVERY,
+                                                       "(td_kernel_timing)" % every,
+                                           "marker": "torch event pairs around every %dth launch" % every,
                                            "none": "not timed"}[args.timing],
                          "algorithmic_bytes_per_launch": B * bpe},
             "board_flags_nonzero": int((flags != 0).sum()),

@@ -47,6 +47,28 @@ s4)  # dry-ring draws in the step (refill interval 0 tests on every kernel), GPU
     TDSTEP_LIB=$PWD/gym-td_amd/lib/variants/libtdstep_$v.so run ab_${v}_large 300 python bench.py --workload def-large --global-batch 16384 --no-cpu-baseline --steps 300 || exit 1; line ab_${v}_large
   done
   ;;
+s5)  # write ceiling at the guide's shape and the step's shape; current-build profiles of configs[2] / configs[4]
+  run write_ceiling 300 ./scripts/bin/write_ceiling || exit 1
+  cat $O/write_ceiling.log
+  NO_PHASES=1 PROF_DIR=$O/prof_2p WL=2p-middle-multi B=16384 run prof_2p 900 bash scripts/profile_session.sh || exit 1
+  NO_PHASES=1 PROF_DIR=$O/prof_large WL=def-large B=16384 run prof_large 900 bash scripts/profile_session.sh || exit 1
+  ;;
+s6)  # step-kernel A/B per workload (two-wave kernel at large batches), timing-event overhead, PC sampling at 8,192
+  for wl in "def-large 16384" "def-large 131072" "2p-middle-multi 16384" "def-small 65536" "def-small 16384"; do
+    set -- $wl
+    for k in large small2; do
+      run ab_${1}_$2_$k 300 python bench.py --workload $1 --global-batch $2 --no-cpu-baseline --steps 200 --step-kernel $k || exit 1; line ab_${1}_$2_$k
+    done
+  done
+  for bb in 65536 8192; do
+    run ev_none_$bb 200 python bench.py --global-batch $bb --no-cpu-baseline --steps 20 --warmup 5 --timing none || exit 1; line ev_none_$bb
+    run ev_1_$bb 200 python bench.py --global-batch $bb --no-cpu-baseline --steps 20 --warmup 5 || exit 1; line ev_1_$bb
+    run ev_none200_$bb 200 python bench.py --global-batch $bb --no-cpu-baseline --steps 200 --timing none || exit 1; line ev_none200_$bb
+    run ev_1_200_$bb 200 python bench.py --global-batch $bb --no-cpu-baseline --steps 200 --event-every 1 || exit 1; line ev_1_200_$bb
+  done
+  TDSTEP_LIB=$PWD/gym-td_amd/lib/variants/libtdstep_pcs.so run pcs 300 rocprofv3 --pc-sampling-beta-enabled --pc-sampling-method stochastic --pc-sampling-unit cycles --pc-sampling-interval 1048576 -d $O/pcs -o pcs --output-format csv -- python bench.py --global-batch 8192 --no-cpu-baseline --steps 300 --burnin 300
+  echo "pcs rc=$?"; ls -R $O/pcs | head -20
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "session $S rc=0"
