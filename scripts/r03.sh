@@ -66,8 +66,16 @@ s6)  # step-kernel A/B per workload (two-wave kernel at large batches), timing-e
     run ev_none200_$bb 200 python bench.py --global-batch $bb --no-cpu-baseline --steps 200 --timing none || exit 1; line ev_none200_$bb
     run ev_1_200_$bb 200 python bench.py --global-batch $bb --no-cpu-baseline --steps 200 --event-every 1 || exit 1; line ev_1_200_$bb
   done
-  TDSTEP_LIB=$PWD/gym-td_amd/lib/variants/libtdstep_pcs.so run pcs 300 rocprofv3 --pc-sampling-beta-enabled --pc-sampling-method stochastic --pc-sampling-unit cycles --pc-sampling-interval 1048576 -d $O/pcs -o pcs --output-format csv -- python bench.py --global-batch 8192 --no-cpu-baseline --steps 300 --burnin 300
-  echo "pcs rc=$?"; ls -R $O/pcs | head -20
+  ;;
+s7)  # step kernel by batch: every kernel at the strong-scaling shares and around the thresholds, two passes
+  for r in 1 2; do
+    for bb in 32768 16384 12288 8192 6144 4096; do for k in large small small2; do
+      run k_${bb}_${k}_$r 200 python bench.py --global-batch $bb --no-cpu-baseline --steps 400 --step-kernel $k || exit 1; line k_${bb}_${k}_$r
+    done; done
+    for bb in 16384 32768 65536; do for k in large small2; do
+      run kl_${bb}_${k}_$r 300 python bench.py --workload def-large --global-batch $bb --no-cpu-baseline --steps 100 --step-kernel $k || exit 1; line kl_${bb}_${k}_$r
+    done; done
+  done
   ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
