@@ -172,7 +172,7 @@ struct WaveMt {
     const uint32_t d = pos - cbase;
     if (d < cn) {
       ++pos;
-      return (uint32_t)__shfl((int)cache, (int)d);
+      return rdl(cache, (int)d);  // d is wave-uniform: a scalar read, no LDS round trip
     }
     if (pos >= (uint32_t)MT_N) { pos = 0; tw = 0; cn = 0; }
     uint32_t y;
@@ -439,7 +439,7 @@ __device__ __forceinline__ void defender_scan(Smem<NC>& S, U& u, const Ctx& x, c
       if (!m) break;
       const int j = ctz64(m);
       const int c = base + j;
-      const uint32_t f = __shfl(fl, j);
+      const uint32_t f = rdl(fl, j);
       uint32_t rb = 0;
       for (int t = 0; t < 4; ++t)
         if ((f >> t) & 1u)
@@ -599,9 +599,9 @@ __device__ __forceinline__ double board_step(Smem<NC>& S, U& u, const Ctx& x, co
     if (lane < u.nt) { const double cd = dsub(tcd, 1.0); tcd = cd > 0.0 ? cd : 0.0; }
   } else {
     for (int k = 0; k < u.nt; ++k) {
-      double cd = dsub(__shfl(tcd, k), 1.0);                 // :307
+      double cd = dsub(rdl(tcd, k), 1.0);                    // :307
       if (!(cd > 0.0)) {
-        const uint32_t ti = __shfl(tinf_l, k);
+        const uint32_t ti = rdl(tinf_l, k);
         const int tt = (ti >> 12) & 3, tl = (ti >> 14) & 1, tc = ti & 0xfff, te = tw_eu(ti);
         const double rge = captured(x, te, [&](const TdDevCfg& c) { return c.t_rge[tt][tl]; });
         bool in0 = val[0] && (double)cheb(en_cell(inf[0]), tc, L) <= rge;
@@ -617,7 +617,7 @@ __device__ __forceinline__ double board_step(Smem<NC>& S, U& u, const Ctx& x, co
               else lp[1] = damage(lp[1], atk, e_def(x, inf[1]), tt == 1);
             }
           } else {
-            const uint32_t tinf = (tgt >> 6) ? __shfl(inf[1], tgt & 63) : __shfl(inf[0], tgt & 63);
+            const uint32_t tinf = (tgt >> 6) ? rdl(inf[1], tgt & 63) : rdl(inf[0], tgt & 63);
             const int tgc = en_cell(tinf);
             const double dr = captured(x, te, [&](const TdDevCfg& c) { return c.t_dmg[tt][tl]; });
             if (tt == 2) {  // TowerBomb splash (:95-110)

@@ -77,6 +77,19 @@ s7)  # step kernel by batch: every kernel at the strong-scaling shares and aroun
     done; done
   done
   ;;
+s8)  # GPU suite on the new kernel rule + scalar lane reads; lines; issue / i-cache counters at 8,192 and 65,536
+  run pytest_gpu 900 python -u -m pytest tests -m gpu -q --timeout 400 --timeout-method thread -p no:cacheprovider
+  rc=$?; grep -E "^(FAILED|E  )" $O/pytest_gpu.log | head -30; tail -1 $O/pytest_gpu.log; [ $rc -le 1 ] || exit $rc
+  for bb in 65536 32768 16384 8192 4096; do
+    run b$bb 200 python bench.py --global-batch $bb --no-cpu-baseline --steps 1000 || exit 1; line b$bb
+  done
+  for bb in 8192 65536; do
+    B="python bench.py --global-batch $bb --steps 20 --warmup 2 --burnin 300 --no-cpu-baseline"
+    run pmcA_$bb 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM -d $O/pmcA_$bb -o pmc --output-format csv -- $B || exit 1
+    run pmcB_$bb 300 rocprofv3 --pmc SQ_IFETCH SQ_IFETCH_LEVEL SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM SQ_BUSY_CYCLES SQ_WAVES -d $O/pmcB_$bb -o pmc --output-format csv -- $B || exit 1
+    run pmcC_$bb 300 rocprofv3 --pmc SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE SQC_ICACHE_REQ -d $O/pmcC_$bb -o pmc --output-format csv -- $B || exit 1
+  done
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "session $S rc=0"
