@@ -1004,6 +1004,9 @@ __device__ __forceinline__ void write_obs_lines(const Smem<NC>& S, int lane, flo
   // only a window at either end of the board holds lanes outside it (i < 0, i >= N4):
   // clamp there, so every lane reads LDS inside the board image
   auto unit = [&](int i, uint32_t wc) { return (wc & 4u) ? (i < 0 ? 0 : (i > N4 - 1 ? N4 - 1 : i)) : i; };
+#ifdef TD_OBS_NOUNROLL  // A/B builds: one copy of the G-window group (code size)
+#pragma nounroll
+#endif
   for (int k0 = KB; k0 < K; k0 += G) {
     uint4 A[G];
     uint32_t W[G];
@@ -1262,6 +1265,9 @@ __device__ __forceinline__ void opponent_enemy(Smem<NC>& S, U& u, const Ctx& x, 
   uint32_t types = 0;
   int road;
   if (difficulty == 0) {
+#ifdef TD_OBS_NOUNROLL
+#pragma nounroll
+#endif
     for (int k = 0; k < 8; ++k) types |= (uint32_t)R.slot(4) << (4 * k);
     road = (int)R.ri(0, u.num_roads - 1);
   } else {
@@ -1487,6 +1493,7 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
       }
     }
   }
+  STAMP(11);
   // ---- attacker
   if (MODE == MODE_DEF) {
     with_opp_rng(a, b, x.lane, R, [&](auto& G) { opponent_enemy(S, u, x, G, a.difficulty); });
@@ -1498,6 +1505,7 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
     if (MODE == MODE_ATK)
       with_opp_rng(a, b, x.lane, R, [&](auto& G) { opponent_tower(S, u, x, G, a.difficulty); });
   }
+  STAMP(12);
   // the towers and map[6] are final: cell words back to HBM if they changed, then
   // packed for the rest of the step (board_step reads the packed direction and distance)
   store_cells(S, u, x, a, b);
@@ -1550,7 +1558,9 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
   }
   STAMP(5);
   enemy_stats(S, u, x);  // no-op for a board without enemies (e.g. just reset)
+  STAMP(13);
   channel_scalars(S, u, x);
+  STAMP(14);
   if (was_reset) {  // the new episode's layout
     store_cells(S, u, x, a, b);
     pack_obs_cells(S, x);

@@ -39,7 +39,10 @@ if fn is not None:
     fn.restype = _lib.ctypes.c_int
     fn.argtypes = [_lib.c_vp, _lib.c_vp]
     fn(eng._h, stamps.data_ptr())
-names = ["load(+early obs)", "actions", "sort", "towers", "march+costs", "stats+state+out", "obs", "-"]
+# stamp slots in time order (td_step.hip STAMP(i)); 9 / 10 are the 100-MHz start / end
+order = [0, 1, 11, 12, 2, 3, 4, 5, 13, 14, 6, 7, 8]
+names = ["load", "defender", "attacker", "cells+pack", "sort", "towers", "march+costs+done", "enemy_stats",
+         "channel_scalars", "state+out", "obs", "-"]
 acc = np.zeros(len(names))
 t0 = time.time()
 for k in range(burn, burn + 20):
@@ -47,8 +50,7 @@ for k in range(burn, burn + 20):
     torch.cuda.synchronize()
     if fn is not None:
         s = stamps.cpu().numpy().astype(np.float64)
-        idx = [0, 1, 2, 3, 4, 5, 6, 7, 8]
-        d = np.diff(s[:, idx], axis=1)
+        d = np.diff(s[:, order], axis=1)
         acc += d.mean(axis=0)
 dt = (time.time() - t0) / 20
 print("B=%d L=%d step %.1f us" % (B, L, dt * 1e6))
@@ -72,3 +74,14 @@ if fn is not None:
     print("  shader clock ~ %.0f MHz" % (100.0 * (s[:, 8] - s[:, 0]).sum() / max(1, (s[:, 10] - s[:, 9]).sum())))
     st = eng.export_state(0, min(B, 4096))
     print("  mean enemies %.2f towers %.2f steps %.0f" % (st["hdr"]["n_en"].mean(), st["hdr"]["n_tw"].mean(), st["hdr"]["steps"].mean()))
+    # which boards form the tail: wave life (the last step) by board features
+    nb = min(B, 4096)
+    lf = life[:nb]
+    tw, en, dn = st["hdr"]["n_tw"], st["hdr"]["n_en"], eng.done[:nb].cpu().numpy().astype(bool)
+    cyc = (s[:nb, order[1:]] - s[:nb, order[:-1]]).astype(np.float64)
+    slow = lf >= np.percentile(lf, 90)
+    print("  tail (p90+ life) vs rest: towers %.2f / %.2f, enemies %.2f / %.2f, done %.3f / %.3f" % (
+        tw[slow].mean(), tw[~slow].mean(), en[slow].mean(), en[~slow].mean(), dn[slow].mean(), dn[~slow].mean()))
+    print("  tail phase cycles: " + " ".join("%s=%.0f/%.0f" % (n, cyc[slow, j].mean(), cyc[~slow, j].mean())
+                                           for j, n in enumerate(names[:-1])))
+    print("  start us of tail / rest: %.2f / %.2f" % (start[:nb][slow].mean(), start[:nb][~slow].mean()))

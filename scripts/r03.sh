@@ -90,6 +90,12 @@ s8)  # GPU suite on the new kernel rule + scalar lane reads; lines; issue / i-ca
     run pmcC_$bb 300 rocprofv3 --pmc SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE SQC_ICACHE_REQ -d $O/pmcC_$bb -o pmc --output-format csv -- $B || exit 1
   done
   ;;
+s9)  # per-phase wave cycles (stamps build): alone on its SIMD (256 boards), 4,096, 8,192, 65,536; the tail boards
+  for bb in 256 4096 8192 65536; do
+    TDSTEP_LIB=$PWD/gym-td_amd/lib/libtdstep_stamps.so run phases_$bb 300 python scripts/probe_phases.py $bb 10 600 || exit 1
+    cat $O/phases_$bb.log | grep -v amdgpu.ids
+  done
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "session $S rc=0"
