@@ -1618,6 +1618,20 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
   STAMP_RT(10);
 }
 
+// The kernel's StepArgs, read through the kernarg segment where each field is used
+// (scalar loads that hit the constant cache) instead of being held in SGPRs for the
+// whole kernel: with 80 SGPRs (8 waves per SIMD) the small kernel otherwise spilled ~50
+// SGPRs into VGPR lanes and read them back with ~150 v_readlane (static counts, L = 10).
+// The StepArgs must be the kernel's first argument (kernarg offset 0).
+__device__ __forceinline__ const StepArgs& kargs(const StepArgs& a) {
+#ifdef TD_KARG_BYVAL  // A/B builds: the by-value argument as the compiler keeps it
+  return a;
+#else
+  (void)a;
+  return *reinterpret_cast<const StepArgs*>(__builtin_amdgcn_kernarg_segment_ptr());
+#endif
+}
+
 // One workgroup (one wave) per board.  (A persistent variant that prefetched the
 // next board while stepping the current one measured slower: its static board
 // assignment leaves a one-board tail, and the step is bound by HBM writes.)
@@ -1650,7 +1664,7 @@ constexpr int large_waves() { return LT == 10 ? 7 : LT == 20 ? 5 : 3; }  // LDS-
 #endif
 template <int LT, int MODE, bool SCAN>
 __global__ __launch_bounds__(64) TD_LARGE_ATTR void td_step_kernel(StepArgs a) {
-  step_kernel_body<LT, MODE, SCAN, false>(a);
+  step_kernel_body<LT, MODE, SCAN, false>(kargs(a));
 }
 
 // Batches that fit one round of waves.  8 waves per SIMD where LDS allows it (L = 10:
@@ -1673,7 +1687,7 @@ constexpr int small2_waves() { return LT == 30 ? 6 : 8; }
 #endif
 template <int LT, int MODE, bool SCAN>
 __global__ __launch_bounds__(64) TD_SMALL_ATTR void td_step_kernel_small(StepArgs a) {
-  step_kernel_body<LT, MODE, SCAN, true>(a);
+  step_kernel_body<LT, MODE, SCAN, true>(kargs(a));
 }
 
 // Batches up to half the resident waves: two waves per board.  The first steps the board
@@ -1681,7 +1695,8 @@ __global__ __launch_bounds__(64) TD_SMALL_ATTR void td_step_kernel_small(StepArg
 // of the observation windows beside it, which shortens a board's critical path where the
 // batch leaves issue slots free (4,096 boards: 8,192 waves, 8 per SIMD).
 template <int LT, int MODE, bool SCAN>
-__global__ __launch_bounds__(128) TD_SMALL2_ATTR void td_step_kernel_small2(StepArgs a) {
+__global__ __launch_bounds__(128) TD_SMALL2_ATTR void td_step_kernel_small2(StepArgs a_) {
+  const StepArgs& a = kargs(a_);
   constexpr int NC = LT * LT;
   __shared__ Smem<NC> S;
   const int b = blockIdx.x;

@@ -96,6 +96,17 @@ s9)  # per-phase wave cycles (stamps build): alone on its SIMD (256 boards), 4,0
     cat $O/phases_$bb.log | grep -v amdgpu.ids
   done
   ;;
+s10) # kernel arguments read through the kernarg segment (product) vs by value: A/B, then the GPU suite
+  for r in 1 2; do for v in byval karg; do
+    for bb in 65536 16384 8192 4096; do
+      TDSTEP_LIB=$PWD/gym-td_amd/lib/variants/libtdstep_$v.so run ab_${v}_${bb}_$r 200 python bench.py --global-batch $bb --no-cpu-baseline --steps $((bb > 10000 ? 400 : 2000)) || exit 1; line ab_${v}_${bb}_$r
+    done
+    TDSTEP_LIB=$PWD/gym-td_amd/lib/variants/libtdstep_$v.so run ab_${v}_p2_$r 300 python bench.py --workload 2p-middle-multi --no-cpu-baseline --steps 300 || exit 1; line ab_${v}_p2_$r
+    TDSTEP_LIB=$PWD/gym-td_amd/lib/variants/libtdstep_$v.so run ab_${v}_large_$r 300 python bench.py --workload def-large --global-batch 16384 --no-cpu-baseline --steps 200 || exit 1; line ab_${v}_large_$r
+  done; done
+  run pytest_gpu 900 python -u -m pytest tests -m gpu -q --timeout 400 --timeout-method thread -p no:cacheprovider
+  rc=$?; grep -E "^(FAILED|E  )" $O/pytest_gpu.log | head -30; tail -1 $O/pytest_gpu.log; [ $rc -le 1 ] || exit $rc
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "session $S rc=0"
