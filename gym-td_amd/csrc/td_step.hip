@@ -1130,9 +1130,8 @@ __device__ __forceinline__ void prefetch_issue(Prefetch& P, const StepArgs& a, i
   }
   if ((ncr & 3) == 0) {
     P.c4 = lane < (ncr >> 2) ? reinterpret_cast<const uint4*>(a.cells + cb)[lane] : uint4{0u, 0u, 0u, 0u};
-  } else {
-    P.c4.x = lane < ncr ? a.cells[cb + lane] : 0u;
-    P.c4.y = lane + 64 < ncr ? a.cells[cb + lane + 64] : 0u;
+  } else {  // (assigned whole: member-wise stores kept P.c4 in scratch in the generic-L build)
+    P.c4 = uint4{lane < ncr ? a.cells[cb + lane] : 0u, lane + 64 < ncr ? a.cells[cb + lane + 64] : 0u, 0u, 0u};
   }
   const uint32_t* src;
   if (lane < PF_ACT) src = reinterpret_cast<const uint32_t*>(a.hdr + b) + lane;
@@ -1620,15 +1619,18 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
 
 // The kernel's StepArgs, read through the kernarg segment where each field is used
 // (scalar loads that hit the constant cache) instead of being held in SGPRs for the
-// whole kernel: with 80 SGPRs (8 waves per SIMD) the small kernel otherwise spilled ~50
-// SGPRs into VGPR lanes and read them back with ~150 v_readlane (static counts, L = 10).
-// The StepArgs must be the kernel's first argument (kernarg offset 0).
+// whole kernel: with 80 SGPRs (8 waves per SIMD) the small kernels otherwise spilled ~50
+// SGPRs into VGPR lanes and read them back with ~150 v_readlane (static counts, L = 10):
+// +1.4 % at 4,096 / 8,192 boards (profiles/r03/s10).  The large kernel keeps its
+// by-value arguments (106 SGPRs at 7 waves per SIMD; read through the segment it fell
+// to 83 SGPRs, ran 8 waves per SIMD and lost 4.6 % at 65,536 boards).  The StepArgs must
+// be the kernel's first argument (kernarg offset 0).
 __device__ __forceinline__ const StepArgs& kargs(const StepArgs& a) {
 #ifdef TD_KARG_BYVAL  // A/B builds: the by-value argument as the compiler keeps it
   return a;
 #else
   (void)a;
-  return *reinterpret_cast<const StepArgs*>(__builtin_amdgcn_kernarg_segment_ptr());
+  return *(const StepArgs*)__builtin_amdgcn_kernarg_segment_ptr();  // (C cast: leaves the constant address space)
 #endif
 }
 
@@ -1664,7 +1666,7 @@ constexpr int large_waves() { return LT == 10 ? 7 : LT == 20 ? 5 : 3; }  // LDS-
 #endif
 template <int LT, int MODE, bool SCAN>
 __global__ __launch_bounds__(64) TD_LARGE_ATTR void td_step_kernel(StepArgs a) {
-  step_kernel_body<LT, MODE, SCAN, false>(kargs(a));
+  step_kernel_body<LT, MODE, SCAN, false>(a);  // by value (see kargs)
 }
 
 // Batches that fit one round of waves.  8 waves per SIMD where LDS allows it (L = 10:
@@ -1678,12 +1680,17 @@ template <int LT>
 constexpr int small_waves() { return LT == 10 ? 8 : LT == 20 ? 5 : 3; }
 template <int LT>
 constexpr int small2_waves() { return LT == 30 ? 6 : 8; }
+template <int LT, int MODE, bool SCAN>
+constexpr int small2_cap() { return LT == 20 && SCAN ? 5 : LT == 20 && MODE == MODE_ATK ? 6 : 8; }
 #ifdef TD_DRY_DRAW
 #define TD_SMALL_ATTR __attribute__((amdgpu_waves_per_eu(small_waves<LT>(), small_waves<LT>())))
 #define TD_SMALL2_ATTR __attribute__((amdgpu_waves_per_eu(small2_waves<LT>(), small2_waves<LT>())))
 #else
 #define TD_SMALL_ATTR __attribute__((amdgpu_waves_per_eu(8, 8)))
-#define TD_SMALL2_ATTR __attribute__((amdgpu_waves_per_eu(8, 8)))
+// The two-wave 20x20 kernels of the multi-action scan and of TD-atk do not fit 64 VGPRs:
+// at 8 waves per SIMD they spilled (112-116 / 8 B of scratch per lane; the scan still
+// spilled at 6), so 5 / 6.
+#define TD_SMALL2_ATTR __attribute__((amdgpu_waves_per_eu(small2_cap<LT, MODE, SCAN>(), small2_cap<LT, MODE, SCAN>())))
 #endif
 template <int LT, int MODE, bool SCAN>
 __global__ __launch_bounds__(64) TD_SMALL_ATTR void td_step_kernel_small(StepArgs a) {

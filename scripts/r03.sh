@@ -107,6 +107,21 @@ s10) # kernel arguments read through the kernarg segment (product) vs by value: 
   run pytest_gpu 900 python -u -m pytest tests -m gpu -q --timeout 400 --timeout-method thread -p no:cacheprovider
   rc=$?; grep -E "^(FAILED|E  )" $O/pytest_gpu.log | head -30; tail -1 $O/pytest_gpu.log; [ $rc -le 1 ] || exit $rc
   ;;
+s11) # the round's build: GPU suite, every workload line, refill cost at the small shares (interleaved A/B)
+  run pytest_gpu 900 python -u -m pytest tests -m gpu -q --timeout 400 --timeout-method thread -p no:cacheprovider
+  rc=$?; grep -E "^(FAILED|E  )" $O/pytest_gpu.log | head -30; tail -1 $O/pytest_gpu.log; [ $rc -le 1 ] || exit $rc
+  run smoke 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" || exit 1
+  run bench_default 300 python bench.py || exit 1
+  grep '^{' $O/bench_default.log; line bench_default
+  for bb in 32768 16384; do run b$bb 200 python bench.py --global-batch $bb --no-cpu-baseline --steps 1000 || exit 1; line b$bb; done
+  for r in 1 2; do for bb in 8192 4096; do
+    run b${bb}_$r 200 python bench.py --global-batch $bb --no-cpu-baseline --steps 3000 || exit 1; line b${bb}_$r
+    run b${bb}_norefill_$r 200 python bench.py --global-batch $bb --no-cpu-baseline --steps 3000 --refill-interval 0 || exit 1; line b${bb}_norefill_$r
+  done; done
+  run p2 300 python bench.py --workload 2p-middle-multi --no-cpu-baseline --steps 500 || exit 1; line p2
+  run large16k 300 python bench.py --workload def-large --global-batch 16384 --no-cpu-baseline --steps 300 || exit 1; line large16k
+  run large 300 python bench.py --workload def-large --no-cpu-baseline --steps 100 || exit 1; line large
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "session $S rc=0"
