@@ -58,6 +58,14 @@ constexpr int kRefillWaves = 1024;
 // step's waves need (8,192 boards, a refill every 4th step: 37.9 us per step at 48 walks, 36.5 at 12, 36.6 at 4,
 // 36.9 at 1; 34.3 without refills, profiles/r02/s21_session.log).
 constexpr int kWalksPerStep = 3;
+// The ring guard (td_step.hip td_refill_kernel, guard = G) runs on the step stream before
+// every G-th step and fills every ring below G layouts to G: a board consumes at most one
+// layout per step, so none of the next G steps finds a ring empty, whatever the refill
+// cadence.  G = NSLOT - 1: a ring the side refills keep full only falls below it when a
+// board finishes two episodes between two refills, so the guard rarely draws (G = NSLOT
+// made it draw for every board that finished one: 8,192 boards 78 vs 35 us per step,
+// profiles/r03/s12); a launch is then a scan of the rings, paid every G steps.
+constexpr int kGuardEvery = NSLOT - 1;
 constexpr int kSideStreams = 2;  // refill streams: one stuck on a long draw does not stall the next (the HIP
                                  // runtime has 4 hardware queues per process; the step stream needs one)
 
@@ -96,7 +104,10 @@ struct td_handle {
   int refill_every = kRefillEvery;  // 0: no refill launches (td_set_refill_interval)
   int refill_waves = kRefillWaves;  // waves per refill launch
   int n_side = kSideStreams;  // A/B knob (TD_SIDE_STREAMS)
+  int refill_serial = 0;      // A/B knob (TD_REFILL_SERIAL=1): refills on the step stream, between steps
   int refill_walks = 0;  // walks per board per refill launch (0: 12 per step of interval; TD_REFILL_WALKS)
+  int guard_every = kGuardEvery;  // ring guard cadence (<= NSLOT; 0 only in TD_GUARD_EVERY=0 A/B runs)
+  int since_guard = kGuardEvery;  // steps launched since the last ring guard (>= guard_every: guard first)
   // td_kernel_timing: event pairs bound to the next `tev_cap` step-kernel dispatches
   std::vector<hipEvent_t> tev;
   int tev_cap = 0, tev_n = 0, tev_every = 1;
@@ -222,6 +233,7 @@ void apply_kernel(td_handle* h, int small) {
 // Drop staged layouts: they were drawn from a stream that has been replaced.
 int drop_staged(td_handle* h, int b) {
   HIP_OK(hipDeviceSynchronize());
+  h->since_guard = kGuardEvery;
   const size_t ring = (size_t)NSLOT * slot_words(h->L);
   HIP_OK(hipMemset(h->d_nxt + (size_t)b * ring, 0, ring * 4));
   HIP_OK(hipMemset(h->d_lay_head + b, 0, 4));
@@ -233,6 +245,7 @@ int drop_staged(td_handle* h, int b) {
 
 int drop_all_staged(td_handle* h) {
   HIP_OK(hipDeviceSynchronize());
+  h->since_guard = kGuardEvery;
   HIP_OK(hipMemset(h->d_nxt, 0, (size_t)h->B * NSLOT * slot_words(h->L) * 4));
   HIP_OK(hipMemset(h->d_lay_head, 0, (size_t)h->B * 4));
   HIP_OK(hipMemset(h->d_lay_tail, 0, (size_t)h->B * 4));
@@ -253,6 +266,10 @@ int drop_all_staged(td_handle* h) {
 int start_refill(td_handle* h, hipStream_t s) {
   const int q = h->next_side;
   StepArgs a = base_args(h);
+  if (h->refill_serial) {
+    HIP_OK(launch_refill(a, s));
+    return 0;
+  }
   HIP_OK(hipEventRecord(h->ev_main, s));
   HIP_OK(hipStreamWaitEvent(h->side[q], h->ev_main, 0));
   HIP_OK(launch_refill(a, h->side[q]));
@@ -267,6 +284,7 @@ int run_reset(td_handle* h, const std::vector<uint8_t>& mask, float* obs, hipStr
   a.obs = obs;
   a.reset_mask = h->d_mask;
   HIP_OK(launch_step(a, s, true));
+  h->since_guard = kGuardEvery;  // a reset consumed layouts: guard before the next step
   if (h->autoreset && !h->opp_np && start_refill(h, s)) return -1;
   HIP_OK(hipDeviceSynchronize());
   return 0;
@@ -360,7 +378,7 @@ td_handle* td_create(const td_config* cfg, int map_size, int n_boards, int mode,
   rc |= dalloc(&h->d_opp, B * OPP_WORDS);
   rc |= dalloc(&h->d_hot, B * HOT_WORDS);
   rc |= dalloc(&h->d_np, B * OPP_WORDS);
-  rc |= dalloc(&h->d_nxt, B * NSLOT * slot_words(map_size));
+  rc |= dalloc(&h->d_nxt, (size_t)B * NSLOT * slot_words(map_size));
   rc |= dalloc(&h->d_lay_head, B);
   rc |= dalloc(&h->d_lay_tail, B);
   rc |= dalloc(&h->d_lay_claim, B);
@@ -420,7 +438,9 @@ td_handle* td_create(const td_config* cfg, int map_size, int n_boards, int mode,
     if (const char* e = std::getenv("TD_REFILL_EVERY")) h->refill_every = std::max(0, std::atoi(e));  // A/B runs
     if (const char* e = std::getenv("TD_REFILL_WAVES")) h->refill_waves = std::max(1, std::atoi(e));
     if (const char* e = std::getenv("TD_REFILL_WALKS")) h->refill_walks = std::max(1, std::atoi(e));
+    if (const char* e = std::getenv("TD_GUARD_EVERY")) h->guard_every = std::min(kGuardEvery, std::max(0, std::atoi(e)));  // A/B runs
     if (const char* e = std::getenv("TD_SIDE_STREAMS")) h->n_side = std::min(kSideStreams, std::max(1, std::atoi(e)));
+    if (const char* e = std::getenv("TD_REFILL_SERIAL")) h->refill_serial = std::atoi(e) ? 1 : 0;
   }
   std::vector<uint32_t> seeds(B);
   for (size_t b = 0; b < B; ++b) seeds[b] = (uint32_t)b;
@@ -488,6 +508,7 @@ int td_set_autoreset(td_handle* h, int on) {
   if (!h) return fail("NULL handle");
   HIP_OK(hipDeviceSynchronize());
   h->autoreset = on ? 1 : 0;
+  h->since_guard = kGuardEvery;
   return 0;
 }
 
@@ -498,6 +519,7 @@ int td_set_autoreset(td_handle* h, int on) {
 int td_set_random_agent(td_handle* h, int random_agent) {
   if (!h) return fail("NULL handle");
   HIP_OK(hipDeviceSynchronize());
+  h->since_guard = kGuardEvery;
   if (!random_agent && !h->opp_np) {
     std::vector<uint32_t> head((size_t)h->B), tail((size_t)h->B);
     HIP_OK(hipMemcpy(head.data(), h->d_lay_head, (size_t)h->B * 4, hipMemcpyDeviceToHost));
@@ -633,6 +655,7 @@ int td_reset_layouts(td_handle* h, const uint32_t* recs, const int32_t* boards, 
     a.ovr_idx = h->d_ovr_idx;
     a.ovr_rec = h->d_stage;
     HIP_OK(launch_step(a, s, true));
+    h->since_guard = kGuardEvery;
     HIP_OK(hipStreamSynchronize(s));
   }
   return 0;
@@ -659,6 +682,11 @@ int td_step(td_handle* h, const td_step_io* io, void* stream) {
   if (h->autoreset && !h->opp_np && h->refill_every > 0 && (h->steps % h->refill_every) == 0 &&
       start_refill(h, s))
     return -1;
+  // the ring guard (kGuardEvery): behind the previous step, beside the refill just launched
+  if (h->autoreset && !h->opp_np && h->guard_every > 0 && h->since_guard >= h->guard_every) {
+    HIP_OK(launch_refill(a, s, h->guard_every));
+    h->since_guard = 0;
+  }
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (h->tev_n < h->tev_cap && (h->steps - h->tev_from) % h->tev_every == 0) {
     e0 = h->tev[2 * (size_t)h->tev_n];
@@ -668,6 +696,7 @@ int td_step(td_handle* h, const td_step_io* io, void* stream) {
   HIP_OK(launch_step(a, s, false, e0, e1));
   if (h->autoreset && h->opp_np) HIP_OK(launch_autoreset(a, s));
   h->steps += 1;
+  h->since_guard += 1;
   return 0;
 }
 

@@ -77,13 +77,18 @@ int step_resident_boards(const StepArgs& a, int cus, int waves);
 hipError_t launch_autoreset(const StepArgs& a, hipStream_t s);
 // Config epochs referred to by live enemies / towers: bit e of used[NCFG / 32] (zeroed by the caller).
 hipError_t launch_cfg_usage(const StepArgs& a, uint32_t* used, hipStream_t s);
-// Draw staged layouts for every board whose ring has a free slot (side stream).
-hipError_t launch_refill(const StepArgs& a, hipStream_t s);
+// Draw staged layouts for every board whose ring has a free slot: a side-stream refill
+// (guard = 0), or the ring guard on the step stream (guard = G: every ring below G
+// layouts filled to G, draws run to the end; td_step.hip td_refill_kernel).
+hipError_t launch_refill(const StepArgs& a, hipStream_t s, int guard = 0);
 // The built-in opponent (side 0: random_enemy_lv<level>, 1: random_tower_lv<level>)
 // on the boards in a.reset_mask (nullptr = all).
 hipError_t launch_opponent(const StepArgs& a, int side, int level, hipStream_t s);
 
-constexpr int NSLOT = 4;  // staged layouts per board: four episodes of slack for the refill
+// Staged layouts per board: sixteen episodes of slack for the side refills, and the
+// ring guard (td_refill_kernel) needs to run only every NSLOT - 1 steps.  (NSLOT = 4 with
+// a guard every 3rd step: +4 % / +7-9 % per step at 8,192 / 4,096 boards, profiles/r03/s13.)
+constexpr int NSLOT = 16;
 __host__ __device__ inline uint32_t slot_tag(uint32_t n) { return 0x80000000u | (n & 0x7fffffffu); }
 __host__ __device__ inline int slot_words(int L) { return (8 + L * L + 31) & ~31; }
 // Boards scanned per refill wave when a refill launch has `waves` waves (at most 64:

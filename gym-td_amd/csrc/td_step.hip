@@ -110,10 +110,21 @@ struct Ctx {
 // A value an enemy or tower captured when it was created or upgraded (TDElements.py:
 // 4-43, 45-63, 134-170): from the block of its epoch -- the staged current one, or
 // (after a paramConfig) an older block in HBM.
+//
+// The two loads must stay two loads: merged into one load of a selected pointer (what
+// the compiler does with the plain if) they become a FLAT load -- LDS or global -- which
+// counts in vmcnt, and waiting for it waits for every store the wave has in flight
+// (s_waitcnt vmcnt(0) lgkmcnt(0)).  The empty asm on the HBM value keeps them apart.
+__device__ __forceinline__ double keep_apart(double v) {
+#ifndef TD_AB_FLAT  // A/B builds: the merged (flat) load
+  asm volatile("" : "+v"(v));
+#endif
+  return v;
+}
 template <class F>
 __device__ __forceinline__ double captured(const Ctx& x, int ep, F f) {
   double v = f(x.C);
-  if (ep != x.ep) v = f(x.tab[ep]);
+  if (ep != x.ep) v = keep_apart(f(x.tab[ep]));
   return v;
 }
 
@@ -152,16 +163,22 @@ struct WaveMt {
       }
     }
   }
-  __device__ __forceinline__ void prefetch_finish(int lane) {
-    const uint32_t q = cbase + (uint32_t)lane;
+  // finish(..., false) leaves the twisted words' store to prefetch_store: a store's
+  // registers may only be reused once it has completed (s_waitcnt vmcnt), so the step
+  // kernels issue it with the other state stores at the end of the step.
+  __device__ __forceinline__ void prefetch_finish(int lane, bool store = true) {
     uint32_t y = pa;
     if (plazy) {
       const uint32_t yy = (pa & 0x80000000u) | (pnb & 0x7fffffffu);
       y = pfar ^ (yy >> 1) ^ ((yy & 1u) ? 0x9908b0dfu : 0u);
-      w[q] = y;  // after every lane's loads (data dependency)
+      pa = y;
     }
+    if (store) prefetch_store(lane);
     if (cbase + cn > tw) tw = cbase + cn;
     cache = pmine ? mt_temper(y) : 0u;
+  }
+  __device__ __forceinline__ void prefetch_store(int lane) {
+    if (plazy) w[cbase + (uint32_t)lane] = pa;  // after every lane's loads (data dependency)
   }
   __device__ __forceinline__ void prefetch(int lane) {
     prefetch_issue(lane);
@@ -553,7 +570,7 @@ __device__ __forceinline__ double board_step(Smem<NC>& S, U& u, const Ctx& x, co
 
   // --- stable sort by f64 key dist - margin (:305): rank = #smaller + #equal-before
   const int n = u.n;
-  double lp[2], mg[2], key[2];
+  double lp[2], mg[2];
   uint32_t inf[2];
   bool val[2];
 #pragma unroll
@@ -563,29 +580,33 @@ __device__ __forceinline__ double board_step(Smem<NC>& S, U& u, const Ctx& x, co
     lp[s] = val[s] ? S.eLP[i] : 0.0;
     mg[s] = val[s] ? S.eMg[i] : 0.0;
     inf[s] = val[s] ? S.eInf[i] : 0u;
-    key[s] = val[s] ? dsub((double)pk_dist(S.cell[en_cell(inf[s])]), mg[s]) : 0.0;
   }
-  int rank[2] = {0, 0};
-  for (int j = 0; j < n; ++j) {  // enemy j's key from the lane that holds it
-    const double kj = j < 64 ? rdl(key[0], j) : rdl(key[1], j - 64);
+  if (n > 1) {  // (a list of 0 or 1 enemies is sorted; most boards, most steps)
+    double key[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) key[s] = val[s] ? dsub((double)pk_dist(S.cell[en_cell(inf[s])]), mg[s]) : 0.0;
+    int rank[2] = {0, 0};
+    for (int j = 0; j < n; ++j) {  // enemy j's key from the lane that holds it
+      const double kj = j < 64 ? rdl(key[0], j) : rdl(key[1], j - 64);
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        int i = lane + 64 * s;
+        if (kj < key[s] || (kj == key[s] && j < i)) rank[s] += 1;
+      }
+    }
+    wsync();
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+      if (val[s]) { S.eLP[rank[s]] = lp[s]; S.eMg[rank[s]] = mg[s]; S.eInf[rank[s]] = inf[s]; }
+    wsync();
+    // lane owns sorted enemies lane and lane + 64
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       int i = lane + 64 * s;
-      if (kj < key[s] || (kj == key[s] && j < i)) rank[s] += 1;
+      lp[s] = val[s] ? S.eLP[i] : 0.0;
+      mg[s] = val[s] ? S.eMg[i] : 0.0;
+      inf[s] = val[s] ? S.eInf[i] : 0u;
     }
-  }
-  wsync();
-#pragma unroll
-  for (int s = 0; s < 2; ++s)
-    if (val[s]) { S.eLP[rank[s]] = lp[s]; S.eMg[rank[s]] = mg[s]; S.eInf[rank[s]] = inf[s]; }
-  wsync();
-  // lane owns sorted enemies lane and lane + 64
-#pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    int i = lane + 64 * s;
-    lp[s] = val[s] ? S.eLP[i] : 0.0;
-    mg[s] = val[s] ? S.eMg[i] : 0.0;
-    inf[s] = val[s] ? S.eInf[i] : 0u;
   }
 
   STAMP(3);
@@ -598,19 +619,34 @@ __device__ __forceinline__ double board_step(Smem<NC>& S, U& u, const Ctx& x, co
     // no enemy anywhere: every tower just cools down (cd -= 1; no target; clamp at 0)
     if (lane < u.nt) { const double cd = dsub(tcd, 1.0); tcd = cd > 0.0 ? cd : 0.0; }
   } else {
+    // Targeting never depends on another tower's shot (dead enemies stay targetable), so
+    // what the serial loop needs per tower -- range, interval, attack and splash as the
+    // tower captured them -- is gathered once, one tower per lane, into the enemy
+    // arrays' LDS (dead between the sorted load above and the compaction below): the
+    // loop reads it with one uniform-address LDS load per value, no epoch branches.
+    double* const tp = S.eLP;  // [TCAP][4]: rge, intv, atk, dmgrge
+    static_assert(sizeof(S.eLP) >= TCAP * 4 * sizeof(double), "tower table in the enemy LP array");
+    if (lane < u.nt) {
+      const int tt = (tinf_l >> 12) & 3, tl = (tinf_l >> 14) & 1, te = tw_eu(tinf_l);
+      tp[4 * lane + 0] = captured(x, te, [&](const TdDevCfg& c) { return c.t_rge[tt][tl]; });
+      tp[4 * lane + 1] = captured(x, te, [&](const TdDevCfg& c) { return c.t_intv[tt][tl]; });
+      tp[4 * lane + 2] = captured(x, te, [&](const TdDevCfg& c) { return c.t_atk[tt][tl]; });
+      tp[4 * lane + 3] = captured(x, te, [&](const TdDevCfg& c) { return c.t_dmg[tt][tl]; });
+    }
+    wsync();
     for (int k = 0; k < u.nt; ++k) {
       double cd = dsub(rdl(tcd, k), 1.0);                    // :307
       if (!(cd > 0.0)) {
         const uint32_t ti = rdl(tinf_l, k);
-        const int tt = (ti >> 12) & 3, tl = (ti >> 14) & 1, tc = ti & 0xfff, te = tw_eu(ti);
-        const double rge = captured(x, te, [&](const TdDevCfg& c) { return c.t_rge[tt][tl]; });
+        const int tt = (ti >> 12) & 3, tc = ti & 0xfff;
+        const double rge = tp[4 * k];
         bool in0 = val[0] && (double)cheb(en_cell(inf[0]), tc, L) <= rge;
         bool in1 = val[1] && (double)cheb(en_cell(inf[1]), tc, L) <= rge;
         uint64_t m0 = ballot(in0), m1 = ballot(in1);
         if (m0 | m1) {
           const int tgt = m0 ? ctz64(m0) : 64 + ctz64(m1);
-          cd = dadd(cd, captured(x, te, [&](const TdDevCfg& c) { return c.t_intv[tt][tl]; }));  // cd += intv
-          const double atk = captured(x, te, [&](const TdDevCfg& c) { return c.t_atk[tt][tl]; });
+          cd = dadd(cd, tp[4 * k + 1]);  // cd += intv
+          const double atk = tp[4 * k + 2];
           if (tt <= 1) {  // TowerArrow / TowerMagic (TDElements.py:71-93)
             if (lane == (tgt & 63)) {
               if (tgt < 64) lp[0] = damage(lp[0], atk, e_def(x, inf[0]), tt == 1);
@@ -619,7 +655,7 @@ __device__ __forceinline__ double board_step(Smem<NC>& S, U& u, const Ctx& x, co
           } else {
             const uint32_t tinf = (tgt >> 6) ? rdl(inf[1], tgt & 63) : rdl(inf[0], tgt & 63);
             const int tgc = en_cell(tinf);
-            const double dr = captured(x, te, [&](const TdDevCfg& c) { return c.t_dmg[tt][tl]; });
+            const double dr = tp[4 * k + 3];
             if (tt == 2) {  // TowerBomb splash (:95-110)
 #pragma unroll
               for (int s = 0; s < 2; ++s)
@@ -700,14 +736,19 @@ __device__ __forceinline__ double board_step(Smem<NC>& S, U& u, const Ctx& x, co
   u.cost_atk = pymin(dadd(u.cost_atk, rate), u.max_cost);  // self.max_cost (:352-353)
   u.cost_def = pymin(dadd(u.cost_def, C.def_rate), u.max_cost);
   wsync();
-  // the enemy list is final for this step: write it back now (its LDS is reused by the stats)
+  return reward;  // the caller writes the enemy list back (store_enemies)
+}
+
+// The enemy list after board_step from slot i0 on, back to HBM (before enemy_stats
+// reuses its LDS).
+template <int NC>
+__device__ __forceinline__ void store_enemies(const Smem<NC>& S, const U& u, const Ctx& x, const StepArgs& a, int b, int i0) {
   const size_t eb = (size_t)b * ECAP;
-  for (int i = lane; i < n2; i += 64) {
+  for (int i = i0 + x.lane; i < u.n; i += 64) {
     sst(&a.en_lp[eb + i], S.eLP[i]);
     sst(&a.en_mg[eb + i], S.eMg[i]);
     sst(&a.en_inf[eb + i], S.eInf[i]);
   }
-  return reward;
 }
 
 // enemy_LP planes (TDBoard.py:355-365): per (type, cell) min / max / sum in list
@@ -1517,6 +1558,16 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
 
   // ---- TDBoard.step
   double reward = board_step(S, u, x, a, b);
+  // The next step's opponent words, loaded since the attacker phase, are consumed here,
+  // before this step's state stores: gfx950 counts loads and stores in one vmcnt, so
+  // after the stores the wait for these loads became a wait for every store's
+  // acknowledgement (s_waitcnt vmcnt(0)) -- under the observation stream of the
+  // other waves, one of the longest stalls of the step.
+#ifdef TD_AB_EARLY_STORES
+  if (MODE != MODE_2P) R.prefetch_finish(x.lane, true);
+#else
+  if (MODE != MODE_2P) R.prefetch_finish(x.lane, false);
+#endif
   if (MODE == MODE_ATK) reward = -reward;                   // TDAttack.py:50
   const bool done = (u.base_LP <= 0) || (u.steps >= C.max_episode_steps);  // :384-385
   u.ep_ret = dadd(u.ep_ret, reward);
@@ -1555,6 +1606,21 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
       u.flags |= FLAG_NO_LAYOUT;  // 65 failing draws in a row (the reference raises): the board keeps its finished episode
     }
   }
+  // The enemy list goes back to HBM with the other state stores at the end of the step
+  // (see prefetch_finish): slots 0-63 wait in registers while enemy_stats reuses their
+  // LDS; a list longer than 64 (rare) stores its tail now.  A reset board has none.
+  // (TD-atk and the two-wave 20x20 kernel have no registers to spare for them: they
+  // store now.)
+#ifdef TD_AB_EARLY_STORES  // A/B builds: enemy list and opponent words stored where they are final
+  constexpr bool kEnDefer = false;
+#else
+  constexpr bool kEnDefer = MODE != MODE_ATK && !(SPLIT && LT == 20);
+#endif
+  const int n_keep = !kEnDefer ? 0 : u.n < 64 ? u.n : 64;
+  const bool ekeep = x.lane < n_keep;
+  const double e_lp = ekeep ? S.eLP[x.lane] : 0.0, e_mg = ekeep ? S.eMg[x.lane] : 0.0;
+  const uint32_t e_inf = ekeep ? S.eInf[x.lane] : 0u;
+  if (u.n > n_keep) store_enemies(S, u, x, a, b, n_keep);
   STAMP(5);
   enemy_stats(S, u, x);  // no-op for a board without enemies (e.g. just reset)
   STAMP(13);
@@ -1565,8 +1631,16 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
     pack_obs_cells(S, x);
   }
   store_board(S, u, x, a, b);
+  if (ekeep) {
+    const size_t eb = (size_t)b * ECAP + x.lane;
+    sst(&a.en_lp[eb], e_lp);
+    sst(&a.en_mg[eb], e_mg);
+    sst(&a.en_inf[eb], e_inf);
+  }
+#ifndef TD_AB_EARLY_STORES
+  if (MODE != MODE_2P) R.prefetch_store(x.lane);
+#endif
 
-  if (MODE != MODE_2P) R.prefetch_finish(x.lane);
   if (x.lane == 0) {
     if (was_reset)  // the record has been read into LDS: its slot may be redrawn
       st_relaxed(a.lay_head + b, lay_head + 1u);
@@ -2051,14 +2125,29 @@ __global__ __launch_bounds__(64) void td_autoreset_kernel(StepArgs a) {
 
 // Keep every board's ring of staged layouts full: lanes check G boards at once
 // (layouts drawn minus consumed < NSLOT), then the wave draws the missing layouts
-// of those boards one by one with the whole-wave generator (WaveRoadGen).  Runs on a
-// side stream concurrently with the step grids; the step stream never waits for it.
+// of those boards one by one with the whole-wave generator (WaveRoadGen).
+//
+// guard = 0 (refill): runs on a side stream concurrently with the step grids, which
+// never wait for it; a board another refill holds is skipped, and a draw gets at most
+// a.refill_walks walks unless the ring is empty.
+//
+// guard = G > 0 (ring guard): runs ON the step stream, between two steps, before every
+// G-th step (td_capi.hip td_step): every ring holding fewer than G complete layouts is
+// filled to G -- draws run to the end, a board a side refill holds is waited for (its
+// wave is resident and gives the claim back after its walk budget).  A board consumes
+// at most one layout per step, so none of the next G steps finds its ring empty: an
+// episode end never depends on the refill cadence (TDGymBasic.py:37-55 resets at every
+// end).  The one exception is the reference's own failure, 65 failing draws in a row
+// (it raises): the ring stays short and the step flags the board no_layout.  Rings
+// below G are rare when the side refills keep up (a board would have to finish
+// NSLOT - G + 1 episodes between two refills), so a guard launch is mostly a scan.
 template <int LT>
-__global__ __launch_bounds__(64) void td_refill_kernel(StepArgs a) {
+__global__ __launch_bounds__(64) void td_refill_kernel(StepArgs a, int guard) {
   constexpr int NC = LT ? LT * LT : MAX_KERNEL_L * MAX_KERNEL_L;
   __shared__ LayoutSmem<NC> G;
   const int lane = (int)threadIdx.x;
   const int grp = a.refill_grp;
+  const uint32_t level = guard ? (uint32_t)guard : (uint32_t)NSLOT;  // layouts wanted per ring
   for (int base = (int)blockIdx.x * grp; base < a.B; base += (int)gridDim.x * grp) {
     const int b = base + lane;
     const bool mine = lane < grp && b < a.B;
@@ -2067,20 +2156,24 @@ __global__ __launch_bounds__(64) void td_refill_kernel(StepArgs a) {
       head = ld_relaxed(a.lay_head + b);  // a step grid may be advancing it right now
       tail = ld_relaxed(a.lay_tail + b);
     }
-    uint64_t m = ballot(mine && tail - head < (uint32_t)NSLOT);
+    uint64_t m = ballot(mine && tail - head < level);
     while (m) {
       const int l = ctz64(m);
       m &= m - 1;
       const int bb = base + l;
-      if (!claim_board(a.lay_claim + bb, lane)) continue;  // another refill is drawing its layouts
+      if (!claim_board(a.lay_claim + bb, lane)) {  // another refill is drawing its layouts
+        if (!guard) continue;
+        do __builtin_amdgcn_s_sleep(8);
+        while (!claim_board(a.lay_claim + bb, lane));
+      }
       uint32_t t = ld_relaxed(a.lay_tail + bb);
       const uint32_t h = ld_relaxed(a.lay_head + bb);
 #pragma nounroll
-      while (t - h < (uint32_t)NSLOT) {
+      while (t - h < level) {
         uint32_t* slot = a.nxt + ((size_t)bb * NSLOT + t % NSLOT) * a.slot_words;
         // an empty ring is urgent (the board needs this layout at its next episode end):
         // its draw runs to the end; otherwise at most a.refill_walks walks this launch
-        const int st = wave_layout(G, a, bb, kLayoutRetries, slot, t, t == h ? 0x7fffffff : a.refill_walks);
+        const int st = wave_layout(G, a, bb, kLayoutRetries, slot, t, t == h || guard ? 0x7fffffff : a.refill_walks);
         __syncthreads();
         if (st != ROAD_OK) break;  // out of walks (continued next launch), or 65 failing draws in a row
         ++t;
@@ -2214,20 +2307,22 @@ hipError_t launch_autoreset(const StepArgs& a, hipStream_t s) {
 }
 
 template <int LT>
-static void launch_refill2(const StepArgs& a, hipStream_t s) {
+static void launch_refill2(const StepArgs& a_, hipStream_t s, int guard) {
+  StepArgs a = a_;
+  if (guard) a.refill_grp = 64;  // the guard mostly scans: one ballot of 64 boards per wave, one wave per 64 boards
   const int grp = a.refill_grp;
   const int groups = (a.B + grp - 1) / grp;  // a wave walks the groups grid-stride
-  const int waves = groups < a.refill_waves ? groups : a.refill_waves;
-  hipLaunchKernelGGL(td_refill_kernel<LT>, dim3(waves), dim3(64), 0, s, a);
+  const int waves = guard || groups < a.refill_waves ? groups : a.refill_waves;
+  hipLaunchKernelGGL(td_refill_kernel<LT>, dim3(waves), dim3(64), 0, s, a, guard);
 }
 
-hipError_t launch_refill(const StepArgs& a, hipStream_t s) {
+hipError_t launch_refill(const StepArgs& a, hipStream_t s, int guard) {
   switch (a.L) {
-    case 10: launch_refill2<10>(a, s); break;
+    case 10: launch_refill2<10>(a, s, guard); break;
 #ifndef TD_L10_ONLY  // diagnostic register-usage compiles (scripts/kernel_resources.sh)
-    case 20: launch_refill2<20>(a, s); break;
-    case 30: launch_refill2<30>(a, s); break;
-    default: launch_refill2<0>(a, s); break;
+    case 20: launch_refill2<20>(a, s, guard); break;
+    case 30: launch_refill2<30>(a, s, guard); break;
+    default: launch_refill2<0>(a, s, guard); break;
 #else
     default: break;
 #endif

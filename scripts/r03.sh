@@ -122,6 +122,56 @@ s11) # the round's build: GPU suite, every workload line, refill cost at the sma
   run large16k 300 python bench.py --workload def-large --global-batch 16384 --no-cpu-baseline --steps 300 || exit 1; line large16k
   run large 300 python bench.py --workload def-large --no-cpu-baseline --steps 100 || exit 1; line large
   ;;
+s12) # the ring guard: auto-reset under load with refills off on every kernel, then its cost (guard off = A/B only)
+  run pytest_gpu 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -p no:cacheprovider
+  rc=$?; grep -E "under_load|FAIL|^E  " $O/pytest_gpu.log | head -30; tail -1 $O/pytest_gpu.log; [ $rc -le 1 ] || exit $rc
+  for r in 1 2; do for g in 0 4; do for bb in 65536 8192 4096; do
+    TD_GUARD_EVERY=$g run g${g}_${bb}_$r 200 python bench.py --global-batch $bb --no-cpu-baseline --steps $((bb > 10000 ? 500 : 3000)) || exit 1; line g${g}_${bb}_$r
+  done; done; done
+  ;;
+s13) # the ring guard at G = 3 (rings below 3 only): under-load tests, then its cost against guard off
+  run pytest_load 600 python -u -m pytest tests/test_gpu_envs.py -k autoreset_under_load -v --timeout 300 --timeout-method thread -p no:cacheprovider
+  rc=$?; grep -E "PASS|FAIL|^E  " $O/pytest_load.log | head -30; [ $rc -le 1 ] || exit $rc
+  for r in 1 2; do for g in 0 3; do for bb in 65536 8192 4096; do
+    TD_GUARD_EVERY=$g run g${g}_${bb}_$r 200 python bench.py --global-batch $bb --no-cpu-baseline --steps $((bb > 10000 ? 500 : 3000)) || exit 1; line g${g}_${bb}_$r
+  done; done; done
+  for g in 0 3; do
+    TD_GUARD_EVERY=$g run g${g}_p2 300 python bench.py --workload 2p-middle-multi --no-cpu-baseline --steps 300 || exit 1; line g${g}_p2
+  done
+  ;;
+s14) # rings of 16, guard every 15th step: the GPU suite, then guard / serial-refill A/Bs
+  run pytest_gpu 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -p no:cacheprovider
+  rc=$?; grep -E "under_load|FAIL|^E  " $O/pytest_gpu.log | head -30; tail -1 $O/pytest_gpu.log; [ $rc -le 1 ] || exit $rc
+  for r in 1 2; do for v in prod noguard serial serial12; do for bb in 65536 8192 4096; do
+    case $v in prod) E="";; noguard) E="TD_GUARD_EVERY=0";; serial) E="TD_REFILL_SERIAL=1";; serial12) E="TD_REFILL_SERIAL=1 TD_REFILL_WALKS=12";; esac
+    env $E true; export $E 2>/dev/null
+    run ${v}_${bb}_$r 200 python bench.py --global-batch $bb --no-cpu-baseline --steps $((bb > 10000 ? 500 : 3000)) || exit 1; line ${v}_${bb}_$r
+    unset TD_GUARD_EVERY TD_REFILL_SERIAL TD_REFILL_WALKS
+  done; done; done
+  ;;
+s15) # state stores deferred to the end of the step, no flat loads: GPU suite, every workload line, refills off as the bound
+  run pytest_gpu 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread -p no:cacheprovider
+  rc=$?; grep -E "^(FAILED|E  )" $O/pytest_gpu.log | head -30; tail -1 $O/pytest_gpu.log; [ $rc -le 1 ] || exit $rc
+  for r in 1 2; do for bb in 65536 32768 16384 8192 4096; do
+    run b${bb}_$r 200 python bench.py --global-batch $bb --no-cpu-baseline --steps $((bb > 10000 ? 500 : 3000)) || exit 1; line b${bb}_$r
+  done; done
+  for bb in 8192 4096; do
+    run b${bb}_norefill 200 python bench.py --global-batch $bb --no-cpu-baseline --steps 3000 --refill-interval 0 || exit 1; line b${bb}_norefill
+  done
+  run p2 300 python bench.py --workload 2p-middle-multi --no-cpu-baseline --steps 500 || exit 1; line p2
+  run large16k 300 python bench.py --workload def-large --global-batch 16384 --no-cpu-baseline --steps 300 || exit 1; line large16k
+  ;;
+s16) # A/B on one box: state stores at the step's end + no flat loads (product) vs stores where final + flat (early)
+  for r in 1 2 3; do for v in prod early; do for bb in 65536 8192 4096; do
+    L=$PWD/gym-td_amd/lib/libtdstep.so; [ $v = early ] && L=$PWD/gym-td_amd/lib/variants/libtdstep_early.so
+    TDSTEP_LIB=$L run ${v}_${bb}_$r 200 python bench.py --global-batch $bb --no-cpu-baseline --steps $((bb > 10000 ? 500 : 3000)) || exit 1; line ${v}_${bb}_$r
+  done; done; done
+  for v in prod early; do
+    L=$PWD/gym-td_amd/lib/libtdstep.so; [ $v = early ] && L=$PWD/gym-td_amd/lib/variants/libtdstep_early.so
+    TDSTEP_LIB=$L run ${v}_p2 300 python bench.py --workload 2p-middle-multi --no-cpu-baseline --steps 300 || exit 1; line ${v}_p2
+    TDSTEP_LIB=$L run ${v}_large 300 python bench.py --workload def-large --global-batch 16384 --no-cpu-baseline --steps 200 || exit 1; line ${v}_large
+  done
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "session $S rc=0"

@@ -664,9 +664,10 @@ def _obs_checksum(obs):
     return torch.stack([w.sum(1), (w * idx).sum(1)], 1)
 
 
-@pytest.mark.parametrize("B,steps,kernel", [
-    (16384, 200, "large"), (512, 1500, "small2"), (8192, 400, "small"), (4096, 300, "large")])
-def test_autoreset_under_load_matches_explicit_reset(B, steps, kernel):
+@pytest.mark.parametrize("B,steps,kernel,refill", [
+    (16384, 200, "large", 16), (512, 1500, "small2", 16), (8192, 400, "small", 16), (4096, 300, "large", 16),
+    (16384, 200, "large", 0), (8192, 400, "small", 0), (4096, 300, "small2", 0)])
+def test_autoreset_under_load_matches_explicit_reset(B, steps, kernel, refill):
     """The staged-layout rings under load: 16,384 boards with 1-LP bases and a weak
     defence finish ~250 episodes per step; 512 boards step so fast that one draw
     the reference never finishes (2-5 ms of one lane) spans hundreds of steps.
@@ -676,7 +677,9 @@ def test_autoreset_under_load_matches_explicit_reset(B, steps, kernel):
     and dones stay on the device.  Phase 2 replays the same actions on an engine
     reset explicitly (the reset kernel draws each layout on the spot, failing draws
     skipped as the refill skips them).  Every board must agree at every step, on each
-    step kernel (8,192 boards: the N = 8 share's kernel)."""
+    step kernel (8,192 boards: the N = 8 share's kernel).  refill = 0: no refill kernel at
+    all -- every layout comes from the ring guard on the step stream (td_refill_kernel,
+    guard = 1), so an episode end never depends on the refill cadence."""
     from test_gpu_parity import reference_settings
     L = 10
     ov = dict(base_LP=1, defender_init_cost=0, defender_cost_rate=0.02)
@@ -685,6 +688,7 @@ def test_autoreset_under_load_matches_explicit_reset(B, steps, kernel):
         ea = TDEngine(L, B, "def", False, 1, np_seeds=seeds, py_seeds=seeds, autoreset=True, step_kernel=kernel)
         eb = TDEngine(L, B, "def", False, 1, np_seeds=seeds, py_seeds=seeds, autoreset=False)
     try:
+        ea.set_refill_interval(refill)
         ea.reset_all()
         eb.reset_all()
         assert torch.equal(ea.obs, eb.obs)
