@@ -99,7 +99,8 @@ struct td_handle {
   // waits for them (the rings give every board NSLOT episodes of slack, and
   // per-board claims keep concurrent refills apart).
   hipStream_t side[kSideStreams] = {};
-  hipEvent_t ev_main = nullptr;
+  hipEvent_t ev_main = nullptr;  // orders a refill after a reset kernel (system-scope fence)
+  hipEvent_t ev_step = nullptr;  // orders a refill after the previous step (TD_EVENT_FENCE A/B: its fence scope)
   int next_side = 0;
   int refill_every = kRefillEvery;  // 0: no refill launches (td_set_refill_interval)
   int refill_waves = kRefillWaves;  // waves per refill launch
@@ -263,15 +264,16 @@ int drop_all_staged(td_handle* h) {
 // The refill is ordered after the work on s so far: after a reset kernel, whose
 // draws-now use the boards' numpy streams and ring slots without a claim, and after the
 // previous step (see kRefillEvery).
-int start_refill(td_handle* h, hipStream_t s) {
+int start_refill(td_handle* h, hipStream_t s, bool after_step = false) {
   const int q = h->next_side;
   StepArgs a = base_args(h);
   if (h->refill_serial) {
     HIP_OK(launch_refill(a, s));
     return 0;
   }
-  HIP_OK(hipEventRecord(h->ev_main, s));
-  HIP_OK(hipStreamWaitEvent(h->side[q], h->ev_main, 0));
+  hipEvent_t ev = after_step ? h->ev_step : h->ev_main;
+  HIP_OK(hipEventRecord(ev, s));
+  HIP_OK(hipStreamWaitEvent(h->side[q], ev, 0));
   HIP_OK(launch_refill(a, h->side[q]));
   h->next_side = (q + 1) % h->n_side;
   return 0;
@@ -419,6 +421,17 @@ td_handle* td_create(const td_config* cfg, int map_size, int n_boards, int mode,
     }
   }
   if (!rc && hipEventCreateWithFlags(&h->ev_main, hipEventDisableTiming) != hipSuccess) rc = fail("event");
+  {
+    // The step-cadence refill needs the previous step finished, not its memory fenced:
+    // everything a refill reads of a step (lay_head) and publishes (slots, tags, claims,
+    // the stream) goes through write-through / atomic accesses.  Without the event's
+    // system-scope fence (a cache writeback): -0.6 % / -0.8 % per step at 8,192 / 4,096
+    // boards (profiles/r03/s17).  TD_EVENT_FENCE (A/B runs): 0 system, 1 device-scope release.
+    unsigned fl = hipEventDisableTiming | hipEventDisableSystemFence;
+    if (const char* e = std::getenv("TD_EVENT_FENCE"))
+      fl = hipEventDisableTiming | (std::atoi(e) == 1 ? hipEventReleaseToDevice : std::atoi(e) == 2 ? hipEventDisableSystemFence : 0u);
+    if (!rc && hipEventCreateWithFlags(&h->ev_step, fl) != hipSuccess) rc = fail("event");
+  }
   if (rc) { std::string e = g_err; td_destroy(h); g_err = e; return nullptr; }
   {  // TD_KERNEL_AUTO: the small-batch kernel where the whole batch is one round of waves,
      // two waves per board up to half a round -- and again over a few rounds, where the
@@ -458,6 +471,7 @@ void td_destroy(td_handle* h) {
   for (void* p : dptrs)
     if (p) (void)hipFree(p);
   if (h->ev_main) (void)hipEventDestroy(h->ev_main);
+  if (h->ev_step) (void)hipEventDestroy(h->ev_step);
   for (hipEvent_t e : h->tev) (void)hipEventDestroy(e);
   for (int q = 0; q < kSideStreams; ++q)
     if (h->side[q]) (void)hipStreamDestroy(h->side[q]);
@@ -680,7 +694,7 @@ int td_step(td_handle* h, const td_step_io* io, void* stream) {
   // random_agent=True: layouts are staged ahead by refills on the side streams.
   // random_agent=False: they are drawn in stream order right after the step (below).
   if (h->autoreset && !h->opp_np && h->refill_every > 0 && (h->steps % h->refill_every) == 0 &&
-      start_refill(h, s))
+      start_refill(h, s, true))
     return -1;
   // the ring guard (kGuardEvery): behind the previous step, beside the refill just launched
   if (h->autoreset && !h->opp_np && h->guard_every > 0 && h->since_guard >= h->guard_every) {

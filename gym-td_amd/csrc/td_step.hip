@@ -110,21 +110,13 @@ struct Ctx {
 // A value an enemy or tower captured when it was created or upgraded (TDElements.py:
 // 4-43, 45-63, 134-170): from the block of its epoch -- the staged current one, or
 // (after a paramConfig) an older block in HBM.
-//
-// The two loads must stay two loads: merged into one load of a selected pointer (what
-// the compiler does with the plain if) they become a FLAT load -- LDS or global -- which
-// counts in vmcnt, and waiting for it waits for every store the wave has in flight
-// (s_waitcnt vmcnt(0) lgkmcnt(0)).  The empty asm on the HBM value keeps them apart.
-__device__ __forceinline__ double keep_apart(double v) {
-#ifndef TD_AB_FLAT  // A/B builds: the merged (flat) load
-  asm volatile("" : "+v"(v));
-#endif
-  return v;
-}
+// (The compiler merges the two loads into one FLAT load of a selected pointer, which
+// counts in vmcnt; keeping them apart -- an empty asm on the HBM value -- measured
+// +-0.6 % across 65,536 / 8,192 / 4,096 boards, profiles/r03/s17: not kept.)
 template <class F>
 __device__ __forceinline__ double captured(const Ctx& x, int ep, F f) {
   double v = f(x.C);
-  if (ep != x.ep) v = keep_apart(f(x.tab[ep]));
+  if (ep != x.ep) v = f(x.tab[ep]);
   return v;
 }
 
@@ -163,22 +155,16 @@ struct WaveMt {
       }
     }
   }
-  // finish(..., false) leaves the twisted words' store to prefetch_store: a store's
-  // registers may only be reused once it has completed (s_waitcnt vmcnt), so the step
-  // kernels issue it with the other state stores at the end of the step.
-  __device__ __forceinline__ void prefetch_finish(int lane, bool store = true) {
+  __device__ __forceinline__ void prefetch_finish(int lane) {
+    const uint32_t q = cbase + (uint32_t)lane;
     uint32_t y = pa;
     if (plazy) {
       const uint32_t yy = (pa & 0x80000000u) | (pnb & 0x7fffffffu);
       y = pfar ^ (yy >> 1) ^ ((yy & 1u) ? 0x9908b0dfu : 0u);
-      pa = y;
+      w[q] = y;  // after every lane's loads (data dependency)
     }
-    if (store) prefetch_store(lane);
     if (cbase + cn > tw) tw = cbase + cn;
     cache = pmine ? mt_temper(y) : 0u;
-  }
-  __device__ __forceinline__ void prefetch_store(int lane) {
-    if (plazy) w[cbase + (uint32_t)lane] = pa;  // after every lane's loads (data dependency)
   }
   __device__ __forceinline__ void prefetch(int lane) {
     prefetch_issue(lane);
@@ -739,12 +725,11 @@ __device__ __forceinline__ double board_step(Smem<NC>& S, U& u, const Ctx& x, co
   return reward;  // the caller writes the enemy list back (store_enemies)
 }
 
-// The enemy list after board_step from slot i0 on, back to HBM (before enemy_stats
-// reuses its LDS).
+// The enemy list after board_step, back to HBM (before enemy_stats reuses its LDS).
 template <int NC>
-__device__ __forceinline__ void store_enemies(const Smem<NC>& S, const U& u, const Ctx& x, const StepArgs& a, int b, int i0) {
+__device__ __forceinline__ void store_enemies(const Smem<NC>& S, const U& u, const Ctx& x, const StepArgs& a, int b) {
   const size_t eb = (size_t)b * ECAP;
-  for (int i = i0 + x.lane; i < u.n; i += 64) {
+  for (int i = x.lane; i < u.n; i += 64) {
     sst(&a.en_lp[eb + i], S.eLP[i]);
     sst(&a.en_mg[eb + i], S.eMg[i]);
     sst(&a.en_inf[eb + i], S.eInf[i]);
@@ -1561,13 +1546,10 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
   // The next step's opponent words, loaded since the attacker phase, are consumed here,
   // before this step's state stores: gfx950 counts loads and stores in one vmcnt, so
   // after the stores the wait for these loads became a wait for every store's
-  // acknowledgement (s_waitcnt vmcnt(0)) -- under the observation stream of the
-  // other waves, one of the longest stalls of the step.
-#ifdef TD_AB_EARLY_STORES
-  if (MODE != MODE_2P) R.prefetch_finish(x.lane, true);
-#else
-  if (MODE != MODE_2P) R.prefetch_finish(x.lane, false);
-#endif
+  // acknowledgement (s_waitcnt vmcnt(0)).  (Holding every state store back to the end
+  // of the step, next to the observation, measured slower: 219 vs 216 us at 65,536
+  // boards, 35.8 vs 34.9 at 8,192, profiles/r03/s16.)
+  if (MODE != MODE_2P) R.prefetch_finish(x.lane);
   if (MODE == MODE_ATK) reward = -reward;                   // TDAttack.py:50
   const bool done = (u.base_LP <= 0) || (u.steps >= C.max_episode_steps);  // :384-385
   u.ep_ret = dadd(u.ep_ret, reward);
@@ -1606,21 +1588,9 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
       u.flags |= FLAG_NO_LAYOUT;  // 65 failing draws in a row (the reference raises): the board keeps its finished episode
     }
   }
-  // The enemy list goes back to HBM with the other state stores at the end of the step
-  // (see prefetch_finish): slots 0-63 wait in registers while enemy_stats reuses their
-  // LDS; a list longer than 64 (rare) stores its tail now.  A reset board has none.
-  // (TD-atk and the two-wave 20x20 kernel have no registers to spare for them: they
-  // store now.)
-#ifdef TD_AB_EARLY_STORES  // A/B builds: enemy list and opponent words stored where they are final
-  constexpr bool kEnDefer = false;
-#else
-  constexpr bool kEnDefer = MODE != MODE_ATK && !(SPLIT && LT == 20);
-#endif
-  const int n_keep = !kEnDefer ? 0 : u.n < 64 ? u.n : 64;
-  const bool ekeep = x.lane < n_keep;
-  const double e_lp = ekeep ? S.eLP[x.lane] : 0.0, e_mg = ekeep ? S.eMg[x.lane] : 0.0;
-  const uint32_t e_inf = ekeep ? S.eInf[x.lane] : 0u;
-  if (u.n > n_keep) store_enemies(S, u, x, a, b, n_keep);
+  // The enemy list back to HBM (after the layout poll's loads, whose wait would
+  // otherwise wait for these stores too; a reset board has none).
+  store_enemies(S, u, x, a, b);
   STAMP(5);
   enemy_stats(S, u, x);  // no-op for a board without enemies (e.g. just reset)
   STAMP(13);
@@ -1631,15 +1601,6 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
     pack_obs_cells(S, x);
   }
   store_board(S, u, x, a, b);
-  if (ekeep) {
-    const size_t eb = (size_t)b * ECAP + x.lane;
-    sst(&a.en_lp[eb], e_lp);
-    sst(&a.en_mg[eb], e_mg);
-    sst(&a.en_inf[eb], e_inf);
-  }
-#ifndef TD_AB_EARLY_STORES
-  if (MODE != MODE_2P) R.prefetch_store(x.lane);
-#endif
 
   if (x.lane == 0) {
     if (was_reset)  // the record has been read into LDS: its slot may be redrawn

@@ -172,6 +172,35 @@ s16) # A/B on one box: state stores at the step's end + no flat loads (product) 
     TDSTEP_LIB=$L run ${v}_large 300 python bench.py --workload def-large --global-batch 16384 --no-cpu-baseline --steps 200 || exit 1; line ${v}_large
   done
   ;;
+s17) # A/B on one box: no flat loads (product) vs merged flat loads; step-refill event fence scope
+  P=$PWD/gym-td_amd/lib/libtdstep.so; F=$PWD/gym-td_amd/lib/variants/libtdstep_flat.so
+  for r in 1 2 3; do for v in prod flat; do for bb in 65536 8192 4096; do
+    L=$P; [ $v = flat ] && L=$F
+    TDSTEP_LIB=$L run ${v}_${bb}_$r 200 python bench.py --global-batch $bb --no-cpu-baseline --steps $((bb > 10000 ? 500 : 3000)) || exit 1; line ${v}_${bb}_$r
+  done; done; done
+  for r in 1 2; do for fe in 0 1 2; do for bb in 8192 4096; do
+    TD_EVENT_FENCE=$fe run fence${fe}_${bb}_$r 200 python bench.py --global-batch $bb --no-cpu-baseline --steps 3000 || exit 1; line fence${fe}_${bb}_$r
+  done; done; done
+  ;;
+s18|s19) # the round's build: GPU suite, smoke, default line; kernel traces + PMC per workload (summaries on the box)
+  if [ $S = s18 ]; then
+    run pytest_gpu 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread -p no:cacheprovider
+    rc=$?; grep -E "^(FAILED|E  )" $O/pytest_gpu.log | head -30; tail -1 $O/pytest_gpu.log; [ $rc -le 1 ] || exit $rc
+    run smoke 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" || exit 1
+    run bench_default 300 python bench.py || exit 1
+    grep '^{' $O/bench_default.log; line bench_default
+    WLS="def-small:65536 def-small:8192 def-small:4096"
+  else
+    WLS="2p-middle-multi:16384 def-large:16384"
+  fi
+  for wb in $WLS; do
+    wl=${wb%%:*}; bb=${wb##*:}
+    NO_PHASES=1 PROF_DIR=$O/prof_${wl}_$bb WL=$wl B=$bb run prof_${wl}_$bb 900 bash scripts/profile_session.sh || exit 1
+    PMC_PROF=$O/prof_${wl}_$bb PMC_OUT=$O run sum_${wl}_$bb 120 python scripts/pmc_summary.py r03 $bb $wl || exit 1
+    cat $O/sum_${wl}_$bb.log | tail -2
+    rm -rf $O/prof_${wl}_$bb/pmc_* $O/prof_${wl}_$bb/kt/*_trace.csv
+  done
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "session $S rc=0"
