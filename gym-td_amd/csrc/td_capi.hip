@@ -222,6 +222,8 @@ void parallel_for(int n, F fn) {
 void apply_kernel(td_handle* h, int small) {
   h->small = small;
   const double obs_bytes = (double)h->B * NCH * h->NC * 4.0;
+  // (Write-through beyond the Infinity Cache -- any kernel, TD_OBS_WT=1 -- measured 1.5-1.7x
+  // slower steps at 16,384-65,536 boards, profiles/r03/s21.)
   h->obs_wt = h->small && obs_bytes <= 192.0 * 1024 * 1024 ? 1 : 0;
   if (const char* e = std::getenv("TD_OBS_WT")) h->obs_wt = std::atoi(e) ? 1 : 0;  // A/B runs
   const bool has_small = h->L == 10 || h->L == 20 || h->L == 30;

@@ -75,6 +75,7 @@ struct alignas(16) Smem {
     };
   };
   uint32_t obs_go, obs_any;  // td_step_kernel_small2: the stepping wave tells the second one to write
+  uint32_t early_go;         // td_step_kernel_small2: the binary-plane windows may be written early
   TdDevCfg cfg;           // constant block, staged once per board: per-lane table lookups hit LDS
 };
 
@@ -1009,7 +1010,11 @@ struct ObsWinTab {
 // batch's observation fits the 256-MiB Infinity Cache (scripts/storepol.hip at 8,192
 // boards, 147 MB: 21.8 us sc1, 30.0 us nt; at 65,536 boards, 1.18 GB, nt whole lines
 // are the fastest form, with the two lines shared with the neighbours sc1).
-template <int NC, int LT, int KB = 0, int KE = -1, int G = 4>
+//
+// PASS: 0 every window; 1 only the windows of binary planes alone (ObsWinTab class 0:
+// roads, end, starts, buildable, tower level / type -- final once the step's actions
+// are, td_step_kernel_small2 writes them early); 2 every other window.
+template <int NC, int LT, int KB = 0, int KE = -1, int G = 4, int PASS = 0>
 __device__ __forceinline__ void write_obs_lines(const Smem<NC>& S, int lane, float* out, bool any_enemy, bool wt) {
   static_assert(LT >= 8, "a 128-B line spans at most two channel planes");
   constexpr int Q = LT * LT / 4, N4 = NCH * Q;
@@ -1041,6 +1046,7 @@ __device__ __forceinline__ void write_obs_lines(const Smem<NC>& S, int lane, flo
       const int k = k0 + j;
       if ((K - KB) % G == 0 || k < K) {
         const uint32_t wc = wclass(k);
+        if (PASS != 0 && (((wc & 3u) == 0) != (PASS == 1))) continue;  // wave-uniform
         const int i = unit(i0 + 64 * k, wc);
         const int ch = i / Q, q = i - ch * Q;
         A[j] = *reinterpret_cast<const uint4*>(sb + o_cell + 16 * q);
@@ -1063,6 +1069,7 @@ __device__ __forceinline__ void write_obs_lines(const Smem<NC>& S, int lane, flo
       const int k = k0 + j;
       if (!((K - KB) % G == 0 || k < K)) continue;
       const uint32_t wc = wclass(k);
+      if (PASS != 0 && (((wc & 3u) == 0) != (PASS == 1))) continue;
       const bool edge = (wc & 4u) != 0;  // the window holds a line shared with a neighbour
       const int i = i0 + 64 * k;
       const int ch = unit(i, wc) / Q;
@@ -1453,6 +1460,21 @@ __device__ __forceinline__ bool take_dry_ring(const StepArgs& a, int b, uint32_t
 // Observation windows written by the stepping wave of a two-wave board (the first half).
 template <int LT>
 __host__ __device__ constexpr int obs_half() { return ((NCH * LT * LT / 4 + 7 + 63) / 64 + 1) / 2; }
+// After the second wave's early pass over the binary-plane windows: the first window of
+// the second wave's share of the rest, so both waves write half of the remaining
+// windows (counted at a line-aligned board; ObsWinTab class != 0).
+template <int LT>
+constexpr int obs_late_half() {
+  constexpr int K = (NCH * LT * LT / 4 + 7 + 63) / 64;
+  int late = 0;
+  for (int k = 0; k < K; ++k) late += (ObsWinTab<LT>::cls(0, k) & 3u) != 0u;
+  int seen = 0;
+  for (int k = 0; k < K; ++k) {
+    if (2 * seen >= late) return k;
+    seen += (ObsWinTab<LT>::cls(0, k) & 3u) != 0u;
+  }
+  return K;
+}
 
 // SPLIT: the board's workgroup has a second wave (td_step_kernel_small2) that waits at
 // the one workgroup barrier of this path and then writes the second half of the
@@ -1487,13 +1509,14 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
       if (a.win) a.win[b] = -1;
     }
     if constexpr (SPLIT) {
-      if (x.lane == 0) S.obs_go = 0u;
-      __syncthreads();
+      if (x.lane == 0) { S.early_go = 0u; S.obs_go = 0u; }
+      __syncthreads();  // (A)
+      __syncthreads();  // (B)
     }
     return;
   }
   float* const obs = a.obs + (size_t)b * NCH * x.NCr;
-  const bool wt = SMALL && a.obs_wt;
+  const bool wt = a.obs_wt != 0;
 
   u.atk_cd = u.atk_cd - 1 > 0 ? u.atk_cd - 1 : 0;
   u.def_cd = u.def_cd - 1 > 0 ? u.def_cd - 1 : 0;
@@ -1539,6 +1562,10 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
   // pre-draw the next step's words: loads issued now, consumed at the end of the step
   if (MODE != MODE_2P) R.prefetch_issue(x.lane);
   wsync();
+  if constexpr (SPLIT) {  // (A): the second wave writes the binary-plane windows while this one steps
+    if (x.lane == 0) S.early_go = 1u;
+    __syncthreads();
+  }
   STAMP(2);
 
   // ---- TDBoard.step
@@ -1633,9 +1660,13 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
   // the observation last: nothing of the step is live any more, the writer has the registers
   STAMP(6);
   if constexpr (SPLIT) {
-    if (x.lane == 0) { S.obs_go = 1u; S.obs_any = u.n > 0 ? 1u : 0u; }
-    __syncthreads();  // the second wave writes windows [KH, K)
-    write_obs_lines<NC, LT, 0, obs_half<LT>()>(S, x.lane, obs, u.n > 0, wt);
+    // (B) the second wave's early pass has landed.  A board that auto-reset this step has
+    // a new layout: this wave rewrites every window (rare); otherwise each wave writes
+    // half of the windows the early pass left.
+    if (x.lane == 0) { S.obs_go = was_reset ? 2u : 1u; S.obs_any = u.n > 0 ? 1u : 0u; }
+    __syncthreads();
+    if (was_reset) write_obs_lines<NC, LT>(S, x.lane, obs, u.n > 0, wt);
+    else write_obs_lines<NC, LT, 0, obs_late_half<LT>(), 4, 2>(S, x.lane, obs, u.n > 0, wt);
   } else if constexpr (LT != 0) {
     if ((reinterpret_cast<uintptr_t>(a.obs) & 15u) == 0) {
 #ifndef TD_DIAG_NO_OBS  // diagnostic builds only: the step without its observation
@@ -1751,9 +1782,16 @@ __global__ __launch_bounds__(128) TD_SMALL2_ATTR void td_step_kernel_small2(Step
     prefetch_issue<PF_SMALL, PF_SMALL>(P, a, b, lane, NC, MODE != MODE_ATK && !a.multi);
     step_board<NC, LT, MODE, SCAN, true, true>(S, x, a, b, P);
   } else {
-    __syncthreads();
-    if (S.obs_go)
-      write_obs_lines<NC, LT, obs_half<LT>()>(S, lane, a.obs + (size_t)b * NCH * NC, S.obs_any != 0u, a.obs_wt != 0);
+    float* const obs = a.obs + (size_t)b * NCH * NC;
+    __syncthreads();  // (A) actions and towers final, cells packed
+    if (S.early_go) {
+      write_obs_lines<NC, LT, 0, -1, 4, 1>(S, lane, obs, false, a.obs_wt != 0);
+      // landed before (B): after an auto-reset the first wave rewrites these windows
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();  // (B)
+    if (S.obs_go == 1u)
+      write_obs_lines<NC, LT, obs_late_half<LT>(), -1, 4, 2>(S, lane, obs, S.obs_any != 0u, a.obs_wt != 0);
   }
 }
 

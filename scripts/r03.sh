@@ -201,6 +201,26 @@ s18|s19) # the round's build: GPU suite, smoke, default line; kernel traces + PM
     rm -rf $O/prof_${wl}_$bb/pmc_* $O/prof_${wl}_$bb/kt/*_trace.csv
   done
   ;;
+s20) # two-wave kernel: binary-plane windows written early by the second wave; parity on small2, then A/B vs the previous build
+  run pytest_s2 600 python -u -m pytest tests -m gpu -q -k "small2 or 4096 or rollout" --timeout 300 --timeout-method thread -p no:cacheprovider
+  rc=$?; grep -E "^(FAILED|E  )" $O/pytest_s2.log | head -30; tail -1 $O/pytest_s2.log; [ $rc -le 1 ] || exit $rc
+  P=$PWD/gym-td_amd/lib/libtdstep.so; B0=$PWD/gym-td_amd/lib/variants/libtdstep_base.so
+  for r in 1 2 3; do for v in prod base; do for wb in def-small:4096 def-small:16384 def-large:16384; do
+    wl=${wb%%:*}; bb=${wb##*:}; L=$P; [ $v = base ] && L=$B0
+    st=3000; [ $bb -gt 10000 ] && st=1000; [ $wl = def-large ] && st=200
+    TDSTEP_LIB=$L run ${v}_${wl}_${bb}_$r 300 python bench.py --workload $wl --global-batch $bb --no-cpu-baseline --steps $st || exit 1; line ${v}_${wl}_${bb}_$r
+  done; done; done
+  ;;
+s21) # observation stores write-through (sc1) vs non-temporal by batch (scripts/write_ceiling: sc1 6.7-6.9 TB/s up to 302 MB)
+  for r in 1 2; do for wt in 0 1; do for bb in 65536 32768 16384 8192 4096; do
+    st=3000; [ $bb -gt 10000 ] && st=1000; [ $bb -gt 40000 ] && st=500
+    TD_OBS_WT=$wt run wt${wt}_${bb}_$r 200 python bench.py --global-batch $bb --no-cpu-baseline --steps $st || exit 1; line wt${wt}_${bb}_$r
+  done; done; done
+  for wt in 0 1; do
+    TD_OBS_WT=$wt run wt${wt}_large16k 300 python bench.py --workload def-large --global-batch 16384 --no-cpu-baseline --steps 200 || exit 1; line wt${wt}_large16k
+    TD_OBS_WT=$wt run wt${wt}_p2 300 python bench.py --workload 2p-middle-multi --no-cpu-baseline --steps 300 || exit 1; line wt${wt}_p2
+  done
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "session $S rc=0"
