@@ -221,6 +221,38 @@ s21) # observation stores write-through (sc1) vs non-temporal by batch (scripts/
     TD_OBS_WT=$wt run wt${wt}_p2 300 python bench.py --workload 2p-middle-multi --no-cpu-baseline --steps 300 || exit 1; line wt${wt}_p2
   done
   ;;
+s22) # full GPU suite on the early-window build; one- vs two-wave kernel at 8,192; phase stamps at 4,096 / 8,192
+  run pytest_gpu 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread -p no:cacheprovider
+  rc=$?; grep -E "^(FAILED|E  )" $O/pytest_gpu.log | head -30; tail -1 $O/pytest_gpu.log; [ $rc -le 1 ] || exit $rc
+  for r in 1 2; do for k in auto small2; do for bb in 8192 6144; do
+    run k${k}_${bb}_$r 200 python bench.py --global-batch $bb --no-cpu-baseline --steps 3000 --step-kernel $k || exit 1; line k${k}_${bb}_$r
+  done; done; done
+  for bb in 4096 8192; do
+    TDSTEP_LIB=$PWD/gym-td_amd/lib/libtdstep_stamps.so run phases_$bb 300 python scripts/probe_phases.py $bb 10 600 || exit 1
+    grep -v amdgpu.ids $O/phases_$bb.log | head -30
+  done
+  ;;
+s23) # refill cost on the current build: refill interval 16 (product) / 32 / 64 vs no refills and no guard (rings drain: the bound)
+  for r in 1 2; do for v in r16 r32 r64 bound; do for bb in 8192 4096 65536; do
+    st=3000; [ $bb -gt 10000 ] && st=500
+    case $v in r16) A="";; r32) A="--refill-interval 32";; r64) A="--refill-interval 64";; bound) A="--refill-interval 0";; esac
+    G=15; [ $v = bound ] && G=0
+    TD_GUARD_EVERY=$G run ${v}_${bb}_$r 200 python bench.py --global-batch $bb --no-cpu-baseline --steps $st $A || exit 1; line ${v}_${bb}_$r
+  done; done; done
+  ;;
+s24) # one-pass channel divisions (prod, refills every 64th step) vs the previous build at the same interval; longer intervals
+  P=$PWD/gym-td_amd/lib/libtdstep.so; B0=$PWD/gym-td_amd/lib/variants/libtdstep_base.so
+  for r in 1 2 3; do for v in prod base; do for bb in 8192 4096 65536; do
+    st=3000; [ $bb -gt 10000 ] && st=500
+    L=$P; [ $v = base ] && L=$B0
+    TDSTEP_LIB=$L run ${v}_${bb}_$r 200 python bench.py --global-batch $bb --no-cpu-baseline --steps $st --refill-interval 64 || exit 1; line ${v}_${bb}_$r
+  done; done; done
+  for r in 1 2; do for ri in 128 256; do for bb in 8192 4096; do
+    run r${ri}_${bb}_$r 200 python bench.py --global-batch $bb --no-cpu-baseline --steps 3000 --refill-interval $ri || exit 1; line r${ri}_${bb}_$r
+  done; done; done
+  run pytest_load 600 python -u -m pytest tests/test_gpu_envs.py -k "autoreset_under_load" -q --timeout 300 --timeout-method thread -p no:cacheprovider
+  rc=$?; tail -1 $O/pytest_load.log; [ $rc -le 1 ] || exit $rc
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "session $S rc=0"
