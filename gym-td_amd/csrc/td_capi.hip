@@ -51,7 +51,11 @@ int fail(const char* fmt, ...) {
 // refills left unordered between steps ran 4-8 % faster at 4,096 / 8,192 boards, but a
 // step that finds a ring empty then has no refill beside it to wait for: under load a
 // board missed its layout (test_autoreset_under_load, profiles/r02/s43_unordered).
-constexpr int kRefillEvery = 16;
+// With rings of 16 and the ring guard, every 64th step: 34.3 / 21.5 us per step at
+// 8,192 / 4,096 boards vs 34.8 / 22.2-22.75 at every 16th, +-0 at 65,536; no refill and
+// no guard at all (rings draining, not a product setting): 33.1-33.8 / 20.0
+// (profiles/r03/s23).
+constexpr int kRefillEvery = 64;
 constexpr int kRefillWaves = 1024;
 // A pending draw advances 3 walks per step of refill interval (48 per launch at 16): the
 // fewer walks a refill wave runs per launch, the less it holds a wave slot the next

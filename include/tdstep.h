@@ -184,11 +184,11 @@ int td_step_kernel(td_handle* h);
 const char* td_step_kernel_name(td_handle* h);
 
 /* Steps between launches of the layout refill kernel on the side streams (auto-reset;
- * default 16, 0 = none).  A pure performance knob: before every 3rd step (and the first
+ * default 64, 0 = none).  A pure performance knob: before every 15th step (and the first
  * step after a reset) the ring guard runs on the step stream and brings every board's
- * ring of staged layouts to at least 3, so an episode end always finds its next layout,
- * whatever the interval.  The only board that misses one is a board whose draws fail
- * 65 times in a row (where the reference raises): it is flagged no_layout. */
+ * ring of 16 staged layouts to at least 15, so an episode end always finds its next
+ * layout, whatever the interval.  The only board that misses one is a board whose draws
+ * fail 65 times in a row (where the reference raises): it is flagged no_layout. */
 int td_set_refill_interval(td_handle* h, int steps);
 
 /* Kernel timing: every `every`-th td_step call from now on, up to max_launches of them,
