@@ -253,6 +253,19 @@ s24) # one-pass channel divisions (prod, refills every 64th step) vs the previou
   run pytest_load 600 python -u -m pytest tests/test_gpu_envs.py -k "autoreset_under_load" -q --timeout 300 --timeout-method thread -p no:cacheprovider
   rc=$?; tail -1 $O/pytest_load.log; [ $rc -le 1 ] || exit $rc
   ;;
+s25) # serial refills (step stream, no concurrency) at long intervals vs side refills every 64th step
+  for r in 1 2; do for v in side64 ser256 ser1024; do for bb in 4096 8192; do
+    case $v in side64) E=""; A="";; ser256) E="TD_REFILL_SERIAL=1"; A="--refill-interval 256";; ser1024) E="TD_REFILL_SERIAL=1"; A="--refill-interval 1024";; esac
+    env $E timeout -k 10 200 python bench.py --global-batch $bb --no-cpu-baseline --steps 3000 $A > $O/${v}_${bb}_$r.log 2>&1 || { tail $O/${v}_${bb}_$r.log; exit 1; }; line ${v}_${bb}_$r
+  done; done; done
+  ;;
+s26) # the device road generator's time per draw (one wave per SIMD), kernel trace
+  for bb in 256 1024; do
+    run draw_$bb 200 python scripts/probe_draw.py $bb 10 || exit 1; grep "^B=" $O/draw_$bb.log
+    run kt_draw_$bb 200 rocprofv3 --kernel-trace --stats -d $O/kt_draw_$bb -o kt --output-format csv -- python scripts/probe_draw.py $bb 10 || exit 1
+    cut -c1-150 $O/kt_draw_$bb/kt_kernel_stats.csv | head -6
+  done
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "session $S rc=0"
