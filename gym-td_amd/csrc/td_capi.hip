@@ -190,6 +190,9 @@ int dalloc(T** p, size_t n) {
 StepArgs base_args(td_handle* h) {
   StepArgs a;
   std::memset(&a, 0, sizeof a);
+#ifdef TD_GEN_STAMPS  // diagnostic builds: the reset / refill kernels' draws count their cycles
+  a.stamps = h->d_stamps;
+#endif
   a.B = h->B; a.L = h->L; a.mode = h->mode; a.multi = h->multi; a.difficulty = h->difficulty;
   a.autoreset = h->autoreset;
   a.opp_np = h->opp_np;
@@ -899,7 +902,7 @@ int td_get_flags(td_handle* h, int32_t* host_flags) {
   return 0;
 }
 
-#ifdef TD_STAMPS
+#if defined(TD_STAMPS) || defined(TD_GEN_STAMPS)
 // Diagnostic builds: per-board phase timestamps ([B][16] uint64, device memory).
 int td_debug_stamps(td_handle* h, uint64_t* dev) {
   if (!h) return fail("NULL handle");

@@ -1883,6 +1883,9 @@ __device__ int wave_layout(LayoutSmem<NC>& G, const StepArgs& a, int b, int retr
                            int budget) {
   const int lane = (int)threadIdx.x, L = a.L, lw = LAYOUT_HDR + L * L;
   const int sbytes = (int)road_scratch_bytes(L);
+#ifdef TD_GEN_STAMPS
+  const uint64_t wl_t0 = __builtin_amdgcn_s_memtime();
+#endif
   uint32_t* gmt = a.np_mt + (size_t)b * OPP_WORDS;
   RoadResume* ghdr = resume_hdr(a, b);
   uint8_t* gscr = a.scratch + (size_t)b * a.scratch_stride + sizeof(RoadResume);
@@ -1918,6 +1921,14 @@ __device__ int wave_layout(LayoutSmem<NC>& G, const StepArgs& a, int b, int retr
     __syncthreads();
     if (lane < nw) { g.fieldw[lane] = g.field; g.rotw[lane] = g.rot; }
     if (lane == 0) { G.mt[MT_N] = g.pos; G.mt[MT_N + 1] = g.tw; G.res = res; }
+#ifdef TD_GEN_STAMPS
+    if (a.stamps && lane == 0) {
+      uint64_t* sp = a.stamps + (size_t)b * 16;
+      for (int i = 0; i < 6; ++i) sp[i] += g.cyc[i];
+      sp[6] += __builtin_amdgcn_s_memtime() - wl_t0;  // the call so far (stream copy-in and the draw)
+      sp[7] += 1;
+    }
+#endif
   }
   __syncthreads();
   // every store below is write-through (st_relaxed = sc1): the claim release and the

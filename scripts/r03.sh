@@ -266,6 +266,12 @@ s26) # the device road generator's time per draw (one wave per SIMD), kernel tra
     cut -c1-150 $O/kt_draw_$bb/kt_kernel_stats.csv | head -6
   done
   ;;
+s27) # where the device road generator's time goes (diagnostic build)
+  for bb in 256 1024; do
+    TDSTEP_LIB=$PWD/gym-td_amd/lib/variants/libtdstep_genstamps.so run parts_$bb 200 python scripts/probe_draw_parts.py $bb 10 || exit 1
+    grep -v amdgpu.ids $O/parts_$bb.log
+  done
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "session $S rc=0"
