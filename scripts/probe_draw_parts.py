@@ -7,6 +7,7 @@ of B boards is reset (the reset kernel draws each board's first layout) and its 
 filled by one refill launch (15 more draws per board); the generator's s_memtime
 counters, summed per board: walks, the branch-loop proof, stamping, erasing, stream
 windows, and the whole wave_layout call."""
+import ctypes
 import os
 import sys
 
@@ -23,7 +24,10 @@ L = int(sys.argv[2]) if len(sys.argv) > 2 else 10
 seeds = list(range(5000, 5000 + B))
 eng = TDEngine(L, B, "def", False, 1, np_seeds=seeds, py_seeds=seeds, autoreset=True)
 st = torch.zeros((B, 16), dtype=torch.int64, device="cuda")
-_lib.lib.td_debug_stamps(eng._h, st.data_ptr())
+fn = _lib.lib.td_debug_stamps
+fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+fn.restype = ctypes.c_int
+assert fn(eng._h, st.data_ptr()) == 0
 eng.reset()
 act = torch.full((B,), 6 * L * L, dtype=torch.int64, device="cuda")
 eng.step(def_act=act)
