@@ -191,6 +191,10 @@ s18|s19) # the round's build: GPU suite, smoke, default line; kernel traces + PM
     grep '^{' $O/bench_default.log; line bench_default
     WLS="def-small:65536 def-small:8192 def-small:4096"
   else
+    export TD_BENCH_DIST_BACKEND=gloo TD_BENCH_SAME_DEVICE=1
+    run bench_n2 300 python bench.py --gpus 2 --no-cpu-baseline --steps 200 || exit 1
+    unset TD_BENCH_DIST_BACKEND TD_BENCH_SAME_DEVICE
+    grep '^{' $O/bench_n2.log; line bench_n2
     WLS="2p-middle-multi:16384 def-large:16384"
   fi
   for wb in $WLS; do
