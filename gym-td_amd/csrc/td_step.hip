@@ -547,7 +547,12 @@ __device__ __forceinline__ double e_def(const Ctx& x, uint32_t inf) {
   return captured(x, en_ep(inf), [&](const TdDevCfg& c) { return c.e_def[t][lv]; });
 }
 
-template <int NC>
+// Enemies up to which the towers target in parallel (board_step; FEW = false: never --
+// the large kernel, where it measured slower, and the two-wave 20x20 single-action
+// kernel, which has no registers to spare for it).
+constexpr int kFewEnemies = 16;
+
+template <int NC, bool FEW = true>
 __device__ __forceinline__ double board_step(Smem<NC>& S, U& u, const Ctx& x, const StepArgs& a, int b) {
   const TdDevCfg& C = x.C;
   const int L = x.L, lane = x.lane;
@@ -621,6 +626,50 @@ __device__ __forceinline__ double board_step(Smem<NC>& S, U& u, const Ctx& x, co
       tp[4 * lane + 3] = captured(x, te, [&](const TdDevCfg& c) { return c.t_dmg[tt][tl]; });
     }
     wsync();
+    if (FEW && n <= kFewEnemies) {
+      // A few enemies (most boards that have any): the towers pick their targets in
+      // parallel, lane k = tower k, each scanning the n enemies in list order; then the
+      // shots land in tower order, each enemy (lane j) taking the hits of the towers that
+      // fired, one tower after the other -- the reference's order of LP updates per enemy
+      // (:306-313), without a dependent LDS round trip per tower.
+      const bool tk = lane < u.nt;
+      const int tt = (int)((tinf_l >> 12) & 3u), tc = (int)(tinf_l & 0xfffu);
+      double cd = dsub(tcd, 1.0);                            // :307
+      const bool tries = tk && !(cd > 0.0);
+      const double rge = tries ? tp[4 * lane] : -1.0;
+      int tgt = -1;
+      for (int j = 0; j < n; ++j) {  // first enemy within range (list order)
+        const int ec = en_cell(rdl(inf[0], j));
+        if (tgt < 0 && (double)cheb(ec, tc, L) <= rge) tgt = j;
+      }
+      const int tgc = en_cell((uint32_t)__shfl((int)inf[0], tgt < 0 ? 0 : tgt));  // every lane shuffles
+      const double dr = tt >= 2 && tgt >= 0 ? tp[4 * lane + 3] : -1.0;
+      int frz = -1;  // TowerFrozen: the first enemy within splash of the target (:112-132)
+      if (tt == 3)
+        for (int j = 0; j < n; ++j) {
+          const int ec = en_cell(rdl(inf[0], j));
+          if (frz < 0 && (double)cheb(tgc, ec, L) <= dr) frz = j;
+        }
+      if (tgt >= 0) cd = dadd(cd, tp[4 * lane + 1]);         // cd += intv
+      if (tries && cd < 0.0) cd = 0.0;                       // :311-312
+      if (tk) tcd = cd;
+      const uint32_t slow = (uint32_t)C.frozen_time << 16;   // config.frozen_time, read live (:126)
+      for (uint64_t fm = ballot(tgt >= 0); fm; fm &= fm - 1) {  // the towers that fired, in order
+        const int k = ctz64(fm);
+        const int kt = (int)((rdl(tinf_l, k) >> 12) & 3u);
+        const double atk = tp[4 * k + 2];
+        if (kt <= 1) {  // TowerArrow / TowerMagic (TDElements.py:71-93)
+          if (lane == (int)rdl((uint32_t)tgt, k)) lp[0] = damage(lp[0], atk, e_def(x, inf[0]), kt == 1);
+        } else if (kt == 2) {  // TowerBomb splash (:95-110)
+          const int kc = (int)rdl((uint32_t)tgc, k);
+          if (val[0] && (double)cheb(kc, en_cell(inf[0]), L) <= tp[4 * k + 3])
+            lp[0] = damage(lp[0], atk, e_def(x, inf[0]), false);
+        } else if (lane == (int)rdl((uint32_t)frz, k)) {
+          lp[0] = damage(lp[0], atk, 0.0, true);
+          inf[0] = (inf[0] & 0xff00ffffu) | slow;
+        }
+      }
+    } else
     for (int k = 0; k < u.nt; ++k) {
       double cd = dsub(rdl(tcd, k), 1.0);                    // :307
       if (!(cd > 0.0)) {
@@ -1571,7 +1620,8 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
   STAMP(2);
 
   // ---- TDBoard.step
-  double reward = board_step(S, u, x, a, b);
+  // (parallel targeting: +1.1-1.4 % at 8,192 / 4,096 boards, -0.7 % in the large kernel at 65,536, profiles/r03/s29)
+  double reward = board_step<NC, SMALL && !(SPLIT && LT == 20 && MODE == MODE_DEF && !SCAN)>(S, u, x, a, b);
   // The next step's opponent words, loaded since the attacker phase, are consumed here,
   // before this step's state stores: gfx950 counts loads and stores in one vmcnt, so
   // after the stores the wait for these loads became a wait for every store's

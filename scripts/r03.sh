@@ -276,6 +276,20 @@ s27) # where the device road generator's time goes (diagnostic build)
     grep -v amdgpu.ids $O/parts_$bb.log
   done
   ;;
+s29) # towers targeting in parallel on boards with few enemies: GPU suite, then A/B vs the previous build
+  run pytest_gpu 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread -p no:cacheprovider
+  rc=$?; grep -E "^(FAILED|E  )" $O/pytest_gpu.log | head -30; tail -1 $O/pytest_gpu.log; [ $rc -le 1 ] || exit $rc
+  P=$PWD/gym-td_amd/lib/libtdstep.so; B0=$PWD/gym-td_amd/lib/variants/libtdstep_base.so
+  for r in 1 2 3; do for v in prod base; do for bb in 4096 8192 65536; do
+    st=3000; [ $bb -gt 10000 ] && st=500
+    L=$P; [ $v = base ] && L=$B0
+    TDSTEP_LIB=$L run ${v}_${bb}_$r 200 python bench.py --global-batch $bb --no-cpu-baseline --steps $st || exit 1; line ${v}_${bb}_$r
+  done; done; done
+  for v in prod base; do
+    L=$P; [ $v = base ] && L=$B0
+    TDSTEP_LIB=$L run ${v}_p2 300 python bench.py --workload 2p-middle-multi --no-cpu-baseline --steps 300 || exit 1; line ${v}_p2
+  done
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "session $S rc=0"
