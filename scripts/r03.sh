@@ -290,6 +290,16 @@ s29) # towers targeting in parallel on boards with few enemies: GPU suite, then 
     TDSTEP_LIB=$L run ${v}_p2 300 python bench.py --workload 2p-middle-multi --no-cpu-baseline --steps 300 || exit 1; line ${v}_p2
   done
   ;;
+s32) # the step's staged-record read: acquire + plain loads (product) vs sc1 loads without the acquire (noacq)
+  P=$PWD/gym-td_amd/lib/libtdstep.so; V=$PWD/gym-td_amd/lib/variants/libtdstep_noacq.so
+  TDSTEP_LIB=$V run pytest_load 600 python -u -m pytest tests/test_gpu_envs.py -k "autoreset_under_load" -q --timeout 300 --timeout-method thread -p no:cacheprovider
+  rc=$?; tail -1 $O/pytest_load.log; [ $rc -le 1 ] || exit $rc
+  for r in 1 2 3; do for v in prod noacq; do for bb in 4096 8192 65536; do
+    st=3000; [ $bb -gt 10000 ] && st=500
+    L=$P; [ $v = noacq ] && L=$V
+    TDSTEP_LIB=$L run ${v}_${bb}_$r 200 python bench.py --global-batch $bb --no-cpu-baseline --steps $st || exit 1; line ${v}_${bb}_$r
+  done; done; done
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "session $S rc=0"
