@@ -300,6 +300,11 @@ s32) # the step's staged-record read: acquire + plain loads (product) vs sc1 loa
     TDSTEP_LIB=$L run ${v}_${bb}_$r 200 python bench.py --global-batch $bb --no-cpu-baseline --steps $st || exit 1; line ${v}_${bb}_$r
   done; done; done
   ;;
+s33) # long steady-state runs on the final build (board flags, episode counts)
+  run long_8192 400 python bench.py --global-batch 8192 --no-cpu-baseline --steps 20000 || exit 1; line long_8192
+  run long_4096 400 python bench.py --global-batch 4096 --no-cpu-baseline --steps 20000 || exit 1; line long_4096
+  run long_65536 400 python bench.py --no-cpu-baseline --steps 3000 || exit 1; line long_65536
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "session $S rc=0"
