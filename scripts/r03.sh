@@ -305,6 +305,11 @@ s33) # long steady-state runs on the final build (board flags, episode counts)
   run long_4096 400 python bench.py --global-batch 4096 --no-cpu-baseline --steps 20000 || exit 1; line long_4096
   run long_65536 400 python bench.py --no-cpu-baseline --steps 3000 || exit 1; line long_65536
   ;;
+s34) # refill walk budget per launch (TD_REFILL_WALKS; product: 3 per step of interval = 192) at the small shares
+  for r in 1 2; do for w in 192 48 12 768; do for bb in 4096 8192; do
+    TD_REFILL_WALKS=$w run w${w}_${bb}_$r 200 python bench.py --global-batch $bb --no-cpu-baseline --steps 3000 || exit 1; line w${w}_${bb}_$r
+  done; done; done
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "session $S rc=0"
