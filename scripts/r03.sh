@@ -310,6 +310,12 @@ s34) # refill walk budget per launch (TD_REFILL_WALKS; product: 3 per step of in
     TD_REFILL_WALKS=$w run w${w}_${bb}_$r 200 python bench.py --global-batch $bb --no-cpu-baseline --steps 3000 || exit 1; line w${w}_${bb}_$r
   done; done; done
   ;;
+s35) # per-phase wave cycles on the final build (stamps build): 4,096 / 8,192 / 65,536 boards
+  for bb in 4096 8192 65536; do
+    TDSTEP_LIB=$PWD/gym-td_amd/lib/libtdstep_stamps.so run phases_$bb 300 python scripts/probe_phases.py $bb 10 600 || exit 1
+    grep -v amdgpu.ids $O/phases_$bb.log | head -30
+  done
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "session $S rc=0"
