@@ -316,6 +316,13 @@ s35) # per-phase wave cycles on the final build (stamps build): 4,096 / 8,192 / 
     grep -v amdgpu.ids $O/phases_$bb.log | head -30
   done
   ;;
+s36) # the clean rebuild of the final sources: GPU suite, smoke, default line
+  run pytest_gpu 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread -p no:cacheprovider
+  rc=$?; grep -E "^(FAILED|E  )" $O/pytest_gpu.log | head -30; tail -1 $O/pytest_gpu.log; [ $rc -le 1 ] || exit $rc
+  run smoke 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" || exit 1
+  run bench_default 300 python bench.py --gpus 1 --steps 20 --warmup 5 || exit 1
+  grep '^{' $O/bench_default.log; line bench_default
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "session $S rc=0"
