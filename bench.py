@@ -76,13 +76,38 @@ EVENT_EVERY = 8  # timed steps per sampled kernel duration (an event pair per la
 FLAG_BITS = (("enemy_overflow", 1), ("tower_overflow", 2), ("bad_action", 4), ("no_layout", 8), ("bad_move", 16))
 
 
+KERNEL_SAMPLES_MIN = 8  # sampled launches behind a kernel mean
+
+
 def event_every(steps, override=None):
-    """Timed launches per sampled kernel duration: every 8th (a 20-step line averages 3
-    launches).  Sampling every launch perturbs what it measures: 42.5 vs 37.6 us per step
-    at 8,192 boards, 219.8 vs 214.4 us at 65,536 (profiles/r03/s6, --timing none beside it)."""
+    """Timed launches per sampled kernel duration: every 8th.  Sampling every launch
+    perturbs what it measures: 42.5 vs 37.6 us per step at 8,192 boards, 219.8 vs 214.4 us
+    at 65,536 (profiles/r03/s6, --timing none beside it)."""
     if override:
         return max(1, int(override))
     return EVENT_EVERY
+
+
+def timing_plan(steps, every):
+    """Where the step-kernel durations are sampled: ("timed", n) -- every ``every``-th
+    launch of the timed region, n launches -- when the timed region holds at least
+    KERNEL_SAMPLES_MIN of them; else ("after", n_steps): the timed region runs without
+    timing events and an untimed pass of n_steps (>= KERNEL_SAMPLES_MIN samples at the same
+    cadence) follows it.  A 20-step line (the driver's) thus averages 8 launches, not 3."""
+    n = (steps + every - 1) // every
+    if n >= KERNEL_SAMPLES_MIN:
+        return "timed", n
+    return "after", max(steps, KERNEL_SAMPLES_MIN * every)
+
+
+def kernel_vs_step(avg_kernel_us, step_us):
+    """A step kernel cannot take longer than the wall time per step of the steps it was
+    sampled in: when the mean says so, the kernel figure is not trusted and the roofline
+    fraction is withheld (None) with the reason."""
+    if not (avg_kernel_us == avg_kernel_us) or not (step_us > 0):  # nan: not timed
+        return False, None
+    return avg_kernel_us > step_us, ("mean sampled kernel %.2f us exceeds the %.2f us wall time per step it was "
+                                     "sampled in" % (avg_kernel_us, step_us)) if avg_kernel_us > step_us else None
 
 
 def algorithmic_bytes(L, mode="def", multi=False):
@@ -210,11 +235,30 @@ def cpu_baseline(L, mode, multi, seconds, threads, workload):
 
 
 def host_cores():
+    """Every core this process may run on (its affinity mask; SURVEY 8(d): the CPU
+    baseline runs on all host cores and states the count)."""
     try:
         n = len(os.sched_getaffinity(0))
     except Exception:  # noqa: BLE001
         n = os.cpu_count() or 1
-    return max(1, min(16, n))
+    return max(1, n)
+
+
+def cpu_quota():
+    """The cgroup CPU bandwidth limit in cores (cgroup v2 cpu.max / v1 cfs quota), or None
+    when there is none.  A box may give a process fewer cores' worth of time than its
+    affinity mask lists; the baseline line states both."""
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else int(q) / int(p)
+    except Exception:  # noqa: BLE001
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        p = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        return None if q <= 0 else q / p
+    except Exception:  # noqa: BLE001
+        return None
 
 
 # --------------------------------------------------------------------------- launch
@@ -348,32 +392,51 @@ def main():
     # duration is sampled live over the timed region without a timing event pair
     # (and its cache flush) behind every launch
     every = event_every(K, args.event_every)
+    plan, n_plan = timing_plan(K, every) if args.timing == "dispatch" else ("timed", 0)
     sampled = set(range(0, K, every)) if args.timing == "marker" else set()
     ev = {k: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for k in sampled}
     eng.episode_stats(clear=True)  # the device accumulates finished episodes of the timed steps
     if args.refill_interval is not None:
         eng.set_refill_interval(args.refill_interval)
-    if args.timing == "dispatch":
-        eng.kernel_timing((K + every - 1) // every, every)  # timestamped by their own dispatch
+    if plan == "timed" and args.timing == "dispatch":
+        eng.kernel_timing(n_plan, every)  # timestamped by their own dispatch
+
+    def run_steps(n, first):
+        for k in range(n):
+            if first + k in sampled:
+                ev[first + k][0].record(stream)
+            d, a = acts[(first + k) % len(acts)]
+            eng.step(def_act=d, atk_act=a)
+            if first + k in sampled:
+                ev[first + k][1].record(stream)
 
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for k in range(K):
-        if k in sampled:
-            ev[k][0].record(stream)
-        d, a = acts[k % len(acts)]
-        eng.step(def_act=d, atk_act=a)
-        if k in sampled:
-            ev[k][1].record(stream)
+    run_steps(K, 0)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
 
+    # snapshots of the timed steps' episode statistics and flags (stream-ordered copies)
+    flags = eng.flags()
+    ep_stats = eng.episode_stats(clear=True)
+    ep_recs = eng.episode_records()
+    sample_wall = elapsed  # wall time of the steps the kernel samples come from
+    n_sample_steps = K
+    if plan == "after":
+        # short timed region: it ran without timing events; the kernel mean comes from an
+        # untimed pass of the same kernel right behind it, KERNEL_SAMPLES_MIN samples or more
+        eng.kernel_timing((n_plan + every - 1) // every, every)
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        run_steps(n_plan, K)
+        torch.cuda.synchronize(dev)
+        sample_wall, n_sample_steps = time.perf_counter() - t1, n_plan
     if args.timing == "dispatch":
         kern_ms = (eng.kernel_times().astype(np.float64) / 1e3).tolist()
         eng.kernel_timing(0)
@@ -384,12 +447,12 @@ def main():
     avg_kernel_s = float(np.mean(kern_ms)) / 1e3
     # after timing: MAX of the clocks over ranks, and the episode statistics of the
     # timed steps gathered to rank 0 (the only exchange; RCCL on GPUs)
-    flags = eng.flags()
-    t = shard.max_over_ranks(torch.tensor([elapsed, avg_kernel_s], dtype=torch.float64, device=coll))
-    per_rank = shard.gather_stats(eng.episode_stats(clear=True).to(coll))
+    t = shard.max_over_ranks(torch.tensor([elapsed, avg_kernel_s, sample_wall / n_sample_steps], dtype=torch.float64,
+                                          device=coll))
+    per_rank = shard.gather_stats(ep_stats.to(coll))
     # the per-board payload (16 B per board: last episode's return, length, win)
-    recs = shard.gather_episode_records(*[t.to(coll) for t in eng.episode_records()])
-    elapsed, avg_kernel_s = float(t[0]), float(t[1])
+    recs = shard.gather_episode_records(*[t.to(coll) for t in ep_recs])
+    elapsed, avg_kernel_s, sample_step_s = float(t[0]), float(t[1]), float(t[2])
     reported_world = dist.get_world_size() if world > 1 else 1  # what the process group (RCCL) reports
 
     if rank == 0:
@@ -397,6 +460,7 @@ def main():
         value = total_steps / elapsed
         bpe = algorithmic_bytes(L, mode, multi)
         achieved = B * bpe / avg_kernel_s / 1e9
+        exceeds, why = kernel_vs_step(avg_kernel_s * 1e6, sample_step_s * 1e6)
         traffic, traffic_src = measured_traffic(args.workload, B, eng.step_kernel_name)
         out = {
             "metric": metric,
@@ -411,13 +475,19 @@ def main():
                                       args.burnin, ", episode phases staggered" if args.stagger else ""),
                        "global_batch": global_batch, "boards_per_gpu": B,
                        "map_size": L, "parallelism": "boards sharded per GPU (dp%d), no data-path collective" % world},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
+            "roofline": {"bound": "hbm", "achieved": None if exceeds else achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": None if exceeds else achieved / HBM_PEAK_GBS,
+                         "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": eng.step_kernel_name,
                          "avg_kernel_us": avg_kernel_s * 1e6,
                          "kernel_samples": len(kern_ms) * world,
-                         "kernel_timing": {"dispatch": "dispatch-packet timestamps of every %dth timed launch "
-                                                       "(td_kernel_timing)" % every,
+                         "kernel_exceeds_step": exceeds,
+                         "kernel_timing": {"dispatch": "dispatch-packet timestamps of every %dth launch (td_kernel_timing) "
+                                                       "%s, %.2f us wall per step there" % (
+                                                           every, "of the timed region" if plan == "timed" else
+                                                           "of an untimed %d-step pass right after the timed region "
+                                                           "(the timed steps ran without timing events)" % n_plan,
+                                                           sample_step_s * 1e6),
                                            "marker": "torch event pairs around every %dth launch" % every,
                                            "none": "not timed"}[args.timing],
                          "algorithmic_bytes_per_launch": B * bpe},
@@ -429,10 +499,17 @@ def main():
                          "boards_with_a_finished_episode": int((recs[2] >= 0).sum()),
                          "last_episode_win_rate": float((recs[2] == 1).sum()) / max(int((recs[2] >= 0).sum()), 1)},
         }
+        if exceeds:
+            out["roofline"]["frac_withheld"] = why
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(L, mode, multi, args.cpu_seconds, host_cores(), args.workload)
+            cores, quota = host_cores(), cpu_quota()
+            out["cpu_baseline"] = cpu_baseline(L, mode, multi, args.cpu_seconds, cores, args.workload)
+            out["cpu_baseline"]["cpu_quota_cores"] = quota
             if args.py_cpu_seconds > 0:
-                out["cpu_baseline_python"] = cpu_baseline_python(L, mode, multi, args.py_cpu_seconds, host_cores(),
+                # one process per core, within the CPU time the box grants (spawning more
+                # interpreters than that only time-slices them)
+                procs = max(1, min(cores, int(quota) if quota else cores, 64))
+                out["cpu_baseline_python"] = cpu_baseline_python(L, mode, multi, args.py_cpu_seconds, procs,
                                                                  args.workload)
         print(json.dumps(out), flush=True)
     eng.close()

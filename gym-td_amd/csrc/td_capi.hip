@@ -307,6 +307,15 @@ extern "C" {
 
 int td_abi_version(void) { return TD_ABI_VERSION; }
 
+int td_step_io_size(void) { return (int)sizeof(td_step_io); }
+
+void td_step_io_init(td_step_io* io) {
+  if (!io) return;
+  std::memset(io, 0, sizeof *io);
+  io->size = (uint32_t)sizeof(td_step_io);
+  io->abi = TD_ABI_VERSION;
+}
+
 const char* td_last_error(void) { return g_err.c_str(); }
 
 void td_config_default(td_config* c) {
@@ -400,6 +409,15 @@ td_handle* td_create(const td_config* cfg, int map_size, int n_boards, int mode,
   rc |= dalloc(&h->d_stage, (size_t)h->stage_cap * h->lw);
   rc |= dalloc(&h->d_epstats, 2);
   rc |= dalloc(&h->d_lastep, B);
+  if (rc) {  // name the footprint (the staged-layout rings are most of it at large L)
+    const double ring = (double)B * NSLOT * slot_words(map_size) * 4.0;
+    const double total = (double)B * (sizeof(TdHdr) + ECAP * 20 + TCAP * 12 + (size_t)h->NC * 4 + 2 * OPP_WORDS * 4 +
+                                      HOT_WORDS * 4 + 12 + h->scratch_stride + 2 + sizeof(td_episode_record)) + ring;
+    std::string e = g_err;
+    fail("td_create: %d boards at L = %d need %.1f MB of device memory (%.1f MB of it the staged-layout rings, "
+         "%d x %d words per board): %s", n_boards, map_size, total / 1e6, ring / 1e6, NSLOT, slot_words(map_size),
+         e.c_str());
+  }
   if (!rc) {  // win = -1: no finished episode yet
     std::vector<td_episode_record> init((size_t)B, td_episode_record{0.0, 0, -1});
     if (hipMemcpy(h->d_lastep, init.data(), B * sizeof(td_episode_record), hipMemcpyHostToDevice) != hipSuccess)
@@ -685,7 +703,15 @@ int td_reset_layouts(td_handle* h, const uint32_t* recs, const int32_t* boards, 
 }
 
 int td_step(td_handle* h, const td_step_io* io, void* stream) {
-  if (!h || !io) return fail("td_step: NULL argument");
+  if (!io) return fail("td_step: NULL io");
+  // The two header words first (every td_step_io of any ABI has >= 8 bytes): a caller
+  // built against another layout is refused before any pointer of its struct is read.
+  if (io->size != (uint32_t)sizeof(td_step_io) || io->abi != (uint32_t)TD_ABI_VERSION)
+    return fail("td_step: td_step_io has size %u / abi %u, this library expects size %u / abi %d "
+                "(set io.size = sizeof(td_step_io) and io.abi = TD_ABI_VERSION, or call td_step_io_init; "
+                "an ABI-2 struct has no header)",
+                io->size, io->abi, (unsigned)sizeof(td_step_io), TD_ABI_VERSION);
+  if (!h) return fail("td_step: NULL handle");
   if (!io->obs || !io->reward || !io->done) return fail("td_step: obs, reward and done are required");
   if (h->mode != TD_MODE_ATK && !io->def_act) return fail("td_step: def_act required in this mode");
   if (h->mode != TD_MODE_DEF && !io->atk_act) return fail("td_step: atk_act required in this mode");
@@ -911,16 +937,19 @@ int td_debug_stamps(td_handle* h, uint64_t* dev) {
 }
 #endif
 
-// Diagnostic: board b's ring -- head, tail, claim, then the NSLOT slot tags.
-int td_debug_ring(td_handle* h, int b, uint32_t* out) {
+// Diagnostic: board b's ring -- head, tail, claim, then the NSLOT slot tags: 3 + NSLOT
+// words into out[0, cap).  Returns the word count (td_debug_ring(h, 0, NULL, 0) asks for it).
+int td_debug_ring(td_handle* h, int b, uint32_t* out, int cap) {
+  if (!out && cap == 0) return 3 + NSLOT;
   if (!h || b < 0 || b >= h->B || !out) return fail("td_debug_ring: bad arguments");
+  if (cap < 3 + NSLOT) return fail("td_debug_ring: buffer of %d words, needs %d", cap, 3 + NSLOT);
   HIP_OK(hipDeviceSynchronize());
   HIP_OK(hipMemcpy(out, h->d_lay_head + b, 4, hipMemcpyDeviceToHost));
   HIP_OK(hipMemcpy(out + 1, h->d_lay_tail + b, 4, hipMemcpyDeviceToHost));
   HIP_OK(hipMemcpy(out + 2, h->d_lay_claim + b, 4, hipMemcpyDeviceToHost));
   for (int s = 0; s < NSLOT; ++s)
     HIP_OK(hipMemcpy(out + 3 + s, h->d_nxt + ((size_t)b * NSLOT + s) * slot_words(h->L), 4, hipMemcpyDeviceToHost));
-  return 0;
+  return 3 + NSLOT;
 }
 
 void td_py_seed(uint32_t* mt, uint32_t seed) { py_seed(mt, seed); }

@@ -1553,12 +1553,22 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
     const int nf = NCH * x.NCr;
     float* o = a.obs + (size_t)b * nf;
     for (int i = x.lane; i < nf; i += 64) o[i] = 0.0f;
-    if (x.lane == 0) {
+    if (x.lane == 0) {  // every output defined: done, no reward, no action taken
       a.hdr[b].flags = u.flags | FLAG_NO_LAYOUT;
       a.reward[b] = 0.0;
       a.done[b] = 1;
       if (a.win) a.win[b] = -1;
+      if (a.allow_next) a.allow_next[b] = 0;
+      if (a.cooldowns) a.cooldowns[b] = 0;
+      if (a.fail_def) a.fail_def[b] = 0;
+      if (a.real_def && !a.multi) a.real_def[b] = (int64_t)6 * x.NCr;
+      if (a.ep_return) a.ep_return[b] = 0.0;
+      if (a.ep_len) a.ep_len[b] = 0;
     }
+    if (a.real_def && a.multi)
+      for (int i = x.lane; i < 6 * x.NCr; i += 64) a.real_def[(size_t)b * 6 * x.NCr + i] = 0;
+    if (a.fail_atk && x.lane < 3) a.fail_atk[(size_t)b * 3 + x.lane] = -1;
+    if (a.real_atk && x.lane < 24) a.real_atk[(size_t)b * 24 + x.lane] = 4;
     if constexpr (SPLIT) {
       if (x.lane == 0) { S.early_go = 0u; S.obs_go = 0u; }
       __syncthreads();  // (A)
@@ -2225,8 +2235,17 @@ __global__ __launch_bounds__(64) void td_refill_kernel(StepArgs a, int guard) {
       const int bb = base + l;
       if (!claim_board(a.lay_claim + bb, lane)) {  // another refill is drawing its layouts
         if (!guard) continue;
-        do __builtin_amdgcn_s_sleep(8);
-        while (!claim_board(a.lay_claim + bb, lane));
+        // the holder is a resident side-refill wave that gives the claim back after its
+        // walk budget; bounded all the same (1 s, as take_dry_ring): a claim never given
+        // back leaves this board's ring short -- its episode end is then flagged
+        // no_layout by the step -- instead of hanging the step stream
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        bool got = false;
+        while (!got && __builtin_amdgcn_s_memrealtime() - t0 < kTakeSpinTicks) {
+          __builtin_amdgcn_s_sleep(8);
+          got = claim_board(a.lay_claim + bb, lane);
+        }
+        if (!got) continue;
       }
       uint32_t t = ld_relaxed(a.lay_tail + bb);
       const uint32_t h = ld_relaxed(a.lay_head + bb);

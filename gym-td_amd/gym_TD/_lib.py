@@ -17,7 +17,7 @@ ECAP, TCAP, NCH = 128, 32, 45
 MT_WORDS = 625
 OPP_WORDS = 626
 HDR_BYTES = 96
-ABI_VERSION = 2  # include/tdstep.h TD_ABI_VERSION
+ABI_VERSION = 3  # include/tdstep.h TD_ABI_VERSION
 STEP_KERNELS = {"auto": 0, "large": 1, "small": 2, "small2": 3}  # enum td_step_kernel_kind
 
 c_u32p = ctypes.POINTER(ctypes.c_uint32)
@@ -42,10 +42,15 @@ class TdConfig(ctypes.Structure):
 
 
 class TdStepIO(ctypes.Structure):
-    """struct td_step_io (tdstep.h): device pointers."""
-    _fields_ = [(n, c_vp) for n in (
+    """struct td_step_io (tdstep.h): the size / ABI header td_step checks, then device pointers."""
+    _fields_ = [("size", ctypes.c_uint32), ("abi", ctypes.c_uint32)] + [(n, c_vp) for n in (
         "def_act", "atk_act", "obs", "reward", "done", "real_def", "real_atk", "fail_def", "fail_atk",
         "win", "allow_next", "ep_return", "ep_len", "cooldowns")]
+
+    def __init__(self, **kw):
+        kw.setdefault("size", ctypes.sizeof(TdStepIO))
+        kw.setdefault("abi", ABI_VERSION)
+        super().__init__(**kw)
 
 
 def _load():
@@ -55,6 +60,8 @@ def _load():
     lib = ctypes.CDLL(LIB_PATH)
     sig = {
         "td_abi_version": (ctypes.c_int, []),
+        "td_step_io_size": (ctypes.c_int, []),
+        "td_step_io_init": (None, [ctypes.POINTER(TdStepIO)]),
         "td_last_error": (ctypes.c_char_p, []),
         "td_config_default": (None, [ctypes.POINTER(TdConfig)]),
         "td_create": (c_vp, [ctypes.POINTER(TdConfig), ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
@@ -99,8 +106,9 @@ def _load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.td_abi_version() != ABI_VERSION:
-        raise ImportError("libtdstep.so ABI version mismatch")
+    if lib.td_abi_version() != ABI_VERSION or lib.td_step_io_size() != ctypes.sizeof(TdStepIO):
+        raise ImportError("libtdstep.so ABI mismatch: library ABI %d / td_step_io %d bytes, binding ABI %d / %d bytes"
+                          % (lib.td_abi_version(), lib.td_step_io_size(), ABI_VERSION, ctypes.sizeof(TdStepIO)))
     return lib
 
 

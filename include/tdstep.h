@@ -40,7 +40,10 @@
 extern "C" {
 #endif
 
-#define TD_ABI_VERSION 2
+/* ABI 3: td_step_io starts with its own size and ABI words, which td_step checks before
+ * it reads anything else (an ABI-2 struct -- 14 pointers, no header -- is refused).
+ * ABI 2: td_step_io.cooldowns.  ABI 1: the first release. */
+#define TD_ABI_VERSION 3
 
 enum td_mode { TD_MODE_DEF = 0, TD_MODE_ATK = 1, TD_MODE_2P = 2 };
 
@@ -82,8 +85,14 @@ typedef struct td_config {
  *             step (the finished episode's totals when done[b]).
  *   cooldowns uint8 [B]: the env's attacker_cd (bits 0-3) and defender_cd (bits 4-7) after the
  *             step (TDDefense.py:38-39,75, TDAttack.py:31-32,44), each saturated at 15
- *             (ABI 2; ABI 1 packed them into allow_next bits 2-7). */
+ *             (ABI 2; ABI 1 packed them into allow_next bits 2-7).
+ *   size, abi: sizeof(td_step_io) and TD_ABI_VERSION as the caller was built (ABI 3;
+ *             td_step_io_init sets both).  td_step reads these two words first and refuses,
+ *             with no launch, a struct whose size or ABI differs from its own: a caller
+ *             built against another layout of this struct is caught, not stepped. */
 typedef struct td_step_io {
+  uint32_t size;
+  uint32_t abi;
   const int64_t* def_act;
   const int64_t* atk_act;
   float* obs;
@@ -103,9 +112,18 @@ typedef struct td_step_io {
 typedef struct td_handle td_handle;
 
 int td_abi_version(void);
+/* sizeof(td_step_io) as this library was built (120 on LP64 at ABI 3). */
+int td_step_io_size(void);
+/* Zero *io and set its size / abi words (a C caller's initialiser; writes td_step_io_size()
+ * bytes, so io must be this header's td_step_io). */
+void td_step_io_init(td_step_io* io);
 const char* td_last_error(void);
 void td_config_default(td_config* cfg);
 
+/* Device memory per board: ~8.2 KB + 18*L^2 B of state (records, both RNG streams, the
+ * layout draw's scratch) plus a ring of 16 staged layouts of (8 + L^2 rounded up to 32)
+ * words each -- ~18 KB at L = 10 (1.2 GB at 65,536 boards), ~84 KB at L = 30 (5.5 GB at
+ * 65,536).  A failed allocation names the footprint in td_last_error(). */
 /* mode: td_mode; multi_action: HyperParameters.allow_multiple_actions;
  * difficulty: built-in opponent level (TD-def: 0/1, TD-atk: 0/1/2, TD-2p: ignored);
  * map_size: 10/20/30 have specialised kernels, any 4 <= L <= 32 works. */

@@ -15,7 +15,8 @@ for k in range(1, 1200):
 g = torch.Generator(device="cuda").manual_seed(0)
 fn = _lib.lib.td_debug_ring
 fn.restype = ctypes.c_int
-fn.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+fn.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
+NW = fn(None, 0, None, 0)  # 3 + NSLOT words
 prev = np.zeros(B, dtype=np.int32)
 t = time.time()
 for k in range(steps):
@@ -25,10 +26,10 @@ for k in range(steps):
         new = np.nonzero((f & 8) & ~(prev & 8))[0]
         print("flagged", len(new))
         for b in new[:12]:
-            out = np.zeros(8, dtype=np.uint32)
-            fn(eng._h, int(b), out.ctypes.data)
+            out = np.zeros(NW, dtype=np.uint32)
+            fn(eng._h, int(b), out.ctypes.data, NW)
             st = eng.board_state(int(b))
             print("step %d board %d head %d tail %d claim %d tags %s ep_steps %d base_LP %d" % (
-                k, b, out[0], out[1], out[2], [hex(v) for v in out[3:3 + 4]], st["steps"], st["base_LP"]), flush=True)
+                k, b, out[0], out[1], out[2], [hex(v) for v in out[3:]], st["steps"], st["base_LP"]), flush=True)
         prev = f
 print("done %.1fs, flagged %d" % (time.time() - t, int(((eng.flags() & 8) != 0).sum())))

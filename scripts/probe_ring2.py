@@ -14,11 +14,12 @@ eng = TDEngine(10, B, "def", False, 1, np_seeds=seeds, py_seeds=seeds, autoreset
 eng.reset_all()
 fn = _lib.lib.td_debug_ring
 fn.restype = ctypes.c_int
-fn.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+fn.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
+NW = fn(None, 0, None, 0)  # 3 + NSLOT words
 def ring(b):
-    out = np.zeros(8, dtype=np.uint32)
-    fn(eng._h, int(b), out.ctypes.data)
-    return out[:3].tolist(), [hex(v) for v in out[3:7]]
+    out = np.zeros(NW, dtype=np.uint32)
+    fn(eng._h, int(b), out.ctypes.data, NW)
+    return out[:3].tolist(), [hex(v) for v in out[3:]]
 print("after reset", [ring(b) for b in range(3)])
 rng = np.random.RandomState(9)
 for k in range(200):

@@ -72,3 +72,27 @@ def test_gpus_n_starts_n_ranks(monkeypatch):
     assert cmd[1:3] == ["-m", "torch.distributed.run"]
     assert cmd[cmd.index("--nproc-per-node") + 1] == "4" and cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
     assert cmd[-4:] == [bench.os.path.abspath(bench.__file__), "--gpus", "4", "--steps", "5"][-4:]
+
+
+def test_short_runs_sample_enough_launches():
+    # the driver's 20-step line: no events in the timed region, an untimed pass of 64 steps
+    # sampled every 8th launch (8 samples) behind it
+    assert bench.timing_plan(20, 8) == ("after", 64)
+    assert bench.timing_plan(32, 8) == ("after", 64)
+    assert bench.timing_plan(64, 8) == ("timed", 8)
+    assert bench.timing_plan(2000, 8) == ("timed", 250)
+    assert bench.timing_plan(5, 1) == ("after", 8)
+
+
+def test_kernel_longer_than_the_step_withholds_the_fraction():
+    assert bench.kernel_vs_step(225.9, 221.8)[0] is True
+    assert "exceeds" in bench.kernel_vs_step(225.9, 221.8)[1]
+    assert bench.kernel_vs_step(215.0, 221.8) == (False, None)
+    assert bench.kernel_vs_step(float("nan"), 221.8) == (False, None)
+
+
+def test_cpu_baseline_uses_every_core_of_the_affinity_mask():
+    import os
+    assert bench.host_cores() == len(os.sched_getaffinity(0))
+    q = bench.cpu_quota()
+    assert q is None or q > 0

@@ -678,8 +678,9 @@ def test_autoreset_under_load_matches_explicit_reset(B, steps, kernel, refill):
     reset explicitly (the reset kernel draws each layout on the spot, failing draws
     skipped as the refill skips them).  Every board must agree at every step, on each
     step kernel (8,192 boards: the N = 8 share's kernel).  refill = 0: no refill kernel at
-    all -- every layout comes from the ring guard on the step stream (td_refill_kernel,
-    guard = 1), so an episode end never depends on the refill cadence."""
+    all -- every layout comes from the ring guard on the step stream (td_refill_kernel with
+    guard = 15 = NSLOT - 1: before every 15th step it fills every ring below 15 layouts to
+    15), so an episode end never depends on the refill cadence."""
     from test_gpu_parity import reference_settings
     L = 10
     ov = dict(base_LP=1, defender_init_cost=0, defender_cost_rate=0.02)
