@@ -244,6 +244,28 @@ def host_cores():
     return max(1, n)
 
 
+def baseline_threads():
+    """(threads, affinity cores, quota cores) of the CPU baseline: one thread per core the
+    process may run on, bounded by the CPU time the box grants it.  On the MI355X boxes the
+    affinity mask lists 256 cores and the cgroup grants 16 cores' worth of time
+    (cpu.max 1600000 / 100000, profiles/r04/s1/host.log): 256 OpenMP threads there measured
+    3.3 M env-steps/s, 16 threads 8.2 M -- throttled time slices, not a larger host."""
+    affinity, quota = host_cores(), cpu_quota()
+    threads = affinity if not quota else max(1, min(affinity, int(quota)))
+    return threads, affinity, quota
+
+
+def baseline_note(value, threads, affinity, quota):
+    """The core accounting of a CPU-baseline line: what it ran on, what the host has, and
+    the whole host's rate at the measured per-core rate (a linear projection, labelled)."""
+    per_core = value / threads
+    return {"affinity_cores": affinity, "cpu_quota_cores": quota, "value_per_core": per_core,
+            "all_affinity_cores_projection": {
+                "value": per_core * affinity, "cores": affinity,
+                "note": "linear projection of the measured per-core rate to every core of the affinity mask "
+                        "(not measured: the cgroup grants %s cores' worth of CPU time)" % (quota,)}}
+
+
 def cpu_quota():
     """The cgroup CPU bandwidth limit in cores (cgroup v2 cpu.max / v1 cfs quota), or None
     when there is none.  A box may give a process fewer cores' worth of time than its
@@ -502,14 +524,12 @@ def main():
         if exceeds:
             out["roofline"]["frac_withheld"] = why
         if world == 1 and not args.no_cpu_baseline:
-            cores, quota = host_cores(), cpu_quota()
-            out["cpu_baseline"] = cpu_baseline(L, mode, multi, args.cpu_seconds, cores, args.workload)
-            out["cpu_baseline"]["cpu_quota_cores"] = quota
+            threads, affinity, quota = baseline_threads()
+            cb = cpu_baseline(L, mode, multi, args.cpu_seconds, threads, args.workload)
+            cb.update(baseline_note(cb["value"], threads, affinity, quota))
+            out["cpu_baseline"] = cb
             if args.py_cpu_seconds > 0:
-                # one process per core, within the CPU time the box grants (spawning more
-                # interpreters than that only time-slices them)
-                procs = max(1, min(cores, int(quota) if quota else cores, 64))
-                out["cpu_baseline_python"] = cpu_baseline_python(L, mode, multi, args.py_cpu_seconds, procs,
+                out["cpu_baseline_python"] = cpu_baseline_python(L, mode, multi, args.py_cpu_seconds, min(threads, 64),
                                                                  args.workload)
         print(json.dumps(out), flush=True)
     eng.close()

@@ -119,6 +119,13 @@ struct td_handle {
   long long tev_from = 0;  // h->steps when td_kernel_timing was called
   long long steps = 0;
   std::vector<int32_t> last_reset_failed;
+  // longest-work-first board order of the small kernels (td_step.hip ord_*): two lists
+  // (this step's, the next step's) and two sets of chunk counters, by parity of ord_steps
+  uint32_t* d_ord = nullptr;
+  uint32_t* d_ord_cnt = nullptr;
+  int ord_stride = 0;
+  int ord_on = 1;  // TD_ORDER=0: blocks step boards in index order (A/B runs)
+  long long ord_steps = 0;
 };
 
 namespace {
@@ -409,6 +416,16 @@ td_handle* td_create(const td_config* cfg, int map_size, int n_boards, int mode,
   rc |= dalloc(&h->d_stage, (size_t)h->stage_cap * h->lw);
   rc |= dalloc(&h->d_epstats, 2);
   rc |= dalloc(&h->d_lastep, B);
+  h->ord_stride = ord_stride(n_boards);
+  rc |= dalloc(&h->d_ord, (size_t)2 * ORD_XCD * h->ord_stride);
+  rc |= dalloc(&h->d_ord_cnt, (size_t)2 * ORD_CNT_WORDS);
+  if (!rc) {  // both lists start as the identity: block i steps board i
+    std::vector<uint32_t> ord((size_t)2 * ORD_XCD * h->ord_stride, 0u);
+    for (int i = 0; i < n_boards; ++i)
+      for (int p = 0; p < 2; ++p) ord[((size_t)p * ORD_XCD + i % ORD_XCD) * h->ord_stride + i / ORD_XCD] = (uint32_t)i;
+    if (hipMemcpy(h->d_ord, ord.data(), ord.size() * 4, hipMemcpyHostToDevice) != hipSuccess) rc = fail("order init");
+  }
+  if (const char* e = std::getenv("TD_ORDER")) h->ord_on = std::atoi(e) ? 1 : 0;  // A/B runs
   if (rc) {  // name the footprint (the staged-layout rings are most of it at large L)
     const double ring = (double)B * NSLOT * slot_words(map_size) * 4.0;
     const double total = (double)B * (sizeof(TdHdr) + ECAP * 20 + TCAP * 12 + (size_t)h->NC * 4 + 2 * OPP_WORDS * 4 +
@@ -494,7 +511,8 @@ void td_destroy(td_handle* h) {
   (void)hipDeviceSynchronize();
   void* dptrs[] = {h->d_cfg, h->d_hdr, h->d_en_lp, h->d_en_mg, h->d_en_inf, h->d_tw_cd, h->d_tw_inf,
                    h->d_cells, h->d_opp, h->d_hot, h->d_np, h->d_nxt, h->d_scratch, h->d_lay_head, h->d_lay_tail,
-                   h->d_lay_claim, h->d_ovr_idx, h->d_mask, h->d_fail, h->d_stage, h->d_epstats, h->d_lastep};
+                   h->d_lay_claim, h->d_ovr_idx, h->d_mask, h->d_fail, h->d_stage, h->d_epstats, h->d_lastep,
+                   h->d_ord, h->d_ord_cnt};
   for (void* p : dptrs)
     if (p) (void)hipFree(p);
   if (h->ev_main) (void)hipEventDestroy(h->ev_main);
@@ -742,7 +760,20 @@ int td_step(td_handle* h, const td_step_io* io, void* stream) {
     e1 = h->tev[2 * (size_t)h->tev_n + 1];
     h->tev_n += 1;
   }
+  // the small kernels (launched for a 16-B-aligned observation, launch2) step their boards
+  // in the order the previous small-kernel step left
+  const bool ordered = h->ord_on && h->small && ((reinterpret_cast<uintptr_t>(io->obs) & 15u) == 0);
+  if (ordered) {
+    const int p = (int)(h->ord_steps & 1);
+    const size_t span = (size_t)ORD_XCD * h->ord_stride;
+    a.ord_in = h->d_ord + (size_t)p * span;
+    a.ord_out = h->d_ord + (size_t)(1 - p) * span;
+    a.ord_cnt = h->d_ord_cnt + (size_t)p * ORD_CNT_WORDS;
+    a.ord_clr = h->d_ord_cnt + (size_t)(1 - p) * ORD_CNT_WORDS;
+    a.ord_stride = h->ord_stride;
+  }
   HIP_OK(launch_step(a, s, false, e0, e1));
+  if (ordered) h->ord_steps += 1;
   if (h->autoreset && h->opp_np) HIP_OK(launch_autoreset(a, s));
   h->steps += 1;
   h->since_guard += 1;
@@ -772,9 +803,13 @@ int td_set_refill_interval(td_handle* h, int steps) {
 int td_kernel_timing(td_handle* h, int max_launches, int every) {
   if (!h || max_launches < 0 || every < 1) return fail("td_kernel_timing: bad arguments");
   HIP_OK(hipDeviceSynchronize());
+  // TD_TEV_FLAGS=1 (A/B runs): timing events without the system-scope release at the timed
+  // kernel's end (the cache write-back it implies lengthens the kernel being timed)
+  const char* tf = std::getenv("TD_TEV_FLAGS");
+  const unsigned flags = tf && std::atoi(tf) == 1 ? hipEventDisableSystemFence : hipEventDefault;
   while ((int)h->tev.size() < 2 * max_launches) {
     hipEvent_t e = nullptr;
-    HIP_OK(hipEventCreate(&e));
+    HIP_OK(hipEventCreateWithFlags(&e, flags));
     h->tev.push_back(e);
   }
   h->tev_cap = max_launches;

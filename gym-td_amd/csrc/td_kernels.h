@@ -65,7 +65,24 @@ struct StepArgs {
   double* ep_stats;  // [2]: finished episodes, sum of their returns (accumulated by the step kernel)
   td_episode_record* last_ep;  // [B]: each board's last finished episode (written on done)
   const uint8_t* reset_mask;  // reset kernel only (nullptr = all boards)
+  // Longest-work-first board order (small kernels, td_capi.hip): block i steps board
+  // ord_in[(i % 8) * ord_stride + i / 8] (nullptr: board i); each board then claims its slot
+  // in the next step's order -- boards with enemies first -- through ord_cnt (ORD_CHUNKS
+  // chunk counters per XCD, one 128-B line each: [0] heavy, [1] light).  ord_clr: the other
+  // parity's counters, zeroed by block 0 for the step after this one.
+  const uint32_t* ord_in;
+  uint32_t* ord_out;
+  uint32_t* ord_cnt;
+  uint32_t* ord_clr;
+  int ord_stride;
 };
+
+// Board order: 8 XCD lists (block i runs on XCD i % 8, slot i / 8 of its list), each split
+// into ORD_CHUNKS interleaved chunks (slot s in chunk s % ORD_CHUNKS) so no counter sees more
+// than B / 8 / ORD_CHUNKS returning atomics per step.
+constexpr int ORD_XCD = 8, ORD_CHUNKS = 16, ORD_LINE = 32;
+constexpr int ORD_CNT_WORDS = ORD_XCD * ORD_CHUNKS * ORD_LINE;  // per parity
+__host__ __device__ inline int ord_stride(int B) { return (B + ORD_XCD - 1) / ORD_XCD; }
 
 // ev0 / ev1: optional timing events bound to the step kernel's dispatch (td_kernel_timing).
 hipError_t launch_step(const StepArgs& a, hipStream_t s, bool reset, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);

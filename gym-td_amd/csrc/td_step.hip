@@ -1527,6 +1527,41 @@ constexpr int obs_late_half() {
   return K;
 }
 
+// Longest-work-first board order (StepArgs::ord_*).  Block i of a small-kernel step runs
+// on XCD i % 8, slot i / 8 of that XCD's list; its board is ord_in[that slot].  A step
+// grid of one round of waves ends with its last wave, and the waves start over the grid's
+// ~8-us dispatch window in block order: boards with enemies (the longest steps: sort,
+// targeting, march, group statistics) are listed first, so they start at the window's
+// head instead of anywhere in it.  Each board claims its slot in the next step's list of
+// the same XCD (heavy from the front, light from the back of its chunk) with one
+// returning atomic, issued once its header is in and consumed phases later.
+__device__ __forceinline__ int ord_board(const StepArgs& a) {
+  const int i = (int)blockIdx.x;
+  if (!a.ord_in) return i;
+  return (int)a.ord_in[(i & (ORD_XCD - 1)) * a.ord_stride + i / ORD_XCD];
+}
+__device__ __forceinline__ int ord_line(int i) {
+  return ((i & (ORD_XCD - 1)) * ORD_CHUNKS + (i / ORD_XCD) % ORD_CHUNKS) * ORD_LINE;
+}
+// Claim: heavy = the board has enemies now (its next step will: enemies live tens of steps).
+__device__ __forceinline__ uint32_t ord_claim(const StepArgs& a, bool heavy, int lane) {
+  uint32_t r = 0;
+  if (!a.ord_in) return r;
+  const int i = (int)blockIdx.x;
+  if (lane == 0) r = atomicAdd(a.ord_cnt + ord_line(i) + (heavy ? 0 : 1), 1u);
+  if (i == 0)  // the other parity's counters start the step after this one at zero
+    for (int w = lane; w < ORD_XCD * ORD_CHUNKS; w += 64) { a.ord_clr[w * ORD_LINE] = 0u; a.ord_clr[w * ORD_LINE + 1] = 0u; }
+  return r;
+}
+__device__ __forceinline__ void ord_place(const StepArgs& a, int b, bool heavy, uint32_t r, int lane) {
+  if (!a.ord_in || lane != 0) return;
+  const int i = (int)blockIdx.x, xcd = i & (ORD_XCD - 1), c = (i / ORD_XCD) % ORD_CHUNKS;
+  const int nx = (a.B - 1 - xcd) / ORD_XCD + 1;               // slots of this XCD's list
+  const int cs = (nx - c + ORD_CHUNKS - 1) / ORD_CHUNKS;       // of them in chunk c
+  const int pos = heavy ? (int)r : cs - 1 - (int)r;
+  a.ord_out[xcd * a.ord_stride + c + ORD_CHUNKS * pos] = (uint32_t)b;
+}
+
 // SPLIT: the board's workgroup has a second wave (td_step_kernel_small2) that waits at
 // the one workgroup barrier of this path and then writes the second half of the
 // observation windows.
@@ -1540,6 +1575,9 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
   STAMP(0);
   constexpr int PF = SMALL ? PF_SMALL : PF_LARGE;
   load_board<NC, PF, PF>(S, u, x, a, b, P);
+  const bool ord_heavy = u.n > 0;
+  // (the multi-action scan has no register to hold the claim across it: claimed at the place)
+  uint32_t ord_r = SMALL && !SCAN ? ord_claim(a, ord_heavy, x.lane) : 0u;
   const int64_t act_in = (int64_t)(((uint64_t)lane_word(P.w, PF_ACT + 1) << 32) | lane_word(P.w, PF_ACT));
   // built-in opponent stream: position, lazy-twist boundary and the next draws
   // (pre-computed by the previous step) come from the board's hot record
@@ -1550,6 +1588,8 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
   STAMP(1);
   if (u.num_roads < 1 || u.num_roads > 3) {
     // never reset (its road generation failed): nothing to step
+    if constexpr (SMALL && SCAN) ord_r = ord_claim(a, ord_heavy, x.lane);
+    if constexpr (SMALL) ord_place(a, b, ord_heavy, ord_r, x.lane);
     const int nf = NCH * x.NCr;
     float* o = a.obs + (size_t)b * nf;
     for (int i = x.lane; i < nf; i += 64) o[i] = 0.0f;
@@ -1615,6 +1655,8 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
       with_opp_rng(a, b, x.lane, R, [&](auto& G) { opponent_tower(S, u, x, G, a.difficulty); });
   }
   STAMP(12);
+  if constexpr (SMALL && SCAN) ord_r = ord_claim(a, ord_heavy, x.lane);
+  if constexpr (SMALL) ord_place(a, b, ord_heavy, ord_r, x.lane);
   // the towers and map[6] are final: cell words back to HBM if they changed, then
   // packed for the rest of the step (board_step reads the packed direction and distance)
   store_cells(S, u, x, a, b);
@@ -1769,8 +1811,8 @@ template <int LT, int MODE, bool SCAN, bool SMALL>
 __device__ __forceinline__ void step_kernel_body(const StepArgs& a) {
   constexpr int NC = LT ? LT * LT : MAX_KERNEL_L * MAX_KERNEL_L;
   __shared__ Smem<NC> S;
-  const int b = blockIdx.x;
-  if (b >= a.B) return;
+  if ((int)blockIdx.x >= a.B) return;
+  const int b = SMALL ? ord_board(a) : (int)blockIdx.x;
 #ifdef TD_STEP_PRIO  // A/B builds: step waves ahead of concurrent refill waves in issue arbitration
   __builtin_amdgcn_s_setprio(TD_STEP_PRIO);
 #endif
@@ -1834,8 +1876,8 @@ __global__ __launch_bounds__(128) TD_SMALL2_ATTR void td_step_kernel_small2(Step
   const StepArgs& a = kargs(a_);
   constexpr int NC = LT * LT;
   __shared__ Smem<NC> S;
-  const int b = blockIdx.x;
-  if (b >= a.B) return;
+  if ((int)blockIdx.x >= a.B) return;
+  const int b = ord_board(a);
   const int lane = (int)threadIdx.x & 63;
   if (threadIdx.x < 64) {
     stage_cfg(S, a.cfg);

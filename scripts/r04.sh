@@ -22,5 +22,18 @@ s1)  # host probe, the GPU suite on the ABI-3 build, smoke, the driver's command
     run b$bb 200 python bench.py --global-batch $bb --no-cpu-baseline --steps 2000 || exit 1; line b$bb
   done
   ;;
+s2)  # longest-work-first board order: GPU suite (every kernel), A/B at 8,192 / 4,096, phase stamps, timing-event flags
+  gpusuite 900; rc=$?; [ $rc -le 1 ] || exit $rc
+  for r in 1 2; do for o in 0 1; do for bb in 8192 4096; do
+    TD_ORDER=$o run o${o}_${bb}_$r 200 python bench.py --global-batch $bb --no-cpu-baseline --steps 2000 --timing none || exit 1; line o${o}_${bb}_$r
+  done; done; done
+  for o in 0 1; do
+    TD_ORDER=$o TDSTEP_LIB=$PWD/gym-td_amd/lib/libtdstep_stamps.so run phases_o${o}_8192 300 python scripts/probe_phases.py 8192 10 600 || exit 1
+    grep -E "rt |tail" $O/phases_o${o}_8192.log
+  done
+  for f in 0 1; do for bb in 65536 4096; do
+    TD_TEV_FLAGS=$f run tev${f}_$bb 200 python bench.py --global-batch $bb --no-cpu-baseline --steps $((bb > 10000 ? 200 : 2000)) || exit 1; line tev${f}_$bb
+  done; done
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac

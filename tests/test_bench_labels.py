@@ -96,3 +96,14 @@ def test_cpu_baseline_uses_every_core_of_the_affinity_mask():
     assert bench.host_cores() == len(os.sched_getaffinity(0))
     q = bench.cpu_quota()
     assert q is None or q > 0
+    threads, affinity, quota = bench.baseline_threads()
+    assert affinity == len(os.sched_getaffinity(0)) and quota == q
+    assert threads == (affinity if not q else max(1, min(affinity, int(q))))
+
+
+def test_baseline_note_states_cores_and_projection():
+    n = bench.baseline_note(8.0e6, 16, 256, 16.0)
+    assert n["affinity_cores"] == 256 and n["cpu_quota_cores"] == 16.0
+    assert n["value_per_core"] == 0.5e6
+    assert n["all_affinity_cores_projection"]["value"] == 128.0e6
+    assert "not measured" in n["all_affinity_cores_projection"]["note"]
