@@ -125,6 +125,8 @@ struct td_handle {
   uint32_t* d_ord_cnt = nullptr;
   int ord_stride = 0;
   int ord_on = 1;  // TD_ORDER=0: blocks step boards in index order (A/B runs)
+  int xcd_map = 1;  // XCD-contiguous board map (td_step.hip xcd_board; TD_XCD_MAP=0: block i = board i)
+  int edge_wt = 0;  // shared observation lines write-through (default: only without the XCD map; TD_EDGE_WT)
   long long ord_steps = 0;
 };
 
@@ -202,6 +204,8 @@ StepArgs base_args(td_handle* h) {
 #endif
   a.B = h->B; a.L = h->L; a.mode = h->mode; a.multi = h->multi; a.difficulty = h->difficulty;
   a.autoreset = h->autoreset;
+  a.xcd_map = h->xcd_map;
+  a.edge_wt = h->edge_wt;
   a.opp_np = h->opp_np;
   a.small = h->small;
   a.obs_wt = h->obs_wt;
@@ -416,13 +420,18 @@ td_handle* td_create(const td_config* cfg, int map_size, int n_boards, int mode,
   rc |= dalloc(&h->d_stage, (size_t)h->stage_cap * h->lw);
   rc |= dalloc(&h->d_epstats, 2);
   rc |= dalloc(&h->d_lastep, B);
+  if (const char* e = std::getenv("TD_XCD_MAP")) h->xcd_map = std::atoi(e) ? 1 : 0;  // A/B runs
+  h->edge_wt = h->xcd_map ? 0 : 1;
+  if (const char* e = std::getenv("TD_EDGE_WT")) h->edge_wt = std::atoi(e) ? 1 : 0;
   h->ord_stride = ord_stride(n_boards);
   rc |= dalloc(&h->d_ord, (size_t)2 * ORD_XCD * h->ord_stride);
   rc |= dalloc(&h->d_ord_cnt, (size_t)2 * ORD_CNT_WORDS);
-  if (!rc) {  // both lists start as the identity: block i steps board i
+  if (!rc) {  // both lists start as the board map: block i steps board xcd_board(i) (or i)
     std::vector<uint32_t> ord((size_t)2 * ORD_XCD * h->ord_stride, 0u);
     for (int i = 0; i < n_boards; ++i)
-      for (int p = 0; p < 2; ++p) ord[((size_t)p * ORD_XCD + i % ORD_XCD) * h->ord_stride + i / ORD_XCD] = (uint32_t)i;
+      for (int p = 0; p < 2; ++p)
+        ord[((size_t)p * ORD_XCD + i % ORD_XCD) * h->ord_stride + i / ORD_XCD] =
+            (uint32_t)(h->xcd_map ? xcd_board(i, n_boards) : i);
     if (hipMemcpy(h->d_ord, ord.data(), ord.size() * 4, hipMemcpyHostToDevice) != hipSuccess) rc = fail("order init");
   }
   if (const char* e = std::getenv("TD_ORDER")) h->ord_on = std::atoi(e) ? 1 : 0;  // A/B runs

@@ -70,6 +70,8 @@ struct StepArgs {
   // in the next step's order -- boards with enemies first -- through ord_cnt (ORD_CHUNKS
   // chunk counters per XCD, one 128-B line each: [0] heavy, [1] light).  ord_clr: the other
   // parity's counters, zeroed by block 0 for the step after this one.
+  int xcd_map;   // large kernel: block i steps board xcd_board(i, B) (else board i)
+  int edge_wt;   // observation lines shared with a neighbouring board stored write-through (write_obs_lines)
   const uint32_t* ord_in;
   uint32_t* ord_out;
   uint32_t* ord_cnt;
@@ -83,6 +85,17 @@ struct StepArgs {
 constexpr int ORD_XCD = 8, ORD_CHUNKS = 16, ORD_LINE = 32;
 constexpr int ORD_CNT_WORDS = ORD_XCD * ORD_CHUNKS * ORD_LINE;  // per parity
 __host__ __device__ inline int ord_stride(int B) { return (B + ORD_XCD - 1) / ORD_XCD; }
+
+// The XCD-contiguous board map: block i (XCD i % 8, slot i / 8) steps board
+// prefix(i % 8) + i / 8, so XCD x steps the contiguous range of boards after those of
+// XCDs 0 .. x-1.  Neighbouring boards then share an L2: the lines of the small per-board
+// arrays (header, hot record, reward, done, info) and the observation lines two boards
+// share are written whole by one XCD instead of in pieces by several.
+__host__ __device__ inline int xcd_board(int i, int B) {
+  const int x = i & (ORD_XCD - 1), q = B / ORD_XCD, r = B % ORD_XCD;
+  return x * q + (x < r ? x : r) + i / ORD_XCD;
+}
+
 
 // ev0 / ev1: optional timing events bound to the step kernel's dispatch (td_kernel_timing).
 hipError_t launch_step(const StepArgs& a, hipStream_t s, bool reset, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);

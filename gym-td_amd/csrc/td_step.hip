@@ -1065,8 +1065,13 @@ struct ObsWinTab {
 // PASS: 0 every window; 1 only the windows of binary planes alone (ObsWinTab class 0:
 // roads, end, starts, buildable, tower level / type -- final once the step's actions
 // are, td_step_kernel_small2 writes them early); 2 every other window.
+// edge_wt: the two lines the board shares with its neighbours go write-through (sc1): the
+// neighbours' waves run on other XCDs (board i on XCD i % 8); with the XCD-contiguous board
+// map (StepArgs::xcd_map) they share this XCD's L2, which merges the two halves, and the
+// lines go out like the whole ones.
 template <int NC, int LT, int KB = 0, int KE = -1, int G = 4, int PASS = 0>
-__device__ __forceinline__ void write_obs_lines(const Smem<NC>& S, int lane, float* out, bool any_enemy, bool wt) {
+__device__ __forceinline__ void write_obs_lines(const Smem<NC>& S, int lane, float* out, bool any_enemy, bool wt,
+                                                bool edge_wt = true) {
   static_assert(LT >= 8, "a 128-B line spans at most two channel planes");
   constexpr int Q = LT * LT / 4, N4 = NCH * Q;
   constexpr int K = KE >= 0 ? KE : (N4 + 7 + 63) / 64;  // windows [KB, K) of the board's (N4 + 7 + 63) / 64
@@ -1164,7 +1169,7 @@ __device__ __forceinline__ void write_obs_lines(const Smem<NC>& S, int lane, flo
       const uint32_t off = (uint32_t)i * 16u;  // i < 0 or i >= N4: out of range already
       if (wt) {  // wave-uniform
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, val), rs, off, 0, 16 /* sc1 */);
-      } else if (!edge) {  // whole lines of this board only
+      } else if (!edge || !edge_wt) {  // whole lines of this board only (or the neighbours share this L2)
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, val), rs, off, 0, 2 /* nt */);
       } else {
         const bool shared = i < head || i >= tail;  // a line shared with a neighbouring board
@@ -1537,7 +1542,7 @@ constexpr int obs_late_half() {
 // returning atomic, issued once its header is in and consumed phases later.
 __device__ __forceinline__ int ord_board(const StepArgs& a) {
   const int i = (int)blockIdx.x;
-  if (!a.ord_in) return i;
+  if (!a.ord_in) return a.xcd_map ? xcd_board(i, a.B) : i;
   return (int)a.ord_in[(i & (ORD_XCD - 1)) * a.ord_stride + i / ORD_XCD];
 }
 __device__ __forceinline__ int ord_line(int i) {
@@ -1769,12 +1774,12 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
     // half of the windows the early pass left.
     if (x.lane == 0) { S.obs_go = was_reset ? 2u : 1u; S.obs_any = u.n > 0 ? 1u : 0u; }
     __syncthreads();
-    if (was_reset) write_obs_lines<NC, LT>(S, x.lane, obs, u.n > 0, wt);
-    else write_obs_lines<NC, LT, 0, obs_late_half<LT>(), 4, 2>(S, x.lane, obs, u.n > 0, wt);
+    if (was_reset) write_obs_lines<NC, LT>(S, x.lane, obs, u.n > 0, wt, a.edge_wt != 0);
+    else write_obs_lines<NC, LT, 0, obs_late_half<LT>(), 4, 2>(S, x.lane, obs, u.n > 0, wt, a.edge_wt != 0);
   } else if constexpr (LT != 0) {
     if ((reinterpret_cast<uintptr_t>(a.obs) & 15u) == 0) {
 #ifndef TD_DIAG_NO_OBS  // diagnostic builds only: the step without its observation
-      write_obs_lines<NC, LT>(S, x.lane, obs, u.n > 0, wt);
+      write_obs_lines<NC, LT>(S, x.lane, obs, u.n > 0, wt, a.edge_wt != 0);
 #endif
     } else {
       write_obs<NC, LT>(S, x, obs, u.n > 0);
@@ -1812,7 +1817,7 @@ __device__ __forceinline__ void step_kernel_body(const StepArgs& a) {
   constexpr int NC = LT ? LT * LT : MAX_KERNEL_L * MAX_KERNEL_L;
   __shared__ Smem<NC> S;
   if ((int)blockIdx.x >= a.B) return;
-  const int b = SMALL ? ord_board(a) : (int)blockIdx.x;
+  const int b = SMALL ? ord_board(a) : a.xcd_map ? xcd_board((int)blockIdx.x, a.B) : (int)blockIdx.x;
 #ifdef TD_STEP_PRIO  // A/B builds: step waves ahead of concurrent refill waves in issue arbitration
   __builtin_amdgcn_s_setprio(TD_STEP_PRIO);
 #endif
@@ -1889,13 +1894,14 @@ __global__ __launch_bounds__(128) TD_SMALL2_ATTR void td_step_kernel_small2(Step
     float* const obs = a.obs + (size_t)b * NCH * NC;
     __syncthreads();  // (A) actions and towers final, cells packed
     if (S.early_go) {
-      write_obs_lines<NC, LT, 0, -1, 4, 1>(S, lane, obs, false, a.obs_wt != 0);
+      write_obs_lines<NC, LT, 0, -1, 4, 1>(S, lane, obs, false, a.obs_wt != 0, a.edge_wt != 0);
       // landed before (B): after an auto-reset the first wave rewrites these windows
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();  // (B)
     if (S.obs_go == 1u)
-      write_obs_lines<NC, LT, obs_late_half<LT>(), -1, 4, 2>(S, lane, obs, S.obs_any != 0u, a.obs_wt != 0);
+      write_obs_lines<NC, LT, obs_late_half<LT>(), -1, 4, 2>(S, lane, obs, S.obs_any != 0u, a.obs_wt != 0,
+                                                            a.edge_wt != 0);
   }
 }
 

@@ -22,11 +22,19 @@ s1)  # host probe, the GPU suite on the ABI-3 build, smoke, the driver's command
     run b$bb 200 python bench.py --global-batch $bb --no-cpu-baseline --steps 2000 || exit 1; line b$bb
   done
   ;;
-s2)  # longest-work-first board order: GPU suite (every kernel), A/B at 8,192 / 4,096, phase stamps, timing-event flags
+s2)  # board order + XCD map: GPU suite (every kernel), A/B at 8,192 / 4,096 / 65,536, PMC bytes, phase stamps, timing-event flags
   gpusuite 900; rc=$?; [ $rc -le 1 ] || exit $rc
-  for r in 1 2; do for o in 0 1; do for bb in 8192 4096; do
-    TD_ORDER=$o run o${o}_${bb}_$r 200 python bench.py --global-batch $bb --no-cpu-baseline --steps 2000 --timing none || exit 1; line o${o}_${bb}_$r
-  done; done; done
+  for r in 1 2; do
+    for v in "1 1" "0 1" "0 0"; do set -- $v; for bb in 8192 4096; do
+      TD_ORDER=$1 TD_XCD_MAP=$2 run o$1x$2_${bb}_$r 200 python bench.py --global-batch $bb --no-cpu-baseline --steps 2000 --timing none || exit 1; line o$1x$2_${bb}_$r
+    done; done
+    for x in 1 0; do
+      TD_XCD_MAP=$x run x${x}_65536_$r 200 python bench.py --no-cpu-baseline --steps 300 --timing none || exit 1; line x${x}_65536_$r
+    done
+  done
+  for x in 1 0; do for bb in 65536 8192; do
+    OUT=$O/pmc NAME=x${x}_$bb B=$bb TD_XCD_MAP=$x run pmc_x${x}_$bb 600 bash scripts/pmc_ab.sh || exit 1; tail -1 $O/pmc_x${x}_$bb.log
+  done; done
   for o in 0 1; do
     TD_ORDER=$o TDSTEP_LIB=$PWD/gym-td_amd/lib/libtdstep_stamps.so run phases_o${o}_8192 300 python scripts/probe_phases.py 8192 10 600 || exit 1
     grep -E "rt |tail" $O/phases_o${o}_8192.log
