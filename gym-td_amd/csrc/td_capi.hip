@@ -914,6 +914,10 @@ static int state_copy(td_handle* h, int b0, int count, void* host, bool to_host)
     for (size_t i = 0; i < (size_t)count * ECAP; ++i) einf[i] = (einf[i] & 0x00ffffffu) | ((uint32_t)h->epoch << 24);
     for (size_t i = 0; i < (size_t)count * TCAP; ++i)
       tinf[i] = (tinf[i] & 0x0000ffffu) | ((uint32_t)h->epoch << 16) | ((uint32_t)h->epoch << 24);
+    // cell words: bits 10-15 are not part of the layout format (the step keeps the tower of a
+    // cell there in LDS only)
+    uint32_t* cw = (uint32_t*)(q + (size_t)count * (sizeof(TdHdr) + ECAP * 20 + TCAP * 12));
+    for (size_t i = 0; i < (size_t)count * h->NC; ++i) cw[i] &= ~(0x3Fu << 10);
     p = q;
     opp = (uint32_t*)(p + (size_t)count * (sizeof(TdHdr) + ECAP * 20 + TCAP * 12 + (size_t)h->NC * 4));
   }

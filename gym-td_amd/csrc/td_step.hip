@@ -50,8 +50,7 @@ enum : int { FC_OK = 0, FC_COST = 1, FC_POS = 2, FC_LVMAX = 3, FC_TARGET = 4, FC
 template <int NC>
 struct alignas(16) Smem {
   static_assert(NC % 4 == 0, "cell and tower maps are moved in 16-B / 4-B units");
-  uint32_t cell[NC];      // cell words (td_layout.h)
-  uint8_t twr[NC];        // tower at cell: 0 none, else 0x80 | lv << 2 | type
+  uint32_t cell[NC];      // cell words (td_layout.h), + the tower on the cell in bits 10-13 (tw_nib)
   uint8_t grp[4][NC];     // enemy group (head enemy index) per (type, cell), 0xFF none
   union {
     struct {              // load .. march: the enemy list (written back right after the march)
@@ -78,6 +77,22 @@ struct alignas(16) Smem {
   uint32_t early_go;         // td_step_kernel_small2: the binary-plane windows may be written early
   TdDevCfg cfg;           // constant block, staged once per board: per-lane table lookups hit LDS
 };
+
+// The tower on a cell lives in the LDS copy of its cell word, bits 10-13 (unused by the
+// layout format, td_layout.h): bit 3 of the nibble = a tower, bit 2 its level, bits 0-1
+// its type.  (A byte map of its own cost NC bytes of LDS per board: 900 at 30x30, where the
+// board image bounds residency.)  HBM cell words never carry it (store_cells masks it).
+constexpr uint32_t kTwBits = 0xFu << 10;
+__device__ __forceinline__ uint32_t tw_nib(int lv, int type) { return (0x8u | ((uint32_t)lv << 2) | (uint32_t)type) << 10; }
+// the tower byte of a cell word: 0 none, else 0x80 | lv << 2 | type
+__device__ __forceinline__ uint32_t twr_of(uint32_t w) {
+  const uint32_t n = (w >> 10) & 0xFu;
+  return (n & 8u) ? (0x80u | (n & 7u)) : 0u;
+}
+template <int NC>
+__device__ __forceinline__ void set_tower(Smem<NC>& S, int cell, uint32_t nib) {
+  S.cell[cell] = (S.cell[cell] & ~kTwBits) | nib;
+}
 
 // Stage the constant block into LDS (16 bytes per lane).
 template <int NC>
@@ -293,7 +308,7 @@ __device__ __forceinline__ int tower_build(Smem<NC>& S, U& u, const Ctx& x, int 
   if (x.lane == 0) {
     S.tInf[u.nt] = tw_pack(cell, t, 0, x.ep, x.ep);
     S.tCd[u.nt] = 0.0;
-    S.twr[cell] = (uint8_t)(0x80 | t);
+    set_tower(S, cell, tw_nib(0, t));
   }
   u.nt += 1;
   u.cost_def = dsub(u.cost_def, price);                   // :238
@@ -322,7 +337,7 @@ __device__ __forceinline__ int tower_lvup(Smem<NC>& S, U& u, const Ctx& x, int c
   wsync();
   if (x.lane == 0) {
     S.tInf[k] = tw_pack(cell, t, lv + 1, tw_ec(ti), x.ep);
-    S.twr[cell] = (uint8_t)(0x80 | ((lv + 1) << 2) | t);
+    set_tower(S, cell, tw_nib(lv + 1, t));
   }
   u.cost_def = dsub(u.cost_def, price);                   // :266
   wsync();
@@ -349,7 +364,7 @@ __device__ __forceinline__ int tower_destruct(Smem<NC>& S, U& u, const Ctx& x, i
   if (j >= k && j + 1 < u.nt) { vi = S.tInf[j + 1]; vc = S.tCd[j + 1]; }
   wsync();
   if (j >= k && j + 1 < u.nt) { S.tInf[j] = vi; S.tCd[j] = vc; }
-  if (x.lane == 0) S.twr[cell] = 0;
+  if (x.lane == 0) set_tower(S, cell, 0u);
   u.nt -= 1;
   wsync();
   diamond(S, x, cell, -1);                                // :281-287
@@ -426,7 +441,7 @@ __device__ __forceinline__ void defender_scan(Smem<NC>& S, U& u, const Ctx& x, c
       bool cand = false;
       if (valid && fl && x.lane > last) {
         uint32_t w = S.cell[cell];
-        uint32_t tw = S.twr[cell];
+        uint32_t tw = twr_of(w);
         bool canb = false;
         if (cw_block(w) == 0) {
 #pragma unroll
@@ -908,7 +923,7 @@ template <int NC>
 __device__ __forceinline__ void pack_obs_cells(Smem<NC>& S, const Ctx& x) {
   for (int i = x.lane; i < x.NCr; i += 64) {
     const uint32_t w = S.cell[i];
-    S.cell[i] = cell_bits(w, S.twr[i]) | ((uint32_t)cw_dir(w) << 21) | ((uint32_t)cw_dist(w) << 24);
+    S.cell[i] = cell_bits(w, twr_of(w)) | ((uint32_t)cw_dir(w) << 21) | ((uint32_t)cw_dist(w) << 24);
   }
   wsync();
 }
@@ -1259,13 +1274,10 @@ __device__ __forceinline__ void load_board(Smem<NC>& S, U& u, const Ctx& x, cons
       const int i = 64 * (k + 1) + x.lane;
       if (i < n4) s4[i] = r[k];
     }
-    uint32_t* t4 = reinterpret_cast<uint32_t*>(S.twr);  // NC % 4 == 0
-    for (int i = x.lane; i < n4; i += 64) t4[i] = 0u;
   } else {
     if (x.lane < x.NCr) S.cell[x.lane] = P.c4.x;
     if (x.lane + 64 < x.NCr) S.cell[x.lane + 64] = P.c4.y;
     for (int i = 128 + x.lane; i < x.NCr; i += 64) S.cell[i] = a.cells[cb + i];
-    for (int i = x.lane; i < x.NCr; i += 64) S.twr[i] = 0;
   }
   // TdHdr words (td_common.h): 0-5 cost_def, cost_atk, ep_return; 6 steps, 7 base_LP,
   // 8 atk_cd, 9 def_cd, 10 n_en, 11 n_tw, 12 num_roads, 13 end_cell, 14-16 start_cell,
@@ -1294,8 +1306,8 @@ __device__ __forceinline__ void load_board(Smem<NC>& S, U& u, const Ctx& x, cons
     S.tInf[x.lane] = tinf;
   }
   wsync();
-  if (x.lane < u.nt)
-    S.twr[tinf & 0xfffu] = (uint8_t)(0x80u | (((tinf >> 14) & 1u) << 2) | ((tinf >> 12) & 3u));
+  if (x.lane < u.nt)  // (one tower per cell: no two lanes share a word)
+    S.cell[tinf & 0xfffu] |= tw_nib((int)((tinf >> 14) & 1u), (int)((tinf >> 12) & 3u));
   wsync();
 }
 
@@ -1306,7 +1318,7 @@ __device__ __forceinline__ void reset_board(Smem<NC>& S, U& u, const Ctx& x, con
   // vector loads only (lane-indexed, then readlane): a record handed over by a
   // concurrently running refill must not come through the scalar cache
   const uint32_t hw = rec[x.lane & (LAYOUT_HDR - 1)];
-  for (int i = x.lane; i < x.NCr; i += 64) { S.cell[i] = rec[LAYOUT_HDR + i]; S.twr[i] = 0; }
+  for (int i = x.lane; i < x.NCr; i += 64) S.cell[i] = rec[LAYOUT_HDR + i];
   u.num_roads = (int)rdl(hw, 1); u.end_cell = (int)rdl(hw, 2); u.maxdist = (int)rdl(hw, 3);
   u.set_starts(rdl(hw, 4), rdl(hw, 5), rdl(hw, 6));
   u.cost_def = C.def_init_cost; u.cost_atk = C.atk_init_cost;
@@ -1323,7 +1335,7 @@ template <int NC>
 __device__ __forceinline__ void store_cells(const Smem<NC>& S, const U& u, const Ctx& x, const StepArgs& a, int b) {
   const size_t cb = (size_t)b * x.NCr;
   if (u.cells_dirty)
-    for (int i = x.lane; i < x.NCr; i += 64) sst(&a.cells[cb + i], S.cell[i]);
+    for (int i = x.lane; i < x.NCr; i += 64) sst(&a.cells[cb + i], S.cell[i] & ~kTwBits);
 }
 
 template <int NC>

@@ -39,6 +39,7 @@ s2)  # board order + XCD map: GPU suite (every kernel), A/B at 8,192 / 4,096 / 6
     TD_ORDER=$o TDSTEP_LIB=$PWD/gym-td_amd/lib/libtdstep_stamps.so run phases_o${o}_8192 300 python scripts/probe_phases.py 8192 10 600 || exit 1
     grep -E "rt |tail" $O/phases_o${o}_8192.log
   done
+  run large30 300 python bench.py --workload def-large --global-batch 16384 --no-cpu-baseline --steps 200 || exit 1; line large30
   for f in 0 1; do for bb in 65536 4096; do
     TD_TEV_FLAGS=$f run tev${f}_$bb 200 python bench.py --global-batch $bb --no-cpu-baseline --steps $((bb > 10000 ? 200 : 2000)) || exit 1; line tev${f}_$bb
   done; done
