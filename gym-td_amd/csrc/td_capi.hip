@@ -234,10 +234,29 @@ void parallel_for(int n, F fn) {
   for (auto& t : pool) t.join();
 }
 
+// The board-order lists of the small kernels (td_step.hip ord_*) for the kernel now chosen:
+// both start as the board map (virtual block vb steps board xcd_board_v(vb) -- or vb
+// without the XCD map -- with the kernel's boards per workgroup), the chunk counters at
+// zero.  Called with the device idle (td_create, td_set_step_kernel).
+int ord_init(td_handle* h) {
+  const int bpw = h->small == 1 ? kSmallBPW : 1;
+  std::vector<uint32_t> ord((size_t)2 * ORD_XCD * h->ord_stride, 0u);
+  for (int vb = 0; vb < h->B; ++vb) {
+    int x, slot;
+    ord_pos(vb, bpw, x, slot);
+    const uint32_t b = (uint32_t)(h->xcd_map ? xcd_board_v(vb, h->B, bpw) : vb);
+    for (int p = 0; p < 2; ++p) ord[((size_t)p * ORD_XCD + x) * h->ord_stride + slot] = b;
+  }
+  HIP_OK(hipMemcpy(h->d_ord, ord.data(), ord.size() * 4, hipMemcpyHostToDevice));
+  HIP_OK(hipMemset(h->d_ord_cnt, 0, (size_t)2 * ORD_CNT_WORDS * 4));
+  h->ord_steps = 0;
+  return 0;
+}
+
 // The step kernel (td_set_step_kernel): small = 0 large, 1 small, 2 small2.  Write-through
 // observation stores go with the small kernels where the batch's observation fits the
 // 256-MiB Infinity Cache (scripts/storepol.hip: 21.8 vs 30.0 us at 8,192 boards).
-void apply_kernel(td_handle* h, int small) {
+int apply_kernel(td_handle* h, int small) {
   h->small = small;
   const double obs_bytes = (double)h->B * NCH * h->NC * 4.0;
   // (Write-through beyond the Infinity Cache -- any kernel, TD_OBS_WT=1 -- measured 1.5-1.7x
@@ -249,6 +268,7 @@ void apply_kernel(td_handle* h, int small) {
   char buf[96];
   std::snprintf(buf, sizeof buf, "%s<%d, %d, %s>", k, has_small ? h->L : 0, h->mode, h->multi ? "true" : "false");
   h->kernel_name = buf;
+  return ord_init(h);
 }
 
 // Drop staged layouts: they were drawn from a stream that has been replaced.
@@ -426,14 +446,6 @@ td_handle* td_create(const td_config* cfg, int map_size, int n_boards, int mode,
   h->ord_stride = ord_stride(n_boards);
   rc |= dalloc(&h->d_ord, (size_t)2 * ORD_XCD * h->ord_stride);
   rc |= dalloc(&h->d_ord_cnt, (size_t)2 * ORD_CNT_WORDS);
-  if (!rc) {  // both lists start as the board map: block i steps board xcd_board(i) (or i)
-    std::vector<uint32_t> ord((size_t)2 * ORD_XCD * h->ord_stride, 0u);
-    for (int i = 0; i < n_boards; ++i)
-      for (int p = 0; p < 2; ++p)
-        ord[((size_t)p * ORD_XCD + i % ORD_XCD) * h->ord_stride + i / ORD_XCD] =
-            (uint32_t)(h->xcd_map ? xcd_board(i, n_boards) : i);
-    if (hipMemcpy(h->d_ord, ord.data(), ord.size() * 4, hipMemcpyHostToDevice) != hipSuccess) rc = fail("order init");
-  }
   if (const char* e = std::getenv("TD_ORDER")) h->ord_on = std::atoi(e) ? 1 : 0;  // A/B runs
   if (rc) {  // name the footprint (the staged-layout rings are most of it at large L)
     const double ring = (double)B * NSLOT * slot_words(map_size) * 4.0;
@@ -500,7 +512,7 @@ td_handle* td_create(const td_config* cfg, int map_size, int n_boards, int mode,
     const int resident2 = step_resident_boards(base_args(h), cus, 2);
     const int rounds2 = h->multi ? 0 : h->L == 10 ? 3 : h->L == 30 ? 10 : 0;  // two-wave kernel up to this many rounds
     h->small_auto = n_boards <= resident2 ? 2 : n_boards <= resident ? 1 : n_boards <= rounds2 * resident ? 2 : 0;
-    apply_kernel(h, h->small_auto);
+    if (apply_kernel(h, h->small_auto)) { std::string e = g_err; td_destroy(h); g_err = e; return nullptr; }
     if (const char* e = std::getenv("TD_REFILL_EVERY")) h->refill_every = std::max(0, std::atoi(e));  // A/B runs
     if (const char* e = std::getenv("TD_REFILL_WAVES")) h->refill_waves = std::max(1, std::atoi(e));
     if (const char* e = std::getenv("TD_REFILL_WALKS")) h->refill_walks = std::max(1, std::atoi(e));
@@ -795,8 +807,7 @@ int td_set_step_kernel(td_handle* h, int kind) {
   if (kind >= TD_KERNEL_SMALL && h->L != 10 && h->L != 20 && h->L != 30)
     return fail("td_set_step_kernel: L = %d has no small-batch step kernel (only L = 10 / 20 / 30)", h->L);
   HIP_OK(hipDeviceSynchronize());  // launches already queued keep the kernel they were enqueued with
-  apply_kernel(h, kind == TD_KERNEL_AUTO ? h->small_auto : kind - 1);
-  return 0;
+  return apply_kernel(h, kind == TD_KERNEL_AUTO ? h->small_auto : kind - 1);
 }
 
 int td_step_kernel(td_handle* h) { return h ? h->small + 1 : fail("NULL handle"); }

@@ -84,7 +84,42 @@ struct StepArgs {
 // than B / 8 / ORD_CHUNKS returning atomics per step.
 constexpr int ORD_XCD = 8, ORD_CHUNKS = 16, ORD_LINE = 32;
 constexpr int ORD_CNT_WORDS = ORD_XCD * ORD_CHUNKS * ORD_LINE;  // per parity
-__host__ __device__ inline int ord_stride(int B) { return (B + ORD_XCD - 1) / ORD_XCD; }
+
+// Boards per workgroup of td_step_kernel_small (one wave each; TD_BPW A/B builds): a
+// one-round grid of B boards then has B / BPW workgroups to dispatch.  Board slots are
+// "virtual blocks" vb = workgroup * BPW + wave: XCD (vb / BPW) % 8, slot
+// (vb / BPW / 8) * BPW + vb % BPW of that XCD's list.
+#ifndef TD_BPW
+#define TD_BPW 1
+#endif
+constexpr int kSmallBPW = TD_BPW;
+__host__ __device__ inline void ord_pos(int vb, int bpw, int& xcd, int& slot) {
+  const int blk = vb / bpw;
+  xcd = blk & (ORD_XCD - 1);
+  slot = (blk / ORD_XCD) * bpw + vb % bpw;
+}
+// Slots of XCD x's list: every workgroup on XCD x holds bpw boards but the grid's last one.
+__host__ __device__ inline int ord_nx(int x, int B, int bpw) {
+  const int nb = (B + bpw - 1) / bpw;
+  if (x >= nb) return 0;
+  const int nbx = (nb - 1 - x) / ORD_XCD + 1;
+  return nbx * bpw - (((nb - 1) & (ORD_XCD - 1)) == x ? nb * bpw - B : 0);
+}
+// Words per XCD list: the longest list (ord_nx), for either boards-per-workgroup count.
+__host__ __device__ inline int ord_stride(int B) {
+  const int nb = (B + kSmallBPW - 1) / kSmallBPW;
+  const int a = (nb + ORD_XCD - 1) / ORD_XCD * kSmallBPW, b1 = (B + ORD_XCD - 1) / ORD_XCD;
+  return a > b1 ? a : b1;
+}
+// The XCD-contiguous board of virtual block vb: XCD x's slots hold the boards after those
+// of XCDs 0 .. x-1 (for bpw = 1 the same map as xcd_board).
+__host__ __device__ inline int xcd_board_v(int vb, int B, int bpw) {
+  int x, slot;
+  ord_pos(vb, bpw, x, slot);
+  int pre = 0;
+  for (int y = 0; y < x; ++y) pre += ord_nx(y, B, bpw);
+  return pre + slot;
+}
 
 // The XCD-contiguous board map: block i (XCD i % 8, slot i / 8) steps board
 // prefix(i % 8) + i / 8, so XCD x steps the contiguous range of boards after those of

@@ -1552,28 +1552,29 @@ constexpr int obs_late_half() {
 // head instead of anywhere in it.  Each board claims its slot in the next step's list of
 // the same XCD (heavy from the front, light from the back of its chunk) with one
 // returning atomic, issued once its header is in and consumed phases later.
-__device__ __forceinline__ int ord_board(const StepArgs& a) {
-  const int i = (int)blockIdx.x;
-  if (!a.ord_in) return a.xcd_map ? xcd_board(i, a.B) : i;
-  return (int)a.ord_in[(i & (ORD_XCD - 1)) * a.ord_stride + i / ORD_XCD];
-}
-__device__ __forceinline__ int ord_line(int i) {
-  return ((i & (ORD_XCD - 1)) * ORD_CHUNKS + (i / ORD_XCD) % ORD_CHUNKS) * ORD_LINE;
+__device__ __forceinline__ int ord_board(const StepArgs& a, int vb, int bpw) {
+  int xcd, slot;
+  ord_pos(vb, bpw, xcd, slot);
+  if (!a.ord_in) return !a.xcd_map ? vb : bpw == 1 ? xcd_board(vb, a.B) : xcd_board_v(vb, a.B, bpw);
+  return (int)a.ord_in[xcd * a.ord_stride + slot];
 }
 // Claim: heavy = the board has enemies now (its next step will: enemies live tens of steps).
-__device__ __forceinline__ uint32_t ord_claim(const StepArgs& a, bool heavy, int lane) {
+__device__ __forceinline__ uint32_t ord_claim(const StepArgs& a, bool heavy, int lane, int vb, int bpw) {
   uint32_t r = 0;
   if (!a.ord_in) return r;
-  const int i = (int)blockIdx.x;
-  if (lane == 0) r = atomicAdd(a.ord_cnt + ord_line(i) + (heavy ? 0 : 1), 1u);
-  if (i == 0)  // the other parity's counters start the step after this one at zero
+  int xcd, slot;
+  ord_pos(vb, bpw, xcd, slot);
+  if (lane == 0) r = atomicAdd(a.ord_cnt + (xcd * ORD_CHUNKS + slot % ORD_CHUNKS) * ORD_LINE + (heavy ? 0 : 1), 1u);
+  if (vb == 0)  // the other parity's counters start the step after this one at zero
     for (int w = lane; w < ORD_XCD * ORD_CHUNKS; w += 64) { a.ord_clr[w * ORD_LINE] = 0u; a.ord_clr[w * ORD_LINE + 1] = 0u; }
   return r;
 }
-__device__ __forceinline__ void ord_place(const StepArgs& a, int b, bool heavy, uint32_t r, int lane) {
+__device__ __forceinline__ void ord_place(const StepArgs& a, int b, bool heavy, uint32_t r, int lane, int vb, int bpw) {
   if (!a.ord_in || lane != 0) return;
-  const int i = (int)blockIdx.x, xcd = i & (ORD_XCD - 1), c = (i / ORD_XCD) % ORD_CHUNKS;
-  const int nx = (a.B - 1 - xcd) / ORD_XCD + 1;               // slots of this XCD's list
+  int xcd, slot;
+  ord_pos(vb, bpw, xcd, slot);
+  const int c = slot % ORD_CHUNKS;
+  const int nx = ord_nx(xcd, a.B, bpw);                        // slots of this XCD's list
   const int cs = (nx - c + ORD_CHUNKS - 1) / ORD_CHUNKS;       // of them in chunk c
   const int pos = heavy ? (int)r : cs - 1 - (int)r;
   a.ord_out[xcd * a.ord_stride + c + ORD_CHUNKS * pos] = (uint32_t)b;
@@ -1582,8 +1583,9 @@ __device__ __forceinline__ void ord_place(const StepArgs& a, int b, bool heavy, 
 // SPLIT: the board's workgroup has a second wave (td_step_kernel_small2) that waits at
 // the one workgroup barrier of this path and then writes the second half of the
 // observation windows.
-template <int NC, int LT, int MODE, bool SCAN, bool SMALL, bool SPLIT = false>
-__device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const StepArgs& a, int b, const Prefetch& P) {
+template <int NC, int LT, int MODE, bool SCAN, bool SMALL, bool SPLIT = false, int BPW = 1>
+__device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const StepArgs& a, int b, const Prefetch& P,
+                                           int vb) {
   const TdDevCfg& C = x.C;
   uint32_t* const opp = a.opp_mt + (size_t)b * OPP_WORDS;
   uint32_t* const hot = a.opp_hot + (size_t)b * HOT_WORDS;
@@ -1594,7 +1596,7 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
   load_board<NC, PF, PF>(S, u, x, a, b, P);
   const bool ord_heavy = u.n > 0;
   // (the multi-action scan has no register to hold the claim across it: claimed at the place)
-  uint32_t ord_r = SMALL && !SCAN ? ord_claim(a, ord_heavy, x.lane) : 0u;
+  uint32_t ord_r = SMALL && !SCAN ? ord_claim(a, ord_heavy, x.lane, vb, BPW) : 0u;
   const int64_t act_in = (int64_t)(((uint64_t)lane_word(P.w, PF_ACT + 1) << 32) | lane_word(P.w, PF_ACT));
   // built-in opponent stream: position, lazy-twist boundary and the next draws
   // (pre-computed by the previous step) come from the board's hot record
@@ -1605,8 +1607,8 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
   STAMP(1);
   if (u.num_roads < 1 || u.num_roads > 3) {
     // never reset (its road generation failed): nothing to step
-    if constexpr (SMALL && SCAN) ord_r = ord_claim(a, ord_heavy, x.lane);
-    if constexpr (SMALL) ord_place(a, b, ord_heavy, ord_r, x.lane);
+    if constexpr (SMALL && SCAN) ord_r = ord_claim(a, ord_heavy, x.lane, vb, BPW);
+    if constexpr (SMALL) ord_place(a, b, ord_heavy, ord_r, x.lane, vb, BPW);
     const int nf = NCH * x.NCr;
     float* o = a.obs + (size_t)b * nf;
     for (int i = x.lane; i < nf; i += 64) o[i] = 0.0f;
@@ -1672,8 +1674,8 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
       with_opp_rng(a, b, x.lane, R, [&](auto& G) { opponent_tower(S, u, x, G, a.difficulty); });
   }
   STAMP(12);
-  if constexpr (SMALL && SCAN) ord_r = ord_claim(a, ord_heavy, x.lane);
-  if constexpr (SMALL) ord_place(a, b, ord_heavy, ord_r, x.lane);
+  if constexpr (SMALL && SCAN) ord_r = ord_claim(a, ord_heavy, x.lane, vb, BPW);
+  if constexpr (SMALL) ord_place(a, b, ord_heavy, ord_r, x.lane, vb, BPW);
   // the towers and map[6] are final: cell words back to HBM if they changed, then
   // packed for the rest of the step (board_step reads the packed direction and distance)
   store_cells(S, u, x, a, b);
@@ -1827,19 +1829,23 @@ __device__ __forceinline__ const StepArgs& kargs(const StepArgs& a) {
 template <int LT, int MODE, bool SCAN, bool SMALL>
 __device__ __forceinline__ void step_kernel_body(const StepArgs& a) {
   constexpr int NC = LT ? LT * LT : MAX_KERNEL_L * MAX_KERNEL_L;
-  __shared__ Smem<NC> S;
-  if ((int)blockIdx.x >= a.B) return;
-  const int b = SMALL ? ord_board(a) : a.xcd_map ? xcd_board((int)blockIdx.x, a.B) : (int)blockIdx.x;
+  constexpr int BPW = SMALL ? kSmallBPW : 1;  // boards (waves) per workgroup
+  __shared__ Smem<NC> SS[BPW];
+  const int w = BPW > 1 ? (int)(threadIdx.x >> 6) : 0;
+  const int vb = (int)blockIdx.x * BPW + w;  // the board slot of this wave
+  if (vb >= a.B) return;
+  Smem<NC>& S = SS[w];
+  const int b = SMALL ? ord_board(a, vb, BPW) : a.xcd_map ? xcd_board(vb, a.B) : vb;
 #ifdef TD_STEP_PRIO  // A/B builds: step waves ahead of concurrent refill waves in issue arbitration
   __builtin_amdgcn_s_setprio(TD_STEP_PRIO);
 #endif
   stage_cfg(S, a.cfg);
   const int L = LT ? LT : a.L;
-  const Ctx x{S.cfg, L, L * L, (int)threadIdx.x, a.cfgs, a.epoch};
+  const Ctx x{S.cfg, L, L * L, (int)(threadIdx.x & 63), a.cfgs, a.epoch};
   Prefetch P;
   constexpr int PF = SMALL ? PF_SMALL : PF_LARGE;
   prefetch_issue<PF, PF>(P, a, b, x.lane, x.NCr, MODE != MODE_ATK && !a.multi);
-  step_board<NC, LT, MODE, SCAN, SMALL>(S, x, a, b, P);
+  step_board<NC, LT, MODE, SCAN, SMALL, false, BPW>(S, x, a, b, P, vb);
 }
 
 // Large batches (several rounds of waves, HBM-write bound): 6 waves per SIMD at
@@ -1880,7 +1886,7 @@ constexpr int small2_cap() { return LT == 20 && SCAN ? 5 : LT == 20 && MODE == M
 #define TD_SMALL2_ATTR __attribute__((amdgpu_waves_per_eu(small2_cap<LT, MODE, SCAN>(), small2_cap<LT, MODE, SCAN>())))
 #endif
 template <int LT, int MODE, bool SCAN>
-__global__ __launch_bounds__(64) TD_SMALL_ATTR void td_step_kernel_small(StepArgs a) {
+__global__ __launch_bounds__(64 * kSmallBPW) TD_SMALL_ATTR void td_step_kernel_small(StepArgs a) {
   step_kernel_body<LT, MODE, SCAN, true>(kargs(a));
 }
 
@@ -1894,14 +1900,14 @@ __global__ __launch_bounds__(128) TD_SMALL2_ATTR void td_step_kernel_small2(Step
   constexpr int NC = LT * LT;
   __shared__ Smem<NC> S;
   if ((int)blockIdx.x >= a.B) return;
-  const int b = ord_board(a);
+  const int b = ord_board(a, (int)blockIdx.x, 1);
   const int lane = (int)threadIdx.x & 63;
   if (threadIdx.x < 64) {
     stage_cfg(S, a.cfg);
     const Ctx x{S.cfg, LT, NC, lane, a.cfgs, a.epoch};
     Prefetch P;
     prefetch_issue<PF_SMALL, PF_SMALL>(P, a, b, lane, NC, MODE != MODE_ATK && !a.multi);
-    step_board<NC, LT, MODE, SCAN, true, true>(S, x, a, b, P);
+    step_board<NC, LT, MODE, SCAN, true, true>(S, x, a, b, P, (int)blockIdx.x);
   } else {
     float* const obs = a.obs + (size_t)b * NCH * NC;
     __syncthreads();  // (A) actions and towers final, cells packed
@@ -2350,18 +2356,25 @@ static hipError_t launch2(const StepArgs& a, hipStream_t s, bool reset, hipEvent
     if (ev0) hipExtLaunchKernelGGL(k, dim3(a.B), dim3(128), 0, s, ev0, ev1, 0, a);       \
     else hipLaunchKernelGGL(k, dim3(a.B), dim3(128), 0, s, a);                           \
   } while (0)
+#define TD_LAUNCHS(k)                                                                                      \
+  do {                                                                                                     \
+    const dim3 g((a.B + kSmallBPW - 1) / kSmallBPW), t(64 * kSmallBPW);                                    \
+    if (ev0) hipExtLaunchKernelGGL(k, g, t, 0, s, ev0, ev1, 0, a);                                         \
+    else hipLaunchKernelGGL(k, g, t, 0, s, a);                                                             \
+  } while (0)
   const bool aligned = (reinterpret_cast<uintptr_t>(a.obs) & 15u) == 0;
   if (reset) {
     hipLaunchKernelGGL(td_reset_kernel<LT>, dim3(a.B), dim3(64), 0, s, a);
   } else if constexpr (LT != 0) {
     if (a.small == 2 && aligned) TD_STEP_DISPATCH(td_step_kernel_small2, LT, a, TD_LAUNCH2);
-    else if (a.small && aligned) TD_STEP_DISPATCH(td_step_kernel_small, LT, a, TD_LAUNCH);
+    else if (a.small && aligned) TD_STEP_DISPATCH(td_step_kernel_small, LT, a, TD_LAUNCHS);
     else TD_STEP_DISPATCH(td_step_kernel, LT, a, TD_LAUNCH);
   } else {
     TD_STEP_DISPATCH(td_step_kernel, LT, a, TD_LAUNCH);
   }
 #undef TD_LAUNCH
 #undef TD_LAUNCH2
+#undef TD_LAUNCHS
   return hipGetLastError();
 }
 
@@ -2371,13 +2384,13 @@ template <int LT>
 static int resident3(const StepArgs& a, int cus, int waves) {
   int n = 0;
   hipError_t e = hipErrorInvalidValue;
-#define TD_OCC(k) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, 64, 0)
+#define TD_OCC(k) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, 64 * kSmallBPW, 0)
 #define TD_OCC2(k) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, 128, 0)
   if (waves == 2) TD_STEP_DISPATCH(td_step_kernel_small2, LT, a, TD_OCC2);
   else TD_STEP_DISPATCH(td_step_kernel_small, LT, a, TD_OCC);
 #undef TD_OCC
 #undef TD_OCC2
-  return e == hipSuccess ? n * cus : 0;
+  return e == hipSuccess ? n * cus * (waves == 2 ? 1 : kSmallBPW) : 0;
 }
 
 int step_resident_boards(const StepArgs& a, int cus, int waves) {
