@@ -809,7 +809,9 @@ __device__ __forceinline__ void enemy_stats(Smem<NC>& S, const U& u, const Ctx& 
   const TdDevCfg& C = x.C;
   const int n = u.n;
   if (n == 0) return;  // write_obs emits zero planes without reading grp
-  for (int i = x.lane; i < 4 * NC; i += 64) (&S.grp[0][0])[i] = 0xFF;
+  static_assert((4 * NC) % 16 == 0 && offsetof(Smem<NC>, grp) % 16 == 0, "grp cleared in 16-B units");
+  for (int i = x.lane; i < 4 * NC / 16; i += 64)
+    reinterpret_cast<uint4*>(&S.grp[0][0])[i] = uint4{0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
   uint32_t key[2];
   float r[2] = {0.0f, 0.0f};
   bool val[2];
@@ -874,7 +876,22 @@ template <int NC>
 __device__ __forceinline__ void channel_scalars(Smem<NC>& S, const U& u, const Ctx& x) {
   const TdDevCfg& C = x.C;
   const int l = x.lane;
+#ifdef TD_CHV_UNIFORM  // A/B builds: every quotient channel through two wave-wide divisions
+  {
+    const bool en = l >= 41 && l < 45;
+    const bool q = l == 5 || l == 11 || l == 12 || en;
+    const double num = l == 5 ? (double)u.base_LP : l == 12 ? u.cost_atk : u.cost_def;
+    const double den = l == 5 ? (double)u.max_base_LP : en ? C.e_cost[en ? l - 41 : 0][0] : l == 11 || l == 12 ? u.max_cost : 1.0;
+    // (x / 1.0 is exact: lanes without a second divisor divide by one)
+    const double r = ddiv(ddiv(num, den), en ? (double)C.max_cluster_length : 1.0);
+    float v = q ? f32(r) : l == 13 ? f32(u.progress) : 0.0f;
+    if (l >= 21 && l < 25) v = (u.cost_def >= C.t_price[l - 21][0]) ? 1.0f : 0.0f;
+    if (l < 48) S.chv[l] = v;
+  }
+  if (false) {
+#else
   if (l < 48) {
+#endif
     float v = 0.0f;
     if (l == 5) v = f32(ddiv((double)u.base_LP, (double)u.max_base_LP));
     else if (l == 11) v = f32(ddiv(u.cost_def, u.max_cost));

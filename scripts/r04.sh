@@ -44,15 +44,22 @@ s2)  # board order + XCD map: GPU suite (every kernel), A/B at 8,192 / 4,096 / 6
     TD_TEV_FLAGS=$f run tev${f}_$bb 200 python bench.py --global-batch $bb --no-cpu-baseline --steps $((bb > 10000 ? 200 : 2000)) || exit 1; line tev${f}_$bb
   done; done
   ;;
-s3)  # boards per workgroup of the small kernel (TD_BPW variant builds): parity of the small kernels, A/B at 8,192 / 4,096
+s3)  # A/B builds: boards per workgroup of the small kernel (TD_BPW), uniform channel divisions (chvu)
   for v in bpw2 bpw4; do
     TDSTEP_LIB=$PWD/gym-td_amd/lib/variants/libtdstep_$v.so run pytest_$v 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_envs.py -m gpu -q -k "small and not small2" --timeout 300 --timeout-method thread -p no:cacheprovider
     rc=$?; grep -E "^(FAILED|E  )" $O/pytest_$v.log | head -10; tail -1 $O/pytest_$v.log; [ $rc -le 1 ] || exit $rc
   done
-  for r in 1 2; do for v in prod bpw2 bpw4; do for bb in 8192 4096; do
+  TDSTEP_LIB=$PWD/gym-td_amd/lib/variants/libtdstep_chvu.so run pytest_chvu 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -q --timeout 300 --timeout-method thread -p no:cacheprovider
+  rc=$?; grep -E "^(FAILED|E  )" $O/pytest_chvu.log | head -10; tail -1 $O/pytest_chvu.log; [ $rc -le 1 ] || exit $rc
+  for r in 1 2; do for v in prod bpw2 bpw4 chvu; do for bb in 8192 4096; do
     lib=$PWD/gym-td_amd/lib/variants/libtdstep_$v.so; [ $v = prod ] && lib=$PWD/gym-td_amd/lib/libtdstep.so
-    TDSTEP_LIB=$lib run ${v}_${bb}_$r 200 python bench.py --global-batch $bb --no-cpu-baseline --steps 2000 --timing none --step-kernel small || exit 1; line ${v}_${bb}_$r
-  done; done; done
+    k=small; [ $v = chvu ] && k=auto
+    TDSTEP_LIB=$lib run ${v}_${bb}_$r 200 python bench.py --global-batch $bb --no-cpu-baseline --steps 2000 --timing none --step-kernel $k || exit 1; line ${v}_${bb}_$r
+  done; done
+  for v in prod chvu; do
+    lib=$PWD/gym-td_amd/lib/variants/libtdstep_$v.so; [ $v = prod ] && lib=$PWD/gym-td_amd/lib/libtdstep.so
+    TDSTEP_LIB=$lib run ${v}_65536_$r 200 python bench.py --no-cpu-baseline --steps 300 --timing none || exit 1; line ${v}_65536_$r
+  done; done
   ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
