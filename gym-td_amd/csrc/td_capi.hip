@@ -124,7 +124,7 @@ struct td_handle {
   uint32_t* d_ord = nullptr;
   uint32_t* d_ord_cnt = nullptr;
   int ord_stride = 0;
-  int ord_on = 1;  // TD_ORDER=0: blocks step boards in index order (A/B runs)
+  int ord_on = 0;  // TD_ORDER=1: longest-work-first order (A/B runs; slower, profiles/r04/s2)
   int xcd_map = 1;  // XCD-contiguous board map (td_step.hip xcd_board; TD_XCD_MAP=0: block i = board i)
   int edge_wt = 0;  // shared observation lines write-through (default: only without the XCD map; TD_EDGE_WT)
   long long ord_steps = 0;
@@ -823,10 +823,12 @@ int td_set_refill_interval(td_handle* h, int steps) {
 int td_kernel_timing(td_handle* h, int max_launches, int every) {
   if (!h || max_launches < 0 || every < 1) return fail("td_kernel_timing: bad arguments");
   HIP_OK(hipDeviceSynchronize());
-  // TD_TEV_FLAGS=1 (A/B runs): timing events without the system-scope release at the timed
-  // kernel's end (the cache write-back it implies lengthens the kernel being timed)
+  // Timing events without the system-scope release at the timed kernel's end: the cache
+  // write-back it implies lengthens the very kernel being timed (4,096 boards: sampled
+  // kernels 21.9 us = the 21.9-us step with it, 20.6 us in a 21.3-us step without;
+  // profiles/r04/s2).  TD_TEV_FLAGS=0 (A/B runs): default events.
   const char* tf = std::getenv("TD_TEV_FLAGS");
-  const unsigned flags = tf && std::atoi(tf) == 1 ? hipEventDisableSystemFence : hipEventDefault;
+  const unsigned flags = tf && std::atoi(tf) == 0 ? hipEventDefault : hipEventDisableSystemFence;
   while ((int)h->tev.size() < 2 * max_launches) {
     hipEvent_t e = nullptr;
     HIP_OK(hipEventCreateWithFlags(&e, flags));

@@ -8,8 +8,19 @@
 namespace td {
 
 // opponent hot record: [0] position, [1] lazy-twist boundary, [2] pre-drawn count,
-// [3] unused, [4..11] pre-drawn tempered outputs for positions pos .. pos+count-1
-constexpr int HOT_WORDS = 12;
+// [3] position of the first pre-drawn output, [4..4+HOT_CACHE) pre-drawn tempered outputs for
+// positions [3] .. [3]+count-1.  A step refills them (from its position on) only when fewer
+// than HOT_REFILL remain unused: the stream's words are then read once per refill instead of
+// once per step (TD_HOT_CACHE / TD_HOT_REFILL A/B builds).
+#ifndef TD_HOT_CACHE
+#define TD_HOT_CACHE 8
+#endif
+#ifndef TD_HOT_REFILL
+#define TD_HOT_REFILL TD_HOT_CACHE
+#endif
+constexpr int HOT_CACHE = TD_HOT_CACHE, HOT_REFILL = TD_HOT_REFILL;
+constexpr int HOT_WORDS = 4 + HOT_CACHE;
+static_assert(HOT_CACHE >= 8 && HOT_CACHE <= 32 && HOT_REFILL <= HOT_CACHE, "hot record");
 
 struct StepArgs {
   int B, L, mode, multi, difficulty, autoreset;

@@ -150,7 +150,12 @@ struct WaveMt {
   uint32_t pos, tw;
   uint32_t cache = 0, cbase = 0, cn = 0;  // lane j: tempered output for position cbase + j (j < cn)
 
-  // Pre-draw the next up-to-8 words in parallel, one per lane, for the next
+  // Pre-draws still unused at the current position (0 after a block wrap).
+  __device__ __forceinline__ uint32_t cached_left() const {
+    const uint32_t d = pos - cbase;
+    return d < cn ? cn - d : 0u;
+  }
+  // Pre-draw the next up-to-HOT_CACHE words in parallel, one per lane, for the next
   // step: issue() starts the loads, finish() (at the end of the step) lazily
   // twists, stores and tempers them -- the memory latency overlaps the step.
   uint32_t pa = 0, pnb = 0, pfar = 0;
@@ -158,7 +163,7 @@ struct WaveMt {
   __device__ __forceinline__ void prefetch_issue(int lane) {
     if (pos >= (uint32_t)MT_N) { pos = 0; tw = 0; }
     cbase = pos;
-    cn = (uint32_t)MT_N - pos < 8u ? (uint32_t)MT_N - pos : 8u;
+    cn = (uint32_t)MT_N - pos < (uint32_t)HOT_CACHE ? (uint32_t)MT_N - pos : (uint32_t)HOT_CACHE;
     const uint32_t q = pos + (uint32_t)lane;
     pmine = (uint32_t)lane < cn;
     plazy = pmine && q >= tw;
@@ -1618,9 +1623,18 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
   // built-in opponent stream: position, lazy-twist boundary and the next draws
   // (pre-computed by the previous step) come from the board's hot record
   WaveMt R{opp, lane_word(P.w, PF_HOT + 0), lane_word(P.w, PF_HOT + 1)};
-  R.cn = lane_word(P.w, PF_HOT + 2);
-  R.cbase = R.pos;
-  R.cache = __shfl(P.w, PF_HOT + 4 + (x.lane & 7));
+  // The large kernel refills the pre-drawn outputs only when they run short (lazy); the
+  // small kernels (no SGPR to spare at 8 waves per SIMD) refill every step and use a cache
+  // only if it starts at the current position.
+  constexpr bool LAZY_HOT = !SMALL;
+  if constexpr (LAZY_HOT) {
+    R.cn = lane_word(P.w, PF_HOT + 2);
+    R.cbase = lane_word(P.w, PF_HOT + 3);
+  } else {
+    R.cn = lane_word(P.w, PF_HOT + 3) == R.pos ? lane_word(P.w, PF_HOT + 2) : 0u;
+    R.cbase = R.pos;
+  }
+  R.cache = __shfl(P.w, PF_HOT + 4 + (x.lane < HOT_CACHE ? x.lane : 0));
   STAMP(1);
   if (u.num_roads < 1 || u.num_roads > 3) {
     // never reset (its road generation failed): nothing to step
@@ -1699,7 +1713,13 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
   u.cells_dirty = false;
   pack_obs_cells(S, x);
   // pre-draw the next step's words: loads issued now, consumed at the end of the step
-  if (MODE != MODE_2P) R.prefetch_issue(x.lane);
+  // (the step's draws are done: refill the pre-drawn outputs if the next step may run short)
+  const bool refill = MODE != MODE_2P && (!LAZY_HOT || R.cached_left() < (uint32_t)HOT_REFILL);
+  // (the multi-action kernels have no registers to carry the loads across the step: at once)
+  if (refill) {
+    if constexpr (SCAN) R.prefetch(x.lane);
+    else R.prefetch_issue(x.lane);
+  }
   wsync();
   if constexpr (SPLIT) {  // (A): the second wave writes the binary-plane windows while this one steps
     if (x.lane == 0) S.early_go = 1u;
@@ -1716,7 +1736,7 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
   // acknowledgement (s_waitcnt vmcnt(0)).  (Holding every state store back to the end
   // of the step, next to the observation, measured slower: 219 vs 216 us at 65,536
   // boards, 35.8 vs 34.9 at 8,192, profiles/r03/s16.)
-  if (MODE != MODE_2P) R.prefetch_finish(x.lane);
+  if (!SCAN && refill) R.prefetch_finish(x.lane);
   if (MODE == MODE_ATK) reward = -reward;                   // TDAttack.py:50
   const bool done = (u.base_LP <= 0) || (u.steps >= C.max_episode_steps);  // :384-385
   u.ep_ret = dadd(u.ep_ret, reward);
@@ -1775,6 +1795,7 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
     sst(&hot[0], R.pos);
     sst(&hot[1], R.tw);
     sst(&hot[2], R.cn);
+    sst(&hot[3], R.cbase);
     sst(&a.reward[b], reward);
     sst(&a.done[b], (uint8_t)(done ? 1 : 0));
     if (a.win) sst(&a.win[b], win);
@@ -1796,7 +1817,7 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
       atomicAdd(&a.ep_stats[1], ep_ret);
     }
   }
-  if (MODE != MODE_2P && x.lane < 8) sst(&hot[4 + x.lane], R.cache);
+  if (refill && x.lane < HOT_CACHE) sst(&hot[4 + x.lane], R.cache);
   // the observation last: nothing of the step is live any more, the writer has the registers
   STAMP(6);
   if constexpr (SPLIT) {
@@ -1962,8 +1983,8 @@ __global__ __launch_bounds__(64) void td_opponent_kernel(StepArgs a, int side, i
   uint32_t* const hot = a.opp_hot + (size_t)b * HOT_WORDS;
   WaveMt R{a.opp_mt + (size_t)b * OPP_WORDS, lane_word(P.w, PF_HOT + 0), lane_word(P.w, PF_HOT + 1)};
   R.cn = lane_word(P.w, PF_HOT + 2);
-  R.cbase = R.pos;
-  R.cache = __shfl(P.w, PF_HOT + 4 + (x.lane & 7));
+  R.cbase = lane_word(P.w, PF_HOT + 3);
+  R.cache = __shfl(P.w, PF_HOT + 4 + (x.lane < HOT_CACHE ? x.lane : 0));
   with_opp_rng(a, b, x.lane, R, [&](auto& G) {
     if (side == 0) opponent_enemy(S, u, x, G, level);
     else opponent_tower(S, u, x, G, level);
@@ -1978,8 +1999,8 @@ __global__ __launch_bounds__(64) void td_opponent_kernel(StepArgs a, int side, i
   }
   store_cells(S, u, x, a, b);
   store_board(S, u, x, a, b);
-  if (x.lane == 0) { hot[0] = R.pos; hot[1] = R.tw; hot[2] = R.cn; }
-  if (x.lane < 8) hot[4 + x.lane] = R.cache;
+  if (x.lane == 0) { hot[0] = R.pos; hot[1] = R.tw; hot[2] = R.cn; hot[3] = R.cbase; }
+  if (x.lane < HOT_CACHE) hot[4 + x.lane] = R.cache;
 }
 
 template <int LT>

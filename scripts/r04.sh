@@ -61,5 +61,35 @@ s3)  # A/B builds: boards per workgroup of the small kernel (TD_BPW), uniform ch
     TDSTEP_LIB=$lib run ${v}_65536_$r 200 python bench.py --no-cpu-baseline --steps 300 --timing none || exit 1; line ${v}_65536_$r
   done; done
   ;;
+s4)  # XCD map x shared-line policy per workload, lazy opponent cache (hc16/hc28), BPW and uniform-division builds
+  gpusuite 900; rc=$?; [ $rc -le 1 ] || exit $rc
+  V=$PWD/gym-td_amd/lib/variants
+  for v in hc28 hc16 bpw2 bpw4 chvu; do
+    TDSTEP_LIB=$V/libtdstep_$v.so run pytest_$v 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -q --timeout 300 --timeout-method thread -p no:cacheprovider
+    rc=$?; grep -E "^(FAILED|E  )" $O/pytest_$v.log | head -10; tail -1 $O/pytest_$v.log; [ $rc -le 1 ] || exit $rc
+  done
+  for r in 1 2; do
+    for xe in "1 1" "1 0" "0 1"; do set -- $xe
+      TD_XCD_MAP=$1 TD_EDGE_WT=$2 run p_x$1e$2_65536_$r 200 python bench.py --no-cpu-baseline --steps 300 --timing none || exit 1; line p_x$1e$2_65536_$r
+    done
+    for v in hc28 hc16; do
+      TDSTEP_LIB=$V/libtdstep_$v.so TD_EDGE_WT=1 run ${v}_x1e1_65536_$r 200 python bench.py --no-cpu-baseline --steps 300 --timing none || exit 1; line ${v}_x1e1_65536_$r
+    done
+    for xe in "1 1" "1 0" "0 1"; do set -- $xe
+      TD_XCD_MAP=$1 TD_EDGE_WT=$2 run l30_x$1e$2_$r 300 python bench.py --workload def-large --global-batch 16384 --no-cpu-baseline --steps 200 --timing none || exit 1; line l30_x$1e$2_$r
+      TD_XCD_MAP=$1 TD_EDGE_WT=$2 run p2_x$1e$2_$r 300 python bench.py --workload 2p-middle-multi --no-cpu-baseline --steps 200 --timing none || exit 1; line p2_x$1e$2_$r
+    done
+    for v in prod bpw2 bpw4 chvu; do for bb in 8192 4096; do
+      lib=$V/libtdstep_$v.so; [ $v = prod ] && lib=$PWD/gym-td_amd/lib/libtdstep.so
+      k=small; [ $v = chvu -o $v = prod ] && k=auto
+      TDSTEP_LIB=$lib run ${v}_${bb}_$r 200 python bench.py --global-batch $bb --no-cpu-baseline --steps 2000 --timing none --step-kernel $k || exit 1; line ${v}_${bb}_$r
+    done; done
+  done
+  for v in prod hc28 hc16; do
+    lib=$V/libtdstep_$v.so; [ $v = prod ] && lib=$PWD/gym-td_amd/lib/libtdstep.so
+    TDSTEP_LIB=$lib TD_EDGE_WT=1 OUT=$O/pmc NAME=${v}_x1e1 B=65536 run pmc_${v} 600 bash scripts/pmc_ab.sh || exit 1; tail -1 $O/pmc_${v}.log
+  done
+  run bench_driver 300 python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline || exit 1; line bench_driver
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
