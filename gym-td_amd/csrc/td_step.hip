@@ -109,6 +109,7 @@ struct U {
   int steps, base_LP, atk_cd, def_cd, n, nt, num_roads, end_cell, maxdist, flags, episodes;
   int max_base_LP;  // captured at reset (TDBoard.py:72)
   bool cells_dirty;  // map[6] changed (tower built / destroyed) or a new layout: write the cells back
+  bool tw_dirty;     // the tower list changed (build / upgrade / destruct, reset): write tw_inf back
   uint64_t starts;  // start cells of roads 0-2, 16 bits each (a shift, not an indexed field: keeps U in registers)
   __device__ __forceinline__ int start(int road) const { return (int)((starts >> (16 * road)) & 0xffffu); }
   __device__ __forceinline__ void set_starts(uint32_t s0, uint32_t s1, uint32_t s2) {
@@ -318,6 +319,7 @@ __device__ __forceinline__ int tower_build(Smem<NC>& S, U& u, const Ctx& x, int 
   u.nt += 1;
   u.cost_def = dsub(u.cost_def, price);                   // :238
   u.cells_dirty = true;
+  u.tw_dirty = true;
   wsync();
   diamond(S, x, cell, +1);                                // :239-245
   return FC_OK;
@@ -345,6 +347,7 @@ __device__ __forceinline__ int tower_lvup(Smem<NC>& S, U& u, const Ctx& x, int c
     set_tower(S, cell, tw_nib(lv + 1, t));
   }
   u.cost_def = dsub(u.cost_def, price);                   // :266
+  u.tw_dirty = true;
   wsync();
   return FC_OK;
 }
@@ -362,6 +365,7 @@ __device__ __forceinline__ int tower_destruct(Smem<NC>& S, U& u, const Ctx& x, i
   u.cost_def = dadd(u.cost_def, dmul(value, x.C.destruct_return));  // :276
   u.cost_def = pymin(u.cost_def, u.max_cost);                      // :277
   u.cells_dirty = true;
+  u.tw_dirty = true;
   // towers.remove(t): keep the order of the rest (:278)
   uint32_t vi = 0;
   double vc = 0.0;
@@ -1314,6 +1318,7 @@ __device__ __forceinline__ void load_board(Smem<NC>& S, U& u, const Ctx& x, cons
   u.max_cost = lane_f64(P.w, 20); u.max_base_LP = (int)lane_word(P.w, 22);
   u.progress = ddiv((double)u.steps, (double)x.C.max_episode_steps);
   u.cells_dirty = false;
+  u.tw_dirty = false;
   if (x.lane < u.n && x.lane < PFE) { S.eLP[x.lane] = P.lp; S.eMg[x.lane] = P.mg; S.eInf[x.lane] = P.inf; }
   for (int i = PFE + x.lane; i < u.n; i += 64) { S.eLP[i] = a.en_lp[eb + i]; S.eMg[i] = a.en_mg[eb + i]; S.eInf[i] = a.en_inf[eb + i]; }
   uint32_t tinf = P.tinf;
@@ -1348,6 +1353,7 @@ __device__ __forceinline__ void reset_board(Smem<NC>& S, U& u, const Ctx& x, con
   u.max_cost = C.max_cost; u.max_base_LP = C.base_LP;  // TDBoard(max_cost, base_LP) from config at reset
   u.atk_cd = 0; u.def_cd = 0; u.n = 0; u.nt = 0; u.ep_ret = 0.0;
   u.cells_dirty = true;
+  u.tw_dirty = true;
   wsync();
 }
 
@@ -1374,7 +1380,11 @@ __device__ __forceinline__ void store_board(const Smem<NC>& S, const U& u, const
   }
   const size_t tb = (size_t)b * TCAP;
   // cells were written back by store_cells, enemies at the end of board_step
-  if (x.lane < u.nt) { sst(&a.tw_cd[tb + x.lane], S.tCd[x.lane]); sst(&a.tw_inf[tb + x.lane], S.tInf[x.lane]); }
+  // (the cool-downs change every step; the tower words only when the list does)
+  if (x.lane < u.nt) {
+    sst(&a.tw_cd[tb + x.lane], S.tCd[x.lane]);
+    if (u.tw_dirty) sst(&a.tw_inf[tb + x.lane], S.tInf[x.lane]);
+  }
 }
 
 // ---------------------------------------------------------------------------
