@@ -411,7 +411,10 @@ __device__ __forceinline__ void defender_scan(Smem<NC>& S, U& u, const Ctx& x, c
     typedef long long i64x2 __attribute__((ext_vector_type(2)));
     const i64x2* A2 = reinterpret_cast<const i64x2*>(A);
     const int n2 = n / 2;
-    constexpr int K = 8;
+#ifndef TD_SCAN_K
+#define TD_SCAN_K 8
+#endif
+    constexpr int K = TD_SCAN_K;  // 16-B loads in flight per lane
     for (int base = 0; base < n2; base += 64 * K) {
       i64x2 v[K];
 #pragma unroll
@@ -1904,6 +1907,10 @@ constexpr int large_waves() { return LT == 10 ? 7 : LT == 20 ? 5 : 3; }  // LDS-
 #define TD_LARGE_ATTR __attribute__((amdgpu_waves_per_eu(large_waves<LT>())))
 #else
 #define TD_LARGE_ATTR
+#endif
+#if defined(TD_SCAN_WAVES) && !defined(TD_DRY_DRAW)  // A/B builds: residency of the multi-action kernels
+#undef TD_LARGE_ATTR
+#define TD_LARGE_ATTR __attribute__((amdgpu_waves_per_eu(SCAN ? TD_SCAN_WAVES : 1)))
 #endif
 template <int LT, int MODE, bool SCAN>
 __global__ __launch_bounds__(64) TD_LARGE_ATTR void td_step_kernel(StepArgs a) {
