@@ -126,7 +126,8 @@ struct td_handle {
   int ord_stride = 0;
   int ord_on = 0;  // TD_ORDER=1: longest-work-first order (A/B runs; slower, profiles/r04/s2)
   int xcd_map = 1;  // XCD-contiguous board map (td_step.hip xcd_board; TD_XCD_MAP=0: block i = board i)
-  int edge_wt = 0;  // shared observation lines write-through (default: only without the XCD map; TD_EDGE_WT)
+  int edge_wt = 1;  // observation lines shared with a neighbour written write-through (TD_EDGE_WT=0: non-temporal,
+                    // A/B runs: 233 vs 212 us at 65,536 boards even with both halves on one XCD, profiles/r04/s4)
   long long ord_steps = 0;
 };
 
@@ -441,7 +442,6 @@ td_handle* td_create(const td_config* cfg, int map_size, int n_boards, int mode,
   rc |= dalloc(&h->d_epstats, 2);
   rc |= dalloc(&h->d_lastep, B);
   if (const char* e = std::getenv("TD_XCD_MAP")) h->xcd_map = std::atoi(e) ? 1 : 0;  // A/B runs
-  h->edge_wt = h->xcd_map ? 0 : 1;
   if (const char* e = std::getenv("TD_EDGE_WT")) h->edge_wt = std::atoi(e) ? 1 : 0;
   h->ord_stride = ord_stride(n_boards);
   rc |= dalloc(&h->d_ord, (size_t)2 * ORD_XCD * h->ord_stride);
@@ -783,7 +783,7 @@ int td_step(td_handle* h, const td_step_io* io, void* stream) {
   }
   // the small kernels (launched for a 16-B-aligned observation, launch2) step their boards
   // in the order the previous small-kernel step left
-  const bool ordered = h->ord_on && h->small && ((reinterpret_cast<uintptr_t>(io->obs) & 15u) == 0);
+  const bool ordered = h->ord_on && (h->small || kOrderLarge) && ((reinterpret_cast<uintptr_t>(io->obs) & 15u) == 0);
   if (ordered) {
     const int p = (int)(h->ord_steps & 1);
     const size_t span = (size_t)ORD_XCD * h->ord_stride;

@@ -100,6 +100,11 @@ constexpr int ORD_CNT_WORDS = ORD_XCD * ORD_CHUNKS * ORD_LINE;  // per parity
 // one-round grid of B boards then has B / BPW workgroups to dispatch.  Board slots are
 // "virtual blocks" vb = workgroup * BPW + wave: XCD (vb / BPW) % 8, slot
 // (vb / BPW / 8) * BPW + vb % BPW of that XCD's list.
+// TD_ORDER_LARGE A/B builds: the large kernel follows the board order too.
+#ifndef TD_ORDER_LARGE
+#define TD_ORDER_LARGE 0
+#endif
+constexpr bool kOrderLarge = TD_ORDER_LARGE != 0;
 #ifndef TD_BPW
 #define TD_BPW 1
 #endif

@@ -888,22 +888,7 @@ template <int NC>
 __device__ __forceinline__ void channel_scalars(Smem<NC>& S, const U& u, const Ctx& x) {
   const TdDevCfg& C = x.C;
   const int l = x.lane;
-#ifdef TD_CHV_UNIFORM  // A/B builds: every quotient channel through two wave-wide divisions
-  {
-    const bool en = l >= 41 && l < 45;
-    const bool q = l == 5 || l == 11 || l == 12 || en;
-    const double num = l == 5 ? (double)u.base_LP : l == 12 ? u.cost_atk : u.cost_def;
-    const double den = l == 5 ? (double)u.max_base_LP : en ? C.e_cost[en ? l - 41 : 0][0] : l == 11 || l == 12 ? u.max_cost : 1.0;
-    // (x / 1.0 is exact: lanes without a second divisor divide by one)
-    const double r = ddiv(ddiv(num, den), en ? (double)C.max_cluster_length : 1.0);
-    float v = q ? f32(r) : l == 13 ? f32(u.progress) : 0.0f;
-    if (l >= 21 && l < 25) v = (u.cost_def >= C.t_price[l - 21][0]) ? 1.0f : 0.0f;
-    if (l < 48) S.chv[l] = v;
-  }
-  if (false) {
-#else
   if (l < 48) {
-#endif
     float v = 0.0f;
     if (l == 5) v = f32(ddiv((double)u.base_LP, (double)u.max_base_LP));
     else if (l == 11) v = f32(ddiv(u.cost_def, u.max_cost));
@@ -1631,7 +1616,8 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
   load_board<NC, PF, PF>(S, u, x, a, b, P);
   const bool ord_heavy = u.n > 0;
   // (the multi-action scan has no register to hold the claim across it: claimed at the place)
-  uint32_t ord_r = SMALL && !SCAN ? ord_claim(a, ord_heavy, x.lane, vb, BPW) : 0u;
+  constexpr bool ORD = SMALL || kOrderLarge;
+  uint32_t ord_r = ORD && !SCAN ? ord_claim(a, ord_heavy, x.lane, vb, BPW) : 0u;
   const int64_t act_in = (int64_t)(((uint64_t)lane_word(P.w, PF_ACT + 1) << 32) | lane_word(P.w, PF_ACT));
   // built-in opponent stream: position, lazy-twist boundary and the next draws
   // (pre-computed by the previous step) come from the board's hot record
@@ -1651,8 +1637,8 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
   STAMP(1);
   if (u.num_roads < 1 || u.num_roads > 3) {
     // never reset (its road generation failed): nothing to step
-    if constexpr (SMALL && SCAN) ord_r = ord_claim(a, ord_heavy, x.lane, vb, BPW);
-    if constexpr (SMALL) ord_place(a, b, ord_heavy, ord_r, x.lane, vb, BPW);
+    if constexpr (ORD && SCAN) ord_r = ord_claim(a, ord_heavy, x.lane, vb, BPW);
+    if constexpr (ORD) ord_place(a, b, ord_heavy, ord_r, x.lane, vb, BPW);
     const int nf = NCH * x.NCr;
     float* o = a.obs + (size_t)b * nf;
     for (int i = x.lane; i < nf; i += 64) o[i] = 0.0f;
@@ -1718,8 +1704,8 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
       with_opp_rng(a, b, x.lane, R, [&](auto& G) { opponent_tower(S, u, x, G, a.difficulty); });
   }
   STAMP(12);
-  if constexpr (SMALL && SCAN) ord_r = ord_claim(a, ord_heavy, x.lane, vb, BPW);
-  if constexpr (SMALL) ord_place(a, b, ord_heavy, ord_r, x.lane, vb, BPW);
+  if constexpr (ORD && SCAN) ord_r = ord_claim(a, ord_heavy, x.lane, vb, BPW);
+  if constexpr (ORD) ord_place(a, b, ord_heavy, ord_r, x.lane, vb, BPW);
   // the towers and map[6] are final: cell words back to HBM if they changed, then
   // packed for the rest of the step (board_step reads the packed direction and distance)
   store_cells(S, u, x, a, b);
@@ -1886,7 +1872,7 @@ __device__ __forceinline__ void step_kernel_body(const StepArgs& a) {
   const int vb = (int)blockIdx.x * BPW + w;  // the board slot of this wave
   if (vb >= a.B) return;
   Smem<NC>& S = SS[w];
-  const int b = SMALL ? ord_board(a, vb, BPW) : a.xcd_map ? xcd_board(vb, a.B) : vb;
+  const int b = SMALL || kOrderLarge ? ord_board(a, vb, BPW) : a.xcd_map ? xcd_board(vb, a.B) : vb;
 #ifdef TD_STEP_PRIO  // A/B builds: step waves ahead of concurrent refill waves in issue arbitration
   __builtin_amdgcn_s_setprio(TD_STEP_PRIO);
 #endif

@@ -91,5 +91,22 @@ s4)  # XCD map x shared-line policy per workload, lazy opponent cache (hc16/hc28
   done
   run bench_driver 300 python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline || exit 1; line bench_driver
   ;;
+s5)  # board order in multi-round grids (small2 at 30x30 / 16,384 10x10; the large kernel: olarge build), driver command
+  gpusuite 900; rc=$?; [ $rc -le 1 ] || exit $rc
+  V=$PWD/gym-td_amd/lib/variants
+  TDSTEP_LIB=$V/libtdstep_olarge.so TD_ORDER=1 run pytest_olarge 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_envs.py -m gpu -q -k "large" --timeout 300 --timeout-method thread -p no:cacheprovider
+  rc=$?; grep -E "^(FAILED|E  )" $O/pytest_olarge.log | head -10; tail -1 $O/pytest_olarge.log; [ $rc -le 1 ] || exit $rc
+  for r in 1 2; do
+    for o in 0 1; do
+      TD_ORDER=$o run l30_o${o}_$r 300 python bench.py --workload def-large --global-batch 16384 --no-cpu-baseline --steps 200 --timing none || exit 1; line l30_o${o}_$r
+      TD_ORDER=$o run s16k_o${o}_$r 200 python bench.py --global-batch 16384 --no-cpu-baseline --steps 1000 --timing none || exit 1; line s16k_o${o}_$r
+      TDSTEP_LIB=$V/libtdstep_olarge.so TD_ORDER=$o run ol65_o${o}_$r 200 python bench.py --no-cpu-baseline --steps 300 --timing none || exit 1; line ol65_o${o}_$r
+      TDSTEP_LIB=$V/libtdstep_olarge.so TD_ORDER=$o run ol32_o${o}_$r 200 python bench.py --global-batch 32768 --no-cpu-baseline --steps 500 --timing none || exit 1; line ol32_o${o}_$r
+      TDSTEP_LIB=$V/libtdstep_olarge.so TD_ORDER=$o run olp2_o${o}_$r 300 python bench.py --workload 2p-middle-multi --no-cpu-baseline --steps 200 --timing none || exit 1; line olp2_o${o}_$r
+    done
+    run p65_$r 200 python bench.py --no-cpu-baseline --steps 300 --timing none || exit 1; line p65_$r
+  done
+  run bench_driver 300 python bench.py --gpus 1 --steps 20 --warmup 5 || exit 1; line bench_driver
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
