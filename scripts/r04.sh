@@ -108,5 +108,18 @@ s5)  # board order in multi-round grids (small2 at 30x30 / 16,384 10x10; the lar
   done
   run bench_driver 300 python bench.py --gpus 1 --steps 20 --warmup 5 || exit 1; line bench_driver
   ;;
+s6)  # 30x30: reproduce r04/s2's 466-us line (timing mode, order, edge policy); refill waves at the small shares
+  for r in 1 2; do
+    for t in dispatch none; do for oe in "0 1" "1 0"; do set -- $oe
+      TD_ORDER=$1 TD_EDGE_WT=$2 run l30_$t_o$1e$2_$r 300 python bench.py --workload def-large --global-batch 16384 --no-cpu-baseline --steps 200 --timing $t || exit 1; line l30_$t_o$1e$2_$r
+    done; done
+    for w in 1024 256 64; do for bb in 8192 4096; do
+      TD_REFILL_WAVES=$w run rw${w}_${bb}_$r 200 python bench.py --global-batch $bb --no-cpu-baseline --steps 2000 --timing none || exit 1; line rw${w}_${bb}_$r
+    done; done
+    for bb in 8192 4096; do
+      run norefill_${bb}_$r 200 python bench.py --global-batch $bb --no-cpu-baseline --steps 2000 --timing none --refill-interval 0 || exit 1; line norefill_${bb}_$r
+    done
+  done
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
