@@ -150,6 +150,45 @@ struct WaveMt {
   uint32_t* w;
   uint32_t pos, tw;
   uint32_t cache = 0, cbase = 0, cn = 0;  // lane j: tempered output for position cbase + j (j < cn)
+  // block_tw: at a block wrap the whole next block is twisted at once, in place (the large
+  // kernel): later draws and pre-draws of the block then read its words as they are --
+  // one line per pre-draw instead of three, and no partial-line stores of lazily twisted
+  // words every step.  Otherwise (the small kernels: latency-bound, where three dependent
+  // round trips in one wave would lengthen the grid's tail) words are twisted as drawn.
+  bool block_tw = false;
+
+  // CPython's twist of the whole block (w[0..624) -> the next block), by the wave in three
+  // dependent phases: new[i] needs old[i], old[i+1] and old[i+397] (i < 227) or new[i-227].
+  // The wave's own completed stores are visible to its later loads (vmcnt(0) between phases).
+  static __device__ __forceinline__ uint32_t twist1(uint32_t a, uint32_t b, uint32_t far) {
+    const uint32_t yy = (a & 0x80000000u) | (b & 0x7fffffffu);
+    return far ^ (yy >> 1) ^ ((yy & 1u) ? 0x9908b0dfu : 0u);
+  }
+  __device__ __forceinline__ void twist_block(int lane) {
+    constexpr int P0 = MT_N - MT_M, P1 = 2 * (MT_N - MT_M);  // 227, 454
+#pragma unroll
+    for (int ph = 0; ph < 3; ++ph) {
+      const int lo = ph == 0 ? 0 : ph == 1 ? P0 : P1, hi = ph == 0 ? P0 : ph == 1 ? P1 : MT_N;
+      uint32_t y[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {  // every load of the phase before any of its stores
+        const int i = lo + lane + 64 * k;
+        y[k] = 0u;
+        if (i < hi) y[k] = twist1(w[i], w[i == MT_N - 1 ? 0 : i + 1], w[ph == 0 ? i + MT_M : i - P0]);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int i = lo + lane + 64 * k;
+        if (i < hi) w[i] = y[k];
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __device__ __forceinline__ void wrap(int lane) {
+    if (block_tw) { twist_block(lane); tw = MT_N; }
+    else tw = 0;
+    pos = 0;
+  }
 
   // Pre-draws still unused at the current position (0 after a block wrap).
   __device__ __forceinline__ uint32_t cached_left() const {
@@ -162,7 +201,7 @@ struct WaveMt {
   uint32_t pa = 0, pnb = 0, pfar = 0;
   bool plazy = false, pmine = false;
   __device__ __forceinline__ void prefetch_issue(int lane) {
-    if (pos >= (uint32_t)MT_N) { pos = 0; tw = 0; }
+    if (pos >= (uint32_t)MT_N) wrap(lane);
     cbase = pos;
     cn = (uint32_t)MT_N - pos < (uint32_t)HOT_CACHE ? (uint32_t)MT_N - pos : (uint32_t)HOT_CACHE;
     const uint32_t q = pos + (uint32_t)lane;
@@ -199,7 +238,7 @@ struct WaveMt {
       ++pos;
       return rdl(cache, (int)d);  // d is wave-uniform: a scalar read, no LDS round trip
     }
-    if (pos >= (uint32_t)MT_N) { pos = 0; tw = 0; cn = 0; }
+    if (pos >= (uint32_t)MT_N) { wrap((int)(threadIdx.x & 63)); cn = 0; }
     uint32_t y;
     if (pos >= tw) {
       const uint32_t a = w[pos];
@@ -1625,7 +1664,10 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
   // The large kernel refills the pre-drawn outputs only when they run short (lazy); the
   // small kernels (no SGPR to spare at 8 waves per SIMD) refill every step and use a cache
   // only if it starts at the current position.
-  constexpr bool LAZY_HOT = !SMALL;
+#ifndef TD_LAZY_HOT_SMALL
+#define TD_LAZY_HOT_SMALL 0
+#endif
+  constexpr bool LAZY_HOT = !SMALL || TD_LAZY_HOT_SMALL;
   if constexpr (LAZY_HOT) {
     R.cn = lane_word(P.w, PF_HOT + 2);
     R.cbase = lane_word(P.w, PF_HOT + 3);
@@ -1634,6 +1676,10 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
     R.cbase = R.pos;
   }
   R.cache = __shfl(P.w, PF_HOT + 4 + (x.lane < HOT_CACHE ? x.lane : 0));
+#ifndef TD_BLOCK_TWIST
+#define TD_BLOCK_TWIST 1
+#endif
+  R.block_tw = !SMALL && TD_BLOCK_TWIST;
   STAMP(1);
   if (u.num_roads < 1 || u.num_roads > 3) {
     // never reset (its road generation failed): nothing to step

@@ -121,5 +121,24 @@ s6)  # 30x30: reproduce r04/s2's 466-us line (timing mode, order, edge policy); 
     done
   done
   ;;
+s7)  # block twist of the opponent stream (large kernel) vs lazy (nobt); lazy-hot small kernels (lhs) at 30x30; PMC
+  gpusuite 900; rc=$?; [ $rc -le 1 ] || exit $rc
+  V=$PWD/gym-td_amd/lib/variants
+  TDSTEP_LIB=$V/libtdstep_lhs.so run pytest_lhs 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -q --timeout 300 --timeout-method thread -p no:cacheprovider
+  rc=$?; tail -1 $O/pytest_lhs.log; [ $rc -le 1 ] || exit $rc
+  for r in 1 2; do
+    for v in prod nobt; do
+      lib=$V/libtdstep_$v.so; [ $v = prod ] && lib=$PWD/gym-td_amd/lib/libtdstep.so
+      TDSTEP_LIB=$lib run ${v}_65536_$r 200 python bench.py --no-cpu-baseline --steps 300 --timing none || exit 1; line ${v}_65536_$r
+      TDSTEP_LIB=$lib run ${v}_p2_$r 300 python bench.py --workload 2p-middle-multi --no-cpu-baseline --steps 200 --timing none || exit 1; line ${v}_p2_$r
+    done
+    for v in prod lhs; do
+      lib=$V/libtdstep_$v.so; [ $v = prod ] && lib=$PWD/gym-td_amd/lib/libtdstep.so
+      TDSTEP_LIB=$lib run ${v}_l30_$r 300 python bench.py --workload def-large --global-batch 16384 --no-cpu-baseline --steps 200 --timing none || exit 1; line ${v}_l30_$r
+      TDSTEP_LIB=$lib run ${v}_8192_$r 200 python bench.py --global-batch 8192 --no-cpu-baseline --steps 2000 --timing none || exit 1; line ${v}_8192_$r
+    done
+  done
+  OUT=$O/pmc NAME=prod B=65536 run pmc_prod 600 bash scripts/pmc_ab.sh || exit 1; tail -1 $O/pmc_prod.log
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
