@@ -554,13 +554,16 @@ __device__ __forceinline__ int summon_cluster(Smem<NC>& S, U& u, const Ctx& x, u
   const int st = u.start(road);
   bool tried = false, summoned = false;
   uint32_t rp = 0;
+  // the four types' cost (lanes 0-3) and max LP (lanes 4-7) at this level in ONE LDS read,
+  // then read per slot from those lanes (8 dependent LDS round trips before, one per slot)
+  const double tab = x.lane < 4 ? C.e_cost[x.lane & 3][lv] : C.e_lp[x.lane & 3][lv];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     const int t = (int)((types >> (4 * k)) & 0xfu);
     int r = t;
     if (t != 4) {                                           // :207-209
       tried = true;
-      const double cost = C.e_cost[t][lv];
+      const double cost = rdl(tab, t);
       if (u.cost_atk < cost) {                              // :212-213
         r = 4;
       } else if (u.n >= ECAP) {
@@ -568,8 +571,9 @@ __device__ __forceinline__ int summon_cluster(Smem<NC>& S, U& u, const Ctx& x, u
         r = 4;
       } else {
         u.cost_atk = dsub(u.cost_atk, cost);                // :215
+        const double lp = rdl(tab, 4 + t);
         if (x.lane == 0) {
-          S.eLP[u.n] = C.e_lp[t][lv];
+          S.eLP[u.n] = lp;
           S.eMg[u.n] = 0.0;
           S.eInf[u.n] = en_pack(st, t, lv, 0, x.ep);
         }
@@ -1677,7 +1681,7 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
   }
   R.cache = __shfl(P.w, PF_HOT + 4 + (x.lane < HOT_CACHE ? x.lane : 0));
 #ifndef TD_BLOCK_TWIST
-#define TD_BLOCK_TWIST 1
+#define TD_BLOCK_TWIST 0
 #endif
   R.block_tw = !SMALL && TD_BLOCK_TWIST;
   STAMP(1);

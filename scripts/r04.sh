@@ -140,5 +140,18 @@ s7)  # block twist of the opponent stream (large kernel) vs lazy (nobt); lazy-ho
   done
   OUT=$O/pmc NAME=prod B=65536 run pmc_prod 600 bash scripts/pmc_ab.sh || exit 1; tail -1 $O/pmc_prod.log
   ;;
+s8)  # 30x30 bisect (builds of commits 9f7a2e2 / bf5cc12 vs current); summon-cost change at the small shares (vs nobt)
+  V=$PWD/gym-td_amd/lib/variants
+  for r in 1 2; do
+    for v in prod c9f7 cbf5; do
+      lib=$V/libtdstep_$v.so; [ $v = prod ] && lib=$PWD/gym-td_amd/lib/libtdstep.so
+      TDSTEP_LIB=$lib run ${v}_l30_$r 300 python bench.py --workload def-large --global-batch 16384 --no-cpu-baseline --steps 200 --timing none || exit 1; line ${v}_l30_$r
+    done
+    for v in prod nobt; do for bb in 8192 4096; do
+      lib=$V/libtdstep_$v.so; [ $v = prod ] && lib=$PWD/gym-td_amd/lib/libtdstep.so
+      TDSTEP_LIB=$lib run ${v}_${bb}_$r 200 python bench.py --global-batch $bb --no-cpu-baseline --steps 2000 --timing none || exit 1; line ${v}_${bb}_$r
+    done; done
+  done
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
