@@ -73,7 +73,6 @@ struct alignas(16) Smem {
       float d9[64];       // channel 9 by distance (road length < 2L <= 64)
     };
   };
-  uint32_t obs_go, obs_any;  // td_step_kernel_small2: the stepping wave tells the second one to write
   uint32_t early_go;         // td_step_kernel_small2: the binary-plane windows may be written early
   TdDevCfg cfg;           // constant block, staged once per board: per-lane table lookups hit LDS
 };
@@ -1397,25 +1396,78 @@ __device__ __forceinline__ void store_cells(const Smem<NC>& S, const U& u, const
     for (int i = x.lane; i < x.NCr; i += 64) sst(&a.cells[cb + i], S.cell[i] & ~kTwBits);
 }
 
+__device__ __forceinline__ TdHdr hdr_of(const U& u) {
+  TdHdr h;
+  h.cost_def = u.cost_def; h.cost_atk = u.cost_atk; h.ep_return = u.ep_ret;
+  h.steps = u.steps; h.base_LP = u.base_LP; h.atk_cd = u.atk_cd; h.def_cd = u.def_cd;
+  h.n_en = u.n; h.n_tw = u.nt; h.num_roads = u.num_roads; h.end_cell = u.end_cell;
+  h.start_cell[0] = u.start(0); h.start_cell[1] = u.start(1); h.start_cell[2] = u.start(2);
+  h.maxdist = u.maxdist; h.flags = u.flags; h.episodes = u.episodes;
+  h.max_cost = u.max_cost; h.max_base_LP = u.max_base_LP; h.format = kHdrFormat;
+  return h;
+}
+
+// The towers' words (cool-downs every step, the rest only when the list changed).
+template <int NC>
+__device__ __forceinline__ void store_towers(const Smem<NC>& S, int nt, bool dirty, int lane, const StepArgs& a, int b) {
+  const size_t tb = (size_t)b * TCAP;
+  if (lane < nt) {
+    sst(&a.tw_cd[tb + lane], S.tCd[lane]);
+    if (dirty) sst(&a.tw_inf[tb + lane], S.tInf[lane]);
+  }
+}
+
 template <int NC>
 __device__ __forceinline__ void store_board(const Smem<NC>& S, const U& u, const Ctx& x, const StepArgs& a, int b) {
-  if (x.lane == 0) {
-    TdHdr h;
-    h.cost_def = u.cost_def; h.cost_atk = u.cost_atk; h.ep_return = u.ep_ret;
-    h.steps = u.steps; h.base_LP = u.base_LP; h.atk_cd = u.atk_cd; h.def_cd = u.def_cd;
-    h.n_en = u.n; h.n_tw = u.nt; h.num_roads = u.num_roads; h.end_cell = u.end_cell;
-    h.start_cell[0] = u.start(0); h.start_cell[1] = u.start(1); h.start_cell[2] = u.start(2);
-    h.maxdist = u.maxdist; h.flags = u.flags; h.episodes = u.episodes;
-    h.max_cost = u.max_cost; h.max_base_LP = u.max_base_LP; h.format = kHdrFormat;
-    a.hdr[b] = h;
-  }
-  const size_t tb = (size_t)b * TCAP;
+  if (x.lane == 0) a.hdr[b] = hdr_of(u);
   // cells were written back by store_cells, enemies at the end of board_step
-  // (the cool-downs change every step; the tower words only when the list does)
-  if (x.lane < u.nt) {
-    sst(&a.tw_cd[tb + x.lane], S.tCd[x.lane]);
-    if (u.tw_dirty) sst(&a.tw_inf[tb + x.lane], S.tInf[x.lane]);
+  store_towers(S, u.nt, u.tw_dirty, x.lane, a, b);
+}
+
+// The per-board outputs of a step (td_step_io) and the board after it: in
+// td_step_kernel_small2 the stepping wave hands them to the second wave in LDS, which
+// stores them (store_board, store_outputs) while the stepping wave computes the group
+// statistics and broadcast channels -- off the board's critical path.
+struct StepOut {
+  TdHdr hdr;           // the board's header after the step (6 lanes copy it out, 16 B each)
+  int32_t nt, tw_dirty;
+  double reward, ep_ret;
+  int64_t real_def;
+  int32_t ep_steps, fail_def;
+  uint32_t done, win, allow, cool;
+  uint32_t go;   // second wave: 0 nothing (a board never reset wrote its own outputs), 1 store and write
+                 // half of the late windows, 2 store only (an auto-reset board: the stepping wave writes every window)
+  uint32_t any;  // the board has enemies (enemy windows read the group statistics)
+};
+
+__device__ __forceinline__ void store_outputs(const StepArgs& a, int b, double reward, double ep_ret, int64_t real_def,
+                                              int32_t ep_steps, int32_t fail_def, bool done, int win, uint32_t allow,
+                                              uint32_t cool, int lane) {
+  if (lane != 0) return;
+  sst(&a.reward[b], reward);
+  sst(&a.done[b], (uint8_t)(done ? 1 : 0));
+  if (a.win) sst(&a.win[b], (int8_t)win);
+  if (a.allow_next) sst(&a.allow_next[b], (uint8_t)allow);
+  if (a.cooldowns) sst(&a.cooldowns[b], (uint8_t)cool);
+  if (a.fail_def) sst(&a.fail_def[b], fail_def);
+  if (a.real_def && !a.multi) sst(&a.real_def[b], real_def);
+  if (a.ep_return) sst(&a.ep_return[b], ep_ret);
+  if (a.ep_len) sst(&a.ep_len[b], ep_steps);
+  if (done && a.last_ep) {  // the board's last finished episode (td_episode_records)
+    td_episode_record r;
+    r.ret = ep_ret;
+    r.length = ep_steps;
+    r.win = win;
+    a.last_ep[b] = r;
   }
+  if (done && a.ep_stats) {  // device-side episode accounting (SURVEY §8(b) td_episode_stats)
+    atomicAdd(&a.ep_stats[0], 1.0);
+    atomicAdd(&a.ep_stats[1], ep_ret);
+  }
+}
+__device__ __forceinline__ void store_outputs(const StepArgs& a, int b, const StepOut& o, int lane) {
+  store_outputs(a, b, o.reward, o.ep_ret, o.real_def, o.ep_steps, o.fail_def, o.done != 0u, (int)(int32_t)o.win, o.allow,
+                o.cool, lane);
 }
 
 // ---------------------------------------------------------------------------
@@ -1648,7 +1700,7 @@ __device__ __forceinline__ void ord_place(const StepArgs& a, int b, bool heavy, 
 // observation windows.
 template <int NC, int LT, int MODE, bool SCAN, bool SMALL, bool SPLIT = false, int BPW = 1>
 __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const StepArgs& a, int b, const Prefetch& P,
-                                           int vb) {
+                                           int vb, StepOut* so = nullptr) {
   const TdDevCfg& C = x.C;
   uint32_t* const opp = a.opp_mt + (size_t)b * OPP_WORDS;
   uint32_t* const hot = a.opp_hot + (size_t)b * HOT_WORDS;
@@ -1709,9 +1761,10 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
     if (a.fail_atk && x.lane < 3) a.fail_atk[(size_t)b * 3 + x.lane] = -1;
     if (a.real_atk && x.lane < 24) a.real_atk[(size_t)b * 24 + x.lane] = 4;
     if constexpr (SPLIT) {
-      if (x.lane == 0) { S.early_go = 0u; S.obs_go = 0u; }
+      if (x.lane == 0) { S.early_go = 0u; so->go = 0u; }
       __syncthreads();  // (A)
       __syncthreads();  // (B)
+      __syncthreads();  // (C)
     }
     return;
   }
@@ -1828,16 +1881,13 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
   // otherwise wait for these stores too; a reset board has none).
   store_enemies(S, u, x, a, b);
   STAMP(5);
-  enemy_stats(S, u, x);  // no-op for a board without enemies (e.g. just reset)
-  STAMP(13);
-  channel_scalars(S, u, x);
-  STAMP(14);
-  if (was_reset) {  // the new episode's layout
-    store_cells(S, u, x, a, b);
-    pack_obs_cells(S, x);
+  if constexpr (SPLIT) {
+    // the new episode's layout first (the second wave stores the board next)
+    if (was_reset) {
+      store_cells(S, u, x, a, b);
+      pack_obs_cells(S, x);
+    }
   }
-  store_board(S, u, x, a, b);
-
   if (x.lane == 0) {
     if (was_reset)  // the record has been read into LDS: its slot may be redrawn
       st_relaxed(a.lay_head + b, lay_head + 1u);
@@ -1845,48 +1895,54 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
     sst(&hot[1], R.tw);
     sst(&hot[2], R.cn);
     sst(&hot[3], R.cbase);
-    sst(&a.reward[b], reward);
-    sst(&a.done[b], (uint8_t)(done ? 1 : 0));
-    if (a.win) sst(&a.win[b], win);
-    if (a.allow_next) sst(&a.allow_next[b], allow);
-    if (a.cooldowns) sst(&a.cooldowns[b], cool);
-    if (a.fail_def) sst(&a.fail_def[b], (int32_t)fail_def);
-    if (a.real_def && !a.multi) sst(&a.real_def[b], real_def);
-    if (a.ep_return) sst(&a.ep_return[b], ep_ret);
-    if (a.ep_len) sst(&a.ep_len[b], (int32_t)ep_steps);
-    if (done && a.last_ep) {  // the board's last finished episode (td_episode_records)
-      td_episode_record r;
-      r.ret = ep_ret;
-      r.length = ep_steps;
-      r.win = win;
-      a.last_ep[b] = r;
-    }
-    if (done && a.ep_stats) {  // device-side episode accounting (SURVEY §8(b) td_episode_stats)
-      atomicAdd(&a.ep_stats[0], 1.0);
-      atomicAdd(&a.ep_stats[1], ep_ret);
-    }
   }
   if (refill && x.lane < HOT_CACHE) sst(&hot[4 + x.lane], R.cache);
-  // the observation last: nothing of the step is live any more, the writer has the registers
-  STAMP(6);
   if constexpr (SPLIT) {
-    // (B) the second wave's early pass has landed.  A board that auto-reset this step has
-    // a new layout: this wave rewrites every window (rare); otherwise each wave writes
-    // half of the windows the early pass left.
-    if (x.lane == 0) { S.obs_go = was_reset ? 2u : 1u; S.obs_any = u.n > 0 ? 1u : 0u; }
+    // (B) the second wave's early pass has landed; it takes the board and the outputs
+    // and stores them while this wave computes the statistics and broadcast channels;
+    // (C) both are in LDS: each wave writes half of the windows the early pass left -- a
+    // board that auto-reset this step has a new layout, and this wave rewrites every window.
+    if (x.lane == 0) {  // field by field: no second register copy of the board
+      so->hdr = hdr_of(u);
+      so->nt = u.nt; so->tw_dirty = u.tw_dirty ? 1 : 0;
+      so->reward = reward; so->ep_ret = ep_ret; so->real_def = real_def;
+      so->ep_steps = ep_steps; so->fail_def = fail_def;
+      so->done = done ? 1u : 0u; so->win = (uint32_t)(int32_t)win; so->allow = allow; so->cool = cool;
+      so->go = was_reset ? 2u : 1u; so->any = u.n > 0 ? 1u : 0u;
+    }
     __syncthreads();
+    enemy_stats(S, u, x);  // no-op for a board without enemies (e.g. just reset)
+    STAMP(13);
+    channel_scalars(S, u, x);
+    STAMP(14);
+    __syncthreads();
+    STAMP(6);
     if (was_reset) write_obs_lines<NC, LT>(S, x.lane, obs, u.n > 0, wt, a.edge_wt != 0);
     else write_obs_lines<NC, LT, 0, obs_late_half<LT>(), 4, 2>(S, x.lane, obs, u.n > 0, wt, a.edge_wt != 0);
-  } else if constexpr (LT != 0) {
-    if ((reinterpret_cast<uintptr_t>(a.obs) & 15u) == 0) {
+  } else {
+    enemy_stats(S, u, x);  // no-op for a board without enemies (e.g. just reset)
+    STAMP(13);
+    channel_scalars(S, u, x);
+    STAMP(14);
+    if (was_reset) {  // the new episode's layout
+      store_cells(S, u, x, a, b);
+      pack_obs_cells(S, x);
+    }
+    store_board(S, u, x, a, b);
+    store_outputs(a, b, reward, ep_ret, real_def, ep_steps, fail_def, done, win, allow, cool, x.lane);
+    // the observation last: nothing of the step is live any more, the writer has the registers
+    STAMP(6);
+    if constexpr (LT != 0) {
+      if ((reinterpret_cast<uintptr_t>(a.obs) & 15u) == 0) {
 #ifndef TD_DIAG_NO_OBS  // diagnostic builds only: the step without its observation
-      write_obs_lines<NC, LT>(S, x.lane, obs, u.n > 0, wt, a.edge_wt != 0);
+        write_obs_lines<NC, LT>(S, x.lane, obs, u.n > 0, wt, a.edge_wt != 0);
 #endif
+      } else {
+        write_obs<NC, LT>(S, x, obs, u.n > 0);
+      }
     } else {
       write_obs<NC, LT>(S, x, obs, u.n > 0);
     }
-  } else {
-    write_obs<NC, LT>(S, x, obs, u.n > 0);
   }
   STAMP(7);
   STAMP(8);
@@ -1990,6 +2046,7 @@ __global__ __launch_bounds__(128) TD_SMALL2_ATTR void td_step_kernel_small2(Step
   const StepArgs& a = kargs(a_);
   constexpr int NC = LT * LT;
   __shared__ Smem<NC> S;
+  __shared__ StepOut SO;
   if ((int)blockIdx.x >= a.B) return;
   const int b = ord_board(a, (int)blockIdx.x, 1);
   const int lane = (int)threadIdx.x & 63;
@@ -1998,7 +2055,7 @@ __global__ __launch_bounds__(128) TD_SMALL2_ATTR void td_step_kernel_small2(Step
     const Ctx x{S.cfg, LT, NC, lane, a.cfgs, a.epoch};
     Prefetch P;
     prefetch_issue<PF_SMALL, PF_SMALL>(P, a, b, lane, NC, MODE != MODE_ATK && !a.multi);
-    step_board<NC, LT, MODE, SCAN, true, true>(S, x, a, b, P, (int)blockIdx.x);
+    step_board<NC, LT, MODE, SCAN, true, true>(S, x, a, b, P, (int)blockIdx.x, &SO);
   } else {
     float* const obs = a.obs + (size_t)b * NCH * NC;
     __syncthreads();  // (A) actions and towers final, cells packed
@@ -2007,9 +2064,17 @@ __global__ __launch_bounds__(128) TD_SMALL2_ATTR void td_step_kernel_small2(Step
       // landed before (B): after an auto-reset the first wave rewrites these windows
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    __syncthreads();  // (B)
-    if (S.obs_go == 1u)
-      write_obs_lines<NC, LT, obs_late_half<LT>(), -1, 4, 2>(S, lane, obs, S.obs_any != 0u, a.obs_wt != 0,
+    __syncthreads();  // (B) the board after the step and its outputs are in SO
+    const uint32_t go = SO.go;
+    if (go) {
+      static_assert(sizeof(TdHdr) == 6 * 16 && offsetof(StepOut, hdr) == 0, "header copied as 6 x 16 B");
+      if (lane < 6) reinterpret_cast<uint4*>(a.hdr + b)[lane] = reinterpret_cast<const uint4*>(&SO.hdr)[lane];
+      store_towers(S, SO.nt, SO.tw_dirty != 0, lane, a, b);
+      store_outputs(a, b, SO, lane);
+    }
+    __syncthreads();  // (C) statistics and broadcast channels in LDS
+    if (go == 1u)
+      write_obs_lines<NC, LT, obs_late_half<LT>(), -1, 4, 2>(S, lane, obs, SO.any != 0u, a.obs_wt != 0,
                                                             a.edge_wt != 0);
   }
 }

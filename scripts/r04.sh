@@ -153,5 +153,20 @@ s8)  # 30x30 bisect (builds of commits 9f7a2e2 / bf5cc12 vs current); summon-cos
     done; done
   done
   ;;
+s9)  # two-wave kernel: the second wave stores the board and the outputs (offload) vs the previous build (pre)
+  gpusuite 900; rc=$?; [ $rc -le 1 ] || exit $rc
+  V=$PWD/gym-td_amd/lib/variants
+  for r in 1 2; do
+    for v in prod pre; do
+      lib=$V/libtdstep_$v.so; [ $v = prod ] && lib=$PWD/gym-td_amd/lib/libtdstep.so
+      for bb in 4096 2048 16384; do
+        TDSTEP_LIB=$lib run ${v}_${bb}_$r 200 python bench.py --global-batch $bb --no-cpu-baseline --steps 2000 --timing none || exit 1; line ${v}_${bb}_$r
+      done
+      TDSTEP_LIB=$lib run ${v}_l30_$r 300 python bench.py --workload def-large --global-batch 16384 --no-cpu-baseline --steps 200 --timing none || exit 1; line ${v}_l30_$r
+    done
+  done
+  TDSTEP_LIB=$PWD/gym-td_amd/lib/libtdstep_stamps.so run phases_4096 300 python scripts/probe_phases.py 4096 10 600 || exit 1
+  grep -E "rt |tail|cycles/wave" $O/phases_4096.log
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
