@@ -168,5 +168,16 @@ s9)  # two-wave kernel: the second wave stores the board and the outputs (offloa
   TDSTEP_LIB=$PWD/gym-td_amd/lib/libtdstep_stamps.so run phases_4096 300 python scripts/probe_phases.py 4096 10 600 || exit 1
   grep -E "rt |tail|cycles/wave" $O/phases_4096.log
   ;;
+s10)  # the profile of the current build: kernel trace + PMC per workload; smoke; driver command; small2 at 2p / 8,192
+  run smoke 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" || exit 1
+  for wb in "def-small 65536" "def-small 8192" "def-small 4096" "2p-middle-multi 16384" "def-large 16384"; do set -- $wb
+    NO_PHASES=1 PROF_DIR=$O/prof_$1_$2 WL=$1 B=$2 run prof_$1_$2 900 bash scripts/profile_session.sh || exit 1
+  done
+  run bench_driver 300 python bench.py --gpus 1 --steps 20 --warmup 5 || exit 1; grep '^{' $O/bench_driver.log; line bench_driver
+  for r in 1 2; do
+    run p2_small2_$r 300 python bench.py --workload 2p-middle-multi --no-cpu-baseline --steps 200 --timing none --step-kernel small2 || exit 1; line p2_small2_$r
+    run b8192_small2_$r 200 python bench.py --global-batch 8192 --no-cpu-baseline --steps 2000 --timing none --step-kernel small2 || exit 1; line b8192_small2_$r
+  done
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
