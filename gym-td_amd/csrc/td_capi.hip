@@ -1013,6 +1013,13 @@ int td_debug_ring(td_handle* h, int b, uint32_t* out, int cap) {
   return 3 + NSLOT;
 }
 
+int td_board_map(int n_boards, int kind, int xcd_map, int32_t* out) {
+  if (n_boards < 1 || !out || kind < 0 || kind > 1) return fail("td_board_map: bad arguments");
+  for (int i = 0; i < n_boards; ++i)
+    out[i] = !xcd_map ? i : kind == 0 ? xcd_board(i, n_boards) : xcd_board_v(i, n_boards, 1);
+  return 0;
+}
+
 void td_py_seed(uint32_t* mt, uint32_t seed) { py_seed(mt, seed); }
 void td_np_seed(uint32_t* mt, uint32_t seed) { np_seed(mt, seed); }
 uint32_t td_mt_next(uint32_t* mt) { return MtRef{mt}.next(); }

@@ -265,6 +265,12 @@ int td_export_state(td_handle* h, int b0, int count, void* host_dst);
 int td_import_state(td_handle* h, int b0, int count, const void* host_src);
 int td_get_flags(td_handle* h, int32_t* host_flags);
 
+/* The board each step-kernel block steps (diagnostic; no GPU needed): out[i] for blocks
+ * i in [0, n_boards).  kind 0: the large kernel's XCD-contiguous map (block i runs on XCD
+ * i % 8 and steps the (i / 8)-th board of that XCD's contiguous range); kind 1: the same for
+ * the small kernels' order lists at boards_per_workgroup = 1.  xcd_map = 0: block i = board i. */
+int td_board_map(int n_boards, int kind, int xcd_map, int32_t* out);
+
 /* Host-side RNG helpers (exposed for tests and for seeding from Python states). */
 void td_py_seed(uint32_t* mt625, uint32_t seed);
 void td_np_seed(uint32_t* mt625, uint32_t seed);

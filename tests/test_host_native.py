@@ -216,3 +216,22 @@ def test_cpu_oracle_follows_the_hopeless_rule():
         finally:
             env.close()
     assert checked >= 1
+
+
+@pytest.mark.parametrize("B", [1, 2, 7, 8, 9, 15, 16, 17, 100, 1000, 4095, 4096, 8192, 65536, 65537])
+def test_board_map_is_an_xcd_contiguous_permutation(B):
+    """td_board_map: every board stepped by exactly one block; the blocks of one XCD
+    (i % 8) step one contiguous range of boards, in block order (neighbouring boards share
+    an L2), and the ranges follow each other by XCD."""
+    for kind in (0, 1):
+        m = np.zeros(B, np.int32)
+        assert lib.td_board_map(B, kind, 1, _lib.ptr(m, _lib.ctypes.c_int32)) == 0
+        assert np.array_equal(np.sort(m), np.arange(B))
+        start = 0
+        for x in range(8):
+            mine = m[x::8]
+            assert np.array_equal(mine, np.arange(start, start + len(mine)))
+            start += len(mine)
+        ident = np.zeros(B, np.int32)
+        assert lib.td_board_map(B, kind, 0, _lib.ptr(ident, _lib.ctypes.c_int32)) == 0
+        assert np.array_equal(ident, np.arange(B))
