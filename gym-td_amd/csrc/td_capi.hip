@@ -504,13 +504,16 @@ td_handle* td_create(const td_config* cfg, int map_size, int n_boards, int mode,
      // halved residency costs (single-action boards, profiles/r03/s7, same box: 10x10
      // 12,288 / 16,384 boards 237.8 / 255.4 vs 224.0 / 238.5 M env-steps/s with the large
      // kernel, 32,768 a tie; 30x30 16,384 / 32,768 boards 30.8 / 31.9 vs 29.8 / 31.2 M, 65,536
-     // 30.0 vs 30.2 M; TD-2p 20x20 multi-action at 16,384: 48.0 vs 51.5 M, kept large).
+     // 30.0 vs 30.2 M; TD-2p 20x20 multi-action at 16,384: 48.0 vs 51.5 M in round 3, 54.0 vs
+     // 52.1 M on the round-4 build, r04/s10).
      // td_set_step_kernel overrides.
     int cus = 0;
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
     const int resident = step_resident_boards(base_args(h), cus, 1);
     const int resident2 = step_resident_boards(base_args(h), cus, 2);
-    const int rounds2 = h->multi ? 0 : h->L == 10 ? 3 : h->L == 30 ? 10 : 0;  // two-wave kernel up to this many rounds
+    // two-wave kernel up to this many rounds (TD-2p 20x20 multi-action at 16,384 boards:
+    // 303.3-303.6 vs 314-315 us per step with the large kernel, profiles/r04/s10)
+    const int rounds2 = h->multi ? (h->L == 20 && h->mode == TD_MODE_2P ? 8 : 0) : h->L == 10 ? 3 : h->L == 30 ? 10 : 0;
     h->small_auto = n_boards <= resident2 ? 2 : n_boards <= resident ? 1 : n_boards <= rounds2 * resident ? 2 : 0;
     if (apply_kernel(h, h->small_auto)) { std::string e = g_err; td_destroy(h); g_err = e; return nullptr; }
     if (const char* e = std::getenv("TD_REFILL_EVERY")) h->refill_every = std::max(0, std::atoi(e));  // A/B runs

@@ -2160,7 +2160,7 @@ __device__ __forceinline__ RoadResume* resume_hdr(const StepArgs& a, int b) {
 // stream: plain stores, every lane's vmcnt(0), the barrier, ONE agent-scope
 // release, then the tag by an sc1 store (MI355X_MICROARCH.md § visibility, "Valid
 // forms", producer bullet).  Returns the road status of the last draw.
-template <int NC>
+template <int NC, bool SB = false>
 __device__ int wave_layout(LayoutSmem<NC>& G, const StepArgs& a, int b, int retries, uint32_t* slot, uint32_t n,
                            int budget) {
   const int lane = (int)threadIdx.x, L = a.L, lw = LAYOUT_HDR + L * L;
@@ -2182,7 +2182,7 @@ __device__ int wave_layout(LayoutSmem<NC>& G, const StepArgs& a, int b, int retr
   }
   int st = ROAD_ERR_BOUND;
   {
-    WaveRoadGen<NC> g;
+    WaveRoadGen<NC, false, SB> g;
     g.carve(G.scratch, L * L);
     g.mt = G.mt; g.rec = G.rec; g.L = L; g.lane = lane;
     // the stream position and the resume state are wave-uniform: SGPRs
@@ -2192,16 +2192,10 @@ __device__ int wave_layout(LayoutSmem<NC>& G, const StepArgs& a, int b, int retr
     RoadResume res;
     for (int i = 0; i < 16; ++i)
       reinterpret_cast<uint32_t*>(&res)[i] = __builtin_amdgcn_readfirstlane(reinterpret_cast<const uint32_t*>(&G.res)[i]);
-    const int nw = (L * L + 31) / 32;
-    if (resumed) {  // the draw's field / turn bitmaps
-      g.field = lane < nw ? g.fieldw[lane] : 0u;
-      g.rot = lane < nw ? g.rotw[lane] : 0u;
-    } else {
-      g.field = g.rot = 0u;
-    }
+    g.load_maps(resumed);  // the draw's field / turn bitmaps
     st = g.draw(res, budget, kRoadAttempts, retries);
     __syncthreads();
-    if (lane < nw) { g.fieldw[lane] = g.field; g.rotw[lane] = g.rot; }
+    g.save_maps();
     if (lane == 0) { G.mt[MT_N] = g.pos; G.mt[MT_N + 1] = g.tw; G.res = res; }
 #ifdef TD_GEN_STAMPS
     if (a.stamps && lane == 0) {
@@ -2255,13 +2249,7 @@ __device__ __attribute__((noinline)) int draw_in_place(const StepArgs& a, int b,
   const uint32_t hw = lane < 16 ? ghdr[lane] : 0u;
   RoadResume res;
   for (int i = 0; i < 16; ++i) reinterpret_cast<uint32_t*>(&res)[i] = rdl(hw, i);
-  const int nw = (L * L + 31) / 32;
-  if (res.phase != RP_NEW) {  // the bitmaps of the draw a refill left pending (its partial record is in the slot)
-    g.field = lane < nw ? g.fieldw[lane] : 0u;
-    g.rot = lane < nw ? g.rotw[lane] : 0u;
-  } else {
-    g.field = g.rot = 0u;
-  }
+  g.load_maps(res.phase != RP_NEW);  // the bitmaps of the draw a refill left pending (its partial record is in the slot)
   const int st = g.draw(res, 0x7fffffff, kRoadAttempts, kLayoutRetries);
   g.sync();
   if (lane == 0) { gmt[MT_N] = g.pos; gmt[MT_N + 1] = g.tw; }
@@ -2476,7 +2464,8 @@ __global__ __launch_bounds__(64) void td_refill_kernel(StepArgs a, int guard) {
         uint32_t* slot = a.nxt + ((size_t)bb * NSLOT + t % NSLOT) * a.slot_words;
         // an empty ring is urgent (the board needs this layout at its next episode end):
         // its draw runs to the end; otherwise at most a.refill_walks walks this launch
-        const int st = wave_layout(G, a, bb, kLayoutRetries, slot, t, t == h || guard ? 0x7fffffff : a.refill_walks);
+        const int st = wave_layout<NC, kGenSB && NC <= 128>(G, a, bb, kLayoutRetries, slot, t,
+                                                            t == h || guard ? 0x7fffffff : a.refill_walks);
         __syncthreads();
         if (st != ROAD_OK) break;  // out of walks (continued next launch), or 65 failing draws in a row
         ++t;

@@ -30,7 +30,17 @@ struct LayoutSmem {
 // v_readlane.  Control flow is wave-uniform.  The road lists stay in LDS (the resumable
 // state); the main road, its branch points and the stamping of a road onto the record
 // run one cell per lane (an accepted road is shorter than 2L <= 64 cells).
-template <int NC, bool GM = false>
+// SB: boards of at most 128 cells (L <= 11) keep both bitmaps as two wave-uniform 64-bit
+// words each (bit c of word c / 64): a walk step's test and set, the erase and the
+// branch-point scan are scalar bit operations, and the hopeless-branch search shifts a
+// 128-bit frontier instead of exchanging lane words.  Used by the refill kernel (kGenSB;
+// TD_GEN_SB=0: the lane-word form everywhere, A/B builds); the reset kernels keep the
+// lane-word form (they have no registers to spare).
+#ifndef TD_GEN_SB
+#define TD_GEN_SB 1
+#endif
+constexpr bool kGenSB = TD_GEN_SB != 0;
+template <int NC, bool GM = false, bool SB = false>
 struct WaveRoadGen {
   // GM: the stream, the record and the scratch arrays are in global memory, not LDS
   // (td_step.hip draw_in_place): a hand-off between lanes then also waits for the
@@ -48,7 +58,8 @@ struct WaveRoadGen {
   uint32_t *fieldw, *rotw;  // the bitmaps' resumable copies in the scratch
   int L, lane;
   uint32_t pos, tw, base, n, win;
-  uint32_t field, rot;
+  uint32_t field, rot;          // lane-word form: lane j holds cells [32j, 32j + 32)
+  uint64_t fs0, fs1, rs0, rs1;  // SB form: cells [0, 64) and [64, 128)
 #ifdef TD_GEN_STAMPS  // diagnostic builds: s_memtime cycles by part of the draw (scripts/probe_draw.py)
   uint64_t cyc[6] = {0, 0, 0, 0, 0, 0};  // walk, proof, stamp, erase, stream window, walks
 #define GEN_T0() const uint64_t gen_t0_ = __builtin_amdgcn_s_memtime()
@@ -118,6 +129,56 @@ struct WaveRoadGen {
   __device__ __forceinline__ uint32_t without(uint32_t m, int c) const {
     return m & ~(lane == (c >> 5) ? 1u << (c & 31) : 0u);
   }
+  static __device__ __forceinline__ bool sbit(uint64_t w0, uint64_t w1, int c) {
+    return (((c < 64 ? w0 : w1) >> (c & 63)) & 1ull) != 0;
+  }
+  static __device__ __forceinline__ void sset(uint64_t& w0, uint64_t& w1, int c) {
+    if (c < 64) w0 |= 1ull << c; else w1 |= 1ull << (c - 64);
+  }
+  static __device__ __forceinline__ void sclr(uint64_t& w0, uint64_t& w1, int c) {
+    if (c < 64) w0 &= ~(1ull << c); else w1 &= ~(1ull << (c - 64));
+  }
+  __device__ __forceinline__ bool fbit(int c) const { if constexpr (SB) return sbit(fs0, fs1, c); else return bit(field, c); }
+  __device__ __forceinline__ bool rbit(int c) const { if constexpr (SB) return sbit(rs0, rs1, c); else return bit(rot, c); }
+  __device__ __forceinline__ void fset(int c) { if constexpr (SB) sset(fs0, fs1, c); else field = with(field, c); }
+  __device__ __forceinline__ void rset(int c) { if constexpr (SB) sset(rs0, rs1, c); else rot = with(rot, c); }
+  __device__ __forceinline__ void clear_maps() {
+    if constexpr (SB) fs0 = fs1 = rs0 = rs1 = 0ull;
+    else field = rot = 0u;
+  }
+  // The bitmaps from / to their resumable copies (fieldw / rotw: u32 word i = cells [32i, 32i + 32)).
+  __device__ __forceinline__ void load_maps(bool resumed) {
+    const int nw = (L * L + 31) / 32;
+    if constexpr (SB) {
+      fs0 = fs1 = rs0 = rs1 = 0ull;
+      if (resumed) {
+        sync();
+        uint32_t fw[4], rw[4];
+        for (int i = 0; i < 4; ++i) {
+          fw[i] = i < nw ? __builtin_amdgcn_readfirstlane(fieldw[i]) : 0u;
+          rw[i] = i < nw ? __builtin_amdgcn_readfirstlane(rotw[i]) : 0u;
+        }
+        fs0 = (uint64_t)fw[0] | ((uint64_t)fw[1] << 32); fs1 = (uint64_t)fw[2] | ((uint64_t)fw[3] << 32);
+        rs0 = (uint64_t)rw[0] | ((uint64_t)rw[1] << 32); rs1 = (uint64_t)rw[2] | ((uint64_t)rw[3] << 32);
+      }
+    } else {
+      field = resumed && lane < nw ? fieldw[lane] : 0u;
+      rot = resumed && lane < nw ? rotw[lane] : 0u;
+    }
+  }
+  __device__ __forceinline__ void save_maps() {
+    const int nw = (L * L + 31) / 32;
+    if constexpr (SB) {
+      if (lane < nw) {
+        const uint64_t f = lane < 2 ? fs0 : fs1, r = lane < 2 ? rs0 : rs1;
+        fieldw[lane] = (uint32_t)(f >> (32 * (lane & 1)));
+        rotw[lane] = (uint32_t)(r >> (32 * (lane & 1)));
+      }
+    } else if (lane < nw) {
+      fieldw[lane] = field;
+      rotw[lane] = rot;
+    }
+  }
   __device__ __forceinline__ bool inner(int r, int c) const { return r > 0 && r < L - 1 && c > 0 && c < L - 1; }
 
   // generate_road (TDRoadGen.py:31-119), as RoadGen::walk; *last = the last cell appended
@@ -133,11 +194,11 @@ struct WaveRoadGen {
         for (int k = 0; k < k_max; ++k) {
           pr += dr; pc += dc;
           const int cell = pr * L + pc;
-          if (bit(field, cell)) { pr -= dr; pc -= dc; cross = true; return; }
+          if (fbit(cell)) { pr -= dr; pc -= dc; cross = true; return; }
           if (reset_cross) cross = false;
           if (lane == 0) out[cnt] = (uint16_t)cell;
           ++cnt;
-          field = with(field, cell);
+          fset(cell);
           if (!inner(pr, pc)) return;
         }
       };
@@ -149,13 +210,13 @@ struct WaveRoadGen {
         int rd;
         if (pending != 0) { rd = pending; pending = 0; }
         else { rd = np_randint(0, 2) * 2 - 1; pending = -rd; }
-        rot = with(rot, pr * L + pc);
+        rset(pr * L + pc);
         d = (d + 4 + rd) % 4;
         run(seg, d, true);
       }
       if (cross) {  // the free neighbours in direction order, one picked at random
-        const uint32_t fm = (bit(field, (pr + 1) * L + pc) ? 0u : 1u) | (bit(field, pr * L + pc - 1) ? 0u : 2u) |
-                            (bit(field, (pr - 1) * L + pc) ? 0u : 4u) | (bit(field, pr * L + pc + 1) ? 0u : 8u);
+        const uint32_t fm = (fbit((pr + 1) * L + pc) ? 0u : 1u) | (fbit(pr * L + pc - 1) ? 0u : 2u) |
+                            (fbit((pr - 1) * L + pc) ? 0u : 4u) | (fbit(pr * L + pc + 1) ? 0u : 8u);
         const int nf = __popc(fm);
         if (nf == 0) { *len = cnt; *last = pr * L + pc; return 0; }
         int pick = np_randint(0, nf);
@@ -163,7 +224,7 @@ struct WaveRoadGen {
         while (pick-- > 0) m &= m - 1;
         d = __builtin_ctz(m);
         pending = 0;
-        rot = with(rot, pr * L + pc);
+        rset(pr * L + pc);
       }
     }
     *len = cnt;
@@ -189,7 +250,54 @@ struct WaveRoadGen {
   // from each candidate branch point picks[klo, khi) over the free cells, one frontier
   // bitmap step per walk length; true when no candidate reaches a border cell at
   // Manhattan distance >= 3L/4 from endc in fewer than 2L - (nm - index) cells.
+  // 128-bit shifts of an SB bitmap (0 < sh < 64)
+  static __device__ __forceinline__ void shl128(uint64_t& lo, uint64_t& hi, int sh) {
+    hi = (hi << sh) | (lo >> (64 - sh)); lo <<= sh;
+  }
+  static __device__ __forceinline__ void shr128(uint64_t& lo, uint64_t& hi, int sh) {
+    lo = (lo >> sh) | (hi << (64 - sh)); hi >>= sh;
+  }
+  __device__ bool hopeless_sb(int klo, int khi, int nm, int endc) {
+    const int ncells = L * L, dmin = L * 3 / 4;
+    // masks by ballot: lane l tests cells l and 64 + l
+    uint64_t valid[2], first[2], last[2], inn[2], qual[2];
+    for (int h = 0; h < 2; ++h) {
+      const int c = 64 * h + lane, r = c / L, cc = c - r * L;
+      const bool v = c < ncells;
+      valid[h] = ballot(v);
+      first[h] = ballot(v && cc == 0);
+      last[h] = ballot(v && cc == L - 1);
+      inn[h] = ballot(v && inner(r, cc));
+      qual[h] = ballot(v && !inner(r, cc) && iabs(r - endc / L) + iabs(cc - endc % L) >= dmin);
+    }
+    sync();
+    for (int k = klo; k < khi; ++k) {
+      const uint32_t pk = picks[k];
+      const int bc = (int)(pk & 0xffffu), lim = 2 * L - (nm - (int)(pk >> 16));
+      if (lim <= 0) continue;                      // every walk from here is too long
+      if (!inner(bc / L, bc % L)) return false;    // an empty branch: IndexError (:189), not a hang
+      uint64_t F0 = bc < 64 ? 1ull << bc : 0ull, F1 = bc < 64 ? 0ull : 1ull << (bc - 64);
+      uint64_t V0 = F0 | fs0, V1 = F1 | fs1;
+      for (int d = 1; d < lim; ++d) {
+        uint64_t a0 = F0 & ~last[0], a1 = F1 & ~last[1];
+        shl128(a0, a1, 1);
+        uint64_t b0 = F0 & ~first[0], b1 = F1 & ~first[1];
+        shr128(b0, b1, 1);
+        uint64_t c0 = F0, c1 = F1;
+        shl128(c0, c1, L);
+        uint64_t e0 = F0, e1 = F1;
+        shr128(e0, e1, L);
+        const uint64_t N0 = (a0 | b0 | c0 | e0) & valid[0] & ~V0, N1 = (a1 | b1 | c1 | e1) & valid[1] & ~V1;
+        if ((N0 & qual[0]) | (N1 & qual[1])) return false;  // a walk could end here
+        V0 |= N0; V1 |= N1;
+        F0 = N0 & inn[0]; F1 = N1 & inn[1];
+        if (!(F0 | F1)) break;
+      }
+    }
+    return true;
+  }
   __device__ bool hopeless(int klo, int khi, int nm, int endc) {
+    if constexpr (SB) return hopeless_sb(klo, khi, nm, endc);
     const int ncells = L * L, dmin = L * 3 / 4;
     uint32_t valid = 0, first = 0, last = 0, inn = 0, qual = 0;
     for (int i = 0; i < 32; ++i) {
@@ -229,8 +337,13 @@ struct WaveRoadGen {
       const int m = cnt - i0 < 64 ? cnt - i0 : 64;
       for (int i = 0; i < m; ++i) {
         const int c = (int)rdl(cv, i);
-        field = without(field, c);
-        rot = without(rot, c);
+        if constexpr (SB) {
+          sclr(fs0, fs1, c);
+          sclr(rs0, rs1, c);
+        } else {
+          field = without(field, c);
+          rot = without(rot, c);
+        }
       }
     }
   }
@@ -280,11 +393,11 @@ struct WaveRoadGen {
         const int nr = (int)st.nr;
         if (L < 4 || L > MAX_L || nr < 1 || nr > 3) { status = ROAD_ERR_ARGS; goto failed; }
         if (L / 4 <= L * 3 / 20) { status = ROAD_ERR_RANDINT; goto failed; }  // segment randint raises (:41)
-        field = 0u; rot = 0u;
+        clear_maps();
         const int lo = L / 3, hi = (L * 2 + 2) / 3;
         st.cr = (uint32_t)np_randint(lo, hi);
         st.cc = (uint32_t)np_randint(lo, hi);
-        field = with(field, (int)(st.cr * L + st.cc));
+        fset((int)(st.cr * L + st.cc));
         st.d0 = (uint32_t)np_randint(0, 4);
         st.phase = RP_ROAD1; st.att = 0;
       }
@@ -368,8 +481,8 @@ struct WaveRoadGen {
           uint32_t pk = 0;
           for (int i = 0; i < tot;) {
             const int ci = (int)rdl(cv, i);
-            if (!bit(rot, ci)) {
-              if (i < tot - 1 && !bit(rot, (int)rdl(cv, i + 1))) {
+            if (!rbit(ci)) {
+              if (i < tot - 1 && !rbit((int)rdl(cv, i + 1))) {
                 if (lane == np) pk = ((uint32_t)i << 16) | (uint32_t)ci;
                 ++np;
               }

@@ -179,5 +179,21 @@ s10)  # the profile of the current build: kernel trace + PMC per workload; smoke
     run b8192_small2_$r 200 python bench.py --global-batch 8192 --no-cpu-baseline --steps 2000 --timing none --step-kernel small2 || exit 1; line b8192_small2_$r
   done
   ;;
+s11)  # scalar-bitmap road generator in the refill kernel (prod) vs lane words (nosb): roadgen parity, draw cycles, small shares; 2p rule
+  gpusuite 900; rc=$?; [ $rc -le 1 ] || exit $rc
+  V=$PWD/gym-td_amd/lib/variants
+  for v in sb nosb; do
+    TDSTEP_LIB=$V/libtdstep_gs_$v.so run parts_${v} 300 python scripts/probe_draw_parts.py 1024 10 || exit 1; cat $O/parts_${v}.log | grep -v amdgpu
+  done
+  for r in 1 2; do
+    for v in prod nosb; do
+      lib=$V/libtdstep_$v.so; [ $v = prod ] && lib=$PWD/gym-td_amd/lib/libtdstep.so
+      for bb in 8192 4096; do
+        TDSTEP_LIB=$lib run ${v}_${bb}_$r 200 python bench.py --global-batch $bb --no-cpu-baseline --steps 2000 --timing none || exit 1; line ${v}_${bb}_$r
+      done
+    done
+    run p2_$r 300 python bench.py --workload 2p-middle-multi --no-cpu-baseline --steps 200 --timing none || exit 1; line p2_$r
+  done
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
