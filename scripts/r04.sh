@@ -194,6 +194,11 @@ s11)  # scalar-bitmap road generator in the refill kernel (prod) vs lane words (
     done
     run p2_$r 300 python bench.py --workload 2p-middle-multi --no-cpu-baseline --steps 200 --timing none || exit 1; line p2_$r
   done
+  # the profile of this build (kernel trace + PMC per workload) and the driver's command
+  for wb in "def-small 65536" "def-small 8192" "def-small 4096" "2p-middle-multi 16384" "def-large 16384"; do set -- $wb
+    NO_PHASES=1 PROF_DIR=$O/prof_$1_$2 WL=$1 B=$2 run prof_$1_$2 900 bash scripts/profile_session.sh || exit 1
+  done
+  run bench_driver 300 python bench.py --gpus 1 --steps 20 --warmup 5 || exit 1; grep '^{' $O/bench_driver.log; line bench_driver
   ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
