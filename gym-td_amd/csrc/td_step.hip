@@ -2160,7 +2160,7 @@ __device__ __forceinline__ RoadResume* resume_hdr(const StepArgs& a, int b) {
 // stream: plain stores, every lane's vmcnt(0), the barrier, ONE agent-scope
 // release, then the tag by an sc1 store (MI355X_MICROARCH.md § visibility, "Valid
 // forms", producer bullet).  Returns the road status of the last draw.
-template <int NC, bool SB = false>
+template <int NC, bool SB = false, bool SBP = false>
 __device__ int wave_layout(LayoutSmem<NC>& G, const StepArgs& a, int b, int retries, uint32_t* slot, uint32_t n,
                            int budget) {
   const int lane = (int)threadIdx.x, L = a.L, lw = LAYOUT_HDR + L * L;
@@ -2182,7 +2182,7 @@ __device__ int wave_layout(LayoutSmem<NC>& G, const StepArgs& a, int b, int retr
   }
   int st = ROAD_ERR_BOUND;
   {
-    WaveRoadGen<NC, false, SB> g;
+    WaveRoadGen<NC, false, SB, SBP> g;
     g.carve(G.scratch, L * L);
     g.mt = G.mt; g.rec = G.rec; g.L = L; g.lane = lane;
     // the stream position and the resume state are wave-uniform: SGPRs
@@ -2464,8 +2464,8 @@ __global__ __launch_bounds__(64) void td_refill_kernel(StepArgs a, int guard) {
         uint32_t* slot = a.nxt + ((size_t)bb * NSLOT + t % NSLOT) * a.slot_words;
         // an empty ring is urgent (the board needs this layout at its next episode end):
         // its draw runs to the end; otherwise at most a.refill_walks walks this launch
-        const int st = wave_layout<NC, kGenSB && NC <= 128>(G, a, bb, kLayoutRetries, slot, t,
-                                                            t == h || guard ? 0x7fffffff : a.refill_walks);
+        const int st = wave_layout<NC, kGenSB && NC <= 128, kGenSBProof && NC <= 128>(
+            G, a, bb, kLayoutRetries, slot, t, t == h || guard ? 0x7fffffff : a.refill_walks);
         __syncthreads();
         if (st != ROAD_OK) break;  // out of walks (continued next launch), or 65 failing draws in a row
         ++t;

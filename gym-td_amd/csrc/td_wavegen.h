@@ -33,14 +33,23 @@ struct LayoutSmem {
 // SB: boards of at most 128 cells (L <= 11) keep both bitmaps as two wave-uniform 64-bit
 // words each (bit c of word c / 64): a walk step's test and set, the erase and the
 // branch-point scan are scalar bit operations, and the hopeless-branch search shifts a
-// 128-bit frontier instead of exchanging lane words.  Used by the refill kernel (kGenSB;
-// TD_GEN_SB=0: the lane-word form everywhere, A/B builds); the reset kernels keep the
-// lane-word form (they have no registers to spare).
+// 128-bit frontier instead of exchanging lane words.  Measured per draw (r04/s11,
+// probe_draw_parts, 1,024 boards at L = 10): the search 17.5 k -> 3.7 k cycles, but a
+// walk 6.8 k -> 7.3 k (64-bit maps held in VGPRs: the refill kernel has no SGPRs to spare),
+// 76.9 k -> 66.5 k per draw.  So the product keeps lane-word bitmaps for the walks and
+// runs only the search on scalar words (SBP, kGenSBProof); TD_GEN_SB=1 builds use SB for
+// all.  Both in the refill kernel only: the reset kernels have no registers to spare.
 #ifndef TD_GEN_SB
-#define TD_GEN_SB 1
+#define TD_GEN_SB 0
 #endif
 constexpr bool kGenSB = TD_GEN_SB != 0;
-template <int NC, bool GM = false, bool SB = false>
+// The hopeless-branch search on scalar words at L <= 11 whatever form the bitmaps have
+// (TD_GEN_SB_PROOF=0: lane words, A/B builds).
+#ifndef TD_GEN_SB_PROOF
+#define TD_GEN_SB_PROOF 1
+#endif
+constexpr bool kGenSBProof = TD_GEN_SB_PROOF != 0;
+template <int NC, bool GM = false, bool SB = false, bool SBP = false>  // SBP: the search on scalar words
 struct WaveRoadGen {
   // GM: the stream, the record and the scratch arrays are in global memory, not LDS
   // (td_step.hip draw_in_place): a hand-off between lanes then also waits for the
@@ -257,7 +266,8 @@ struct WaveRoadGen {
   static __device__ __forceinline__ void shr128(uint64_t& lo, uint64_t& hi, int sh) {
     lo = (lo >> sh) | (hi << (64 - sh)); hi >>= sh;
   }
-  __device__ bool hopeless_sb(int klo, int khi, int nm, int endc) {
+  // (fs0, fs1: the field as scalar words -- SB form, or converted from the lane words)
+  __device__ bool hopeless_sb(int klo, int khi, int nm, int endc, uint64_t fs0, uint64_t fs1) {
     const int ncells = L * L, dmin = L * 3 / 4;
     // masks by ballot: lane l tests cells l and 64 + l
     uint64_t valid[2], first[2], last[2], inn[2], qual[2];
@@ -297,7 +307,14 @@ struct WaveRoadGen {
     return true;
   }
   __device__ bool hopeless(int klo, int khi, int nm, int endc) {
-    if constexpr (SB) return hopeless_sb(klo, khi, nm, endc);
+    if constexpr (SB) return hopeless_sb(klo, khi, nm, endc, fs0, fs1);
+    if constexpr (NC <= 128 && SBP) {
+      // the lane-word field as two scalar words (lane l: cells l and 64 + l), then the
+      // scalar search: 4.7x faster than the lane-word search (r04/s11 probe_draw_parts)
+      const uint32_t w0 = (uint32_t)__shfl((int)field, lane >> 5), w1 = (uint32_t)__shfl((int)field, 2 + (lane >> 5));
+      return hopeless_sb(klo, khi, nm, endc, ballot(((w0 >> (lane & 31)) & 1u) != 0u),
+                         ballot(((w1 >> (lane & 31)) & 1u) != 0u));
+    }
     const int ncells = L * L, dmin = L * 3 / 4;
     uint32_t valid = 0, first = 0, last = 0, inn = 0, qual = 0;
     for (int i = 0; i < 32; ++i) {

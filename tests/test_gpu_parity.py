@@ -235,9 +235,11 @@ def test_full_size_properties(L, B, mode, multi, steps, kernel):
         if kernel == "auto" and torch.cuda.get_device_properties(0).multi_processor_count == 256:
             # td_create's rule on a 256-CU MI355X: two waves per board up to half a round of
             # waves, one round (8 per SIMD) -> small kernel, then two waves per board again
-            # over a few rounds (10x10: 3, 30x30: 10; multi-action boards: large)
+            # over a few rounds (10x10: 3, 30x30: 10, TD-2p 20x20 multi-action: 8; other
+            # multi-action boards: large)
             want = {(10, 4096): "small2", (10, 8192): "small", (10, 16384): "small2", (10, 65536): "large",
-                    (20, 16384): "large", (30, 16384): "small2"}[(L, B)]
+                    (20, 16384): "small2" if mode == "2p" and multi else "large",
+                    (30, 16384): "small2"}[(L, B)]
             assert eng.step_kernel == want, eng.step_kernel_name
         obs, failed = eng.reset()
         good = np.ones(B, bool)
