@@ -1,0 +1,92 @@
+// launch_ramp.hip -- diagnostic: how fast one-round grids of 64-thread workgroups get
+// their waves started on this part, and what slows the ramp: static LDS per workgroup,
+// the VGPR allocation, and work the already-started waves do (VALU, memory, sleep).
+// Each wave stores s_memrealtime (100 MHz, chip-wide) at its start and end.
+//   hipcc --offload-arch=gfx950 -O3 scripts/launch_ramp.hip -o scripts/bin/launch_ramp
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <vector>
+
+#define CK(x)                                                             \
+  do {                                                                    \
+    hipError_t e_ = (x);                                                  \
+    if (e_ != hipSuccess) {                                               \
+      std::printf("%s: %s\n", #x, hipGetErrorString(e_));                 \
+      return 1;                                                           \
+    }                                                                     \
+  } while (0)
+
+// WORK: 0 none, 1 VALU loop (~10 us), 2 memory (16 loads + 18 1-KB stores), 3 s_sleep (~10 us)
+template <int LDS, int WORK>
+__global__ __launch_bounds__(64) void k_ramp(uint64_t* t, float* buf, int iters) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  __shared__ float s[LDS > 0 ? LDS / 4 : 1];
+  float acc = (float)threadIdx.x;
+  if constexpr (LDS > 0) {
+    s[threadIdx.x] = acc;
+    __builtin_amdgcn_s_barrier();
+    acc += s[(threadIdx.x + 1) & 63];
+  }
+  if constexpr (WORK == 1) {
+    for (int i = 0; i < iters; ++i) acc = acc * 1.0001f + 0.5f;
+  } else if constexpr (WORK == 2) {
+    const float* in = buf + (size_t)blockIdx.x * 4096;
+    float4 v[4];
+    for (int k = 0; k < 4; ++k) v[k] = reinterpret_cast<const float4*>(in)[threadIdx.x + 64 * k];
+    for (int k = 0; k < 4; ++k) acc += v[k].x + v[k].y + v[k].z + v[k].w;
+    float* out = buf + (size_t)8192 * 4096 + (size_t)blockIdx.x * 4608;
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    for (int k = 0; k < 18; ++k)
+      __builtin_nontemporal_store(f4{acc, acc, acc, acc}, reinterpret_cast<f4*>(out) + threadIdx.x + 64 * k);
+  } else if constexpr (WORK == 3) {
+    for (int i = 0; i < iters; ++i) __builtin_amdgcn_s_sleep(127);
+  }
+  const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+  if (threadIdx.x == 0) {
+    t[2 * blockIdx.x] = t0;
+    t[2 * blockIdx.x + 1] = t1;
+  }
+  if (acc == -1.0f) buf[0] = acc;  // keeps the work
+}
+
+template <int LDS, int WORK>
+int run(const char* name, int grid, int iters, uint64_t* dt, float* buf) {
+  for (int rep = 0; rep < 3; ++rep) {
+    hipLaunchKernelGGL((k_ramp<LDS, WORK>), dim3(grid), dim3(64), 0, 0, dt, buf, iters);
+    CK(hipDeviceSynchronize());
+  }
+  std::vector<uint64_t> h(2 * (size_t)grid);
+  CK(hipMemcpy(h.data(), dt, h.size() * 8, hipMemcpyDeviceToHost));
+  uint64_t s0 = ~0ull, s1 = 0, e1 = 0;
+  std::vector<double> life;
+  for (int i = 0; i < grid; ++i) {
+    s0 = std::min(s0, h[2 * i]);
+    s1 = std::max(s1, h[2 * i]);
+    e1 = std::max(e1, h[2 * i + 1]);
+    life.push_back((h[2 * i + 1] - h[2 * i]) / 100.0);
+  }
+  std::sort(life.begin(), life.end());
+  std::printf("%-22s grid %5d  start ramp %6.2f us  first start -> last end %6.2f us  wave life p50 %6.2f us\n", name, grid,
+              (s1 - s0) / 100.0, (e1 - s0) / 100.0, life[life.size() / 2]);
+  return 0;
+}
+
+int main() {
+  uint64_t* dt = nullptr;
+  float* buf = nullptr;
+  CK(hipMalloc(&dt, 2 * 65536 * 8));
+  CK(hipMalloc(&buf, (size_t)8192 * (4096 + 4608) * 4));
+  CK(hipMemset(buf, 0, (size_t)8192 * (4096 + 4608) * 4));
+  for (int grid : {4096, 8192}) {
+    if (run<0, 0>("empty", grid, 0, dt, buf)) return 1;
+    if (run<4968, 0>("lds4968", grid, 0, dt, buf)) return 1;
+    if (run<0, 1>("valu", grid, 20000, dt, buf)) return 1;
+    if (run<4968, 1>("lds4968+valu", grid, 20000, dt, buf)) return 1;
+    if (run<0, 2>("memory", grid, 0, dt, buf)) return 1;
+    if (run<4968, 2>("lds4968+memory", grid, 0, dt, buf)) return 1;
+    if (run<0, 3>("sleep", grid, 200, dt, buf)) return 1;
+  }
+  return 0;
+}

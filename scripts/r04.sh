@@ -199,6 +199,7 @@ s11)  # scalar-bitmap road generator in the refill kernel (prod) vs lane words (
     NO_PHASES=1 PROF_DIR=$O/prof_$1_$2 WL=$1 B=$2 run prof_$1_$2 900 bash scripts/profile_session.sh || exit 1
   done
   run bench_driver 300 python bench.py --gpus 1 --steps 20 --warmup 5 || exit 1; grep '^{' $O/bench_driver.log; line bench_driver
+  run launch_ramp 120 ./scripts/bin/launch_ramp || exit 1; cat $O/launch_ramp.log
   ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
