@@ -231,6 +231,52 @@ struct WaveMt {
     prefetch_finish(lane);
   }
 
+  // Early pre-draw (the small kernels, TD_EARLY_MT): the loads of the window [p0, p0 + 16)
+  // at the position p0 the step starts from are issued right after the hot record is in,
+  // before any of the step's stores -- their wait at the step's end then neither waits on
+  // the memory latency nor, through the in-order vmcnt, on the step's own stores.  The step
+  // draws d <= 8 words in practice; the next pre-drawn outputs are the window's lanes
+  // d .. d + 7.  A lazily twisted word the step's slow path twisted meanwhile is twisted
+  // again from the same old words (same value); a window the step outran (d > 8, or a
+  // block wrap) falls back to the late pre-draw.
+  static constexpr uint32_t kEarlyWin = 16;
+  uint32_t ep0 = 0;
+  bool early = false;
+  __device__ __forceinline__ void early_issue(int lane) {
+    early = pos + kEarlyWin <= (uint32_t)MT_N;  // (pos <= tw always: the window's lazy words need old / twisted words only)
+    if (!early) return;
+    ep0 = pos;
+    const uint32_t q = pos + (uint32_t)lane;
+    pmine = (uint32_t)lane < kEarlyWin;
+    plazy = pmine && q >= tw;
+    if (pmine) {
+      pa = w[q];
+      if (plazy) {
+        pnb = w[q == MT_N - 1 ? 0u : q + 1u];
+        pfar = w[q < (uint32_t)(MT_N - MT_M) ? q + MT_M : q - (MT_N - MT_M)];
+      }
+    }
+  }
+  __device__ __forceinline__ void early_finish(int lane) {
+    const uint32_t d = pos - ep0;
+    if (!early || d > kEarlyWin - 8u) {  // outran (or no window): pre-draw from here, late
+      prefetch(lane);
+      return;
+    }
+    const uint32_t q = ep0 + (uint32_t)lane;
+    uint32_t y = pa;
+    if (plazy) {
+      const uint32_t yy = (pa & 0x80000000u) | (pnb & 0x7fffffffu);
+      y = pfar ^ (yy >> 1) ^ ((yy & 1u) ? 0x9908b0dfu : 0u);
+      w[q] = y;
+    }
+    if (ep0 + kEarlyWin > tw) tw = ep0 + kEarlyWin;
+    const uint32_t t = pmine ? mt_temper(y) : 0u;
+    cache = (uint32_t)__shfl((int)t, (int)((uint32_t)lane + d) & 63);
+    cbase = pos;
+    cn = 8u;  // pos + 8 <= ep0 + 16 <= MT_N
+  }
+
   __device__ __forceinline__ uint32_t next() {
     const uint32_t d = pos - cbase;
     if (d < cn) {
@@ -1736,6 +1782,11 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
 #define TD_BLOCK_TWIST 0
 #endif
   R.block_tw = !SMALL && TD_BLOCK_TWIST;
+#ifndef TD_EARLY_MT
+#define TD_EARLY_MT 1
+#endif
+  constexpr bool EARLY_MT = SMALL && !SCAN && MODE != MODE_2P && TD_EARLY_MT;
+  if constexpr (EARLY_MT) R.early_issue(x.lane);
   STAMP(1);
   if (u.num_roads < 1 || u.num_roads > 3) {
     // never reset (its road generation failed): nothing to step
@@ -1818,7 +1869,7 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
   // (the step's draws are done: refill the pre-drawn outputs if the next step may run short)
   const bool refill = MODE != MODE_2P && (!LAZY_HOT || R.cached_left() < (uint32_t)HOT_REFILL);
   // (the multi-action kernels have no registers to carry the loads across the step: at once)
-  if (refill) {
+  if (refill && !EARLY_MT) {
     if constexpr (SCAN) R.prefetch(x.lane);
     else R.prefetch_issue(x.lane);
   }
@@ -1838,7 +1889,8 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
   // acknowledgement (s_waitcnt vmcnt(0)).  (Holding every state store back to the end
   // of the step, next to the observation, measured slower: 219 vs 216 us at 65,536
   // boards, 35.8 vs 34.9 at 8,192, profiles/r03/s16.)
-  if (!SCAN && refill) R.prefetch_finish(x.lane);
+  if constexpr (EARLY_MT) R.early_finish(x.lane);
+  else if (!SCAN && refill) R.prefetch_finish(x.lane);
   if (MODE == MODE_ATK) reward = -reward;                   // TDAttack.py:50
   const bool done = (u.base_LP <= 0) || (u.steps >= C.max_episode_steps);  // :384-385
   u.ep_ret = dadd(u.ep_ret, reward);

@@ -201,5 +201,24 @@ s11)  # scalar-bitmap road generator in the refill kernel (prod) vs lane words (
   run bench_driver 300 python bench.py --gpus 1 --steps 20 --warmup 5 || exit 1; grep '^{' $O/bench_driver.log; line bench_driver
   run launch_ramp 120 ./scripts/bin/launch_ramp || exit 1; cat $O/launch_ramp.log
   ;;
+s12)  # final build: GPU suite, scalar search in the refill kernel (draw cycles; small shares vs noproof), profiles, driver command
+  gpusuite 900; rc=$?; [ $rc -le 1 ] || exit $rc
+  run smoke 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" || exit 1
+  V=$PWD/gym-td_amd/lib/variants
+  TDSTEP_LIB=$V/libtdstep_gs_hyb.so run parts_hyb 300 python scripts/probe_draw_parts.py 1024 10 || exit 1; grep -v amdgpu $O/parts_hyb.log
+  for r in 1 2; do for v in prod noproof; do for bb in 8192 4096; do
+    lib=$V/libtdstep_$v.so; [ $v = prod ] && lib=$PWD/gym-td_amd/lib/libtdstep.so
+    TDSTEP_LIB=$lib run ${v}_${bb}_$r 200 python bench.py --global-batch $bb --no-cpu-baseline --steps 2000 --timing none || exit 1; line ${v}_${bb}_$r
+  done; done; done
+  for wb in "def-small 65536" "def-small 8192" "def-small 4096" "2p-middle-multi 16384" "def-large 16384"; do set -- $wb
+    NO_PHASES=1 PROF_DIR=$O/prof_$1_$2 WL=$1 B=$2 run prof_$1_$2 900 bash scripts/profile_session.sh || exit 1
+  done
+  for bb in 65536 32768 16384 8192 4096; do
+    run line_$bb 200 python bench.py --global-batch $bb --no-cpu-baseline --steps $((bb > 20000 ? 300 : 2000)) || exit 1; line line_$bb
+  done
+  run line_p2 300 python bench.py --workload 2p-middle-multi --no-cpu-baseline --steps 200 || exit 1; line line_p2
+  run line_l30 300 python bench.py --workload def-large --global-batch 16384 --no-cpu-baseline --steps 200 || exit 1; line line_l30
+  run bench_driver 300 python bench.py --gpus 1 --steps 20 --warmup 5 || exit 1; grep '^{' $O/bench_driver.log; line bench_driver
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
