@@ -240,11 +240,10 @@ struct WaveMt {
   // again from the same old words (same value); a window the step outran (d > 8, or a
   // block wrap) falls back to the late pre-draw.
   static constexpr uint32_t kEarlyWin = 16;
-  uint32_t ep0 = 0;
-  bool early = false;
+  uint32_t ep0 = ~0u;  // the window's first position (~0u: none)
   __device__ __forceinline__ void early_issue(int lane) {
-    early = pos + kEarlyWin <= (uint32_t)MT_N;  // (pos <= tw always: the window's lazy words need old / twisted words only)
-    if (!early) return;
+    // (pos <= tw always: the window's lazy words need old or already twisted words only)
+    if (pos + kEarlyWin > (uint32_t)MT_N) return;
     ep0 = pos;
     const uint32_t q = pos + (uint32_t)lane;
     pmine = (uint32_t)lane < kEarlyWin;
@@ -257,24 +256,30 @@ struct WaveMt {
       }
     }
   }
+  __device__ __forceinline__ bool early_ok() const { return ep0 != ~0u && pos - ep0 <= kEarlyWin - 8u; }
+  // The early window's outputs, or (outran: d > 8, a block wrap, no window) a late
+  // pre-draw -- one tail for both, so that no field is stored on one branch only (LLVM
+  // merges such stores through a pointer phi, and the object no longer fits registers).
   __device__ __forceinline__ void early_finish(int lane) {
-    const uint32_t d = pos - ep0;
-    if (!early || d > kEarlyWin - 8u) {  // outran (or no window): pre-draw from here, late
-      prefetch(lane);
-      return;
+    uint32_t base, n, d;
+    if (early_ok()) {
+      base = ep0; n = kEarlyWin; d = pos - ep0;
+    } else {
+      prefetch_issue(lane);  // (wraps if due; cbase = pos)
+      base = cbase; n = cn; d = 0u;
     }
-    const uint32_t q = ep0 + (uint32_t)lane;
+    const uint32_t q = base + (uint32_t)lane;
     uint32_t y = pa;
     if (plazy) {
       const uint32_t yy = (pa & 0x80000000u) | (pnb & 0x7fffffffu);
       y = pfar ^ (yy >> 1) ^ ((yy & 1u) ? 0x9908b0dfu : 0u);
-      w[q] = y;
+      w[q] = y;  // (a word the step's slow path twisted meanwhile: the same value again)
     }
-    if (ep0 + kEarlyWin > tw) tw = ep0 + kEarlyWin;
+    if (base + n > tw) tw = base + n;
     const uint32_t t = pmine ? mt_temper(y) : 0u;
-    cache = (uint32_t)__shfl((int)t, (int)((uint32_t)lane + d) & 63);
+    cache = (uint32_t)__shfl((int)t, (int)(((uint32_t)lane + d) & 63u));
     cbase = pos;
-    cn = 8u;  // pos + 8 <= ep0 + 16 <= MT_N
+    cn = n - d < (uint32_t)HOT_CACHE ? n - d : (uint32_t)HOT_CACHE;
   }
 
   __device__ __forceinline__ uint32_t next() {
@@ -1858,6 +1863,12 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
       with_opp_rng(a, b, x.lane, R, [&](auto& G) { opponent_tower(S, u, x, G, a.difficulty); });
   }
   STAMP(12);
+#ifndef TD_EARLY_AT
+#define TD_EARLY_AT 1
+#endif
+  // (early pre-draw: the step's draws are done -- the window's words are consumed here,
+  // before the step's first state store, and only the pre-drawn outputs live on)
+  if constexpr (EARLY_MT && TD_EARLY_AT == 1) R.early_finish(x.lane);
   if constexpr (ORD && SCAN) ord_r = ord_claim(a, ord_heavy, x.lane, vb, BPW);
   if constexpr (ORD) ord_place(a, b, ord_heavy, ord_r, x.lane, vb, BPW);
   // the towers and map[6] are final: cell words back to HBM if they changed, then
@@ -1889,8 +1900,9 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
   // acknowledgement (s_waitcnt vmcnt(0)).  (Holding every state store back to the end
   // of the step, next to the observation, measured slower: 219 vs 216 us at 65,536
   // boards, 35.8 vs 34.9 at 8,192, profiles/r03/s16.)
-  if constexpr (EARLY_MT) R.early_finish(x.lane);
-  else if (!SCAN && refill) R.prefetch_finish(x.lane);
+  if constexpr (EARLY_MT) {
+    if constexpr (TD_EARLY_AT == 0) R.early_finish(x.lane);
+  } else if (!SCAN && refill) R.prefetch_finish(x.lane);
   if (MODE == MODE_ATK) reward = -reward;                   // TDAttack.py:50
   const bool done = (u.base_LP <= 0) || (u.steps >= C.max_episode_steps);  // :384-385
   u.ep_ret = dadd(u.ep_ret, reward);

@@ -220,5 +220,19 @@ s12)  # final build: GPU suite, scalar search in the refill kernel (draw cycles;
   run line_l30 300 python bench.py --workload def-large --global-batch 16384 --no-cpu-baseline --steps 200 || exit 1; line line_l30
   run bench_driver 300 python bench.py --gpus 1 --steps 20 --warmup 5 || exit 1; grep '^{' $O/bench_driver.log; line bench_driver
   ;;
+s13)  # early opponent pre-draw (small kernels): GPU suite, A/B vs late (noearly) and consumed-at-end, phase stamps, launch ramp
+  gpusuite 900; rc=$?; [ $rc -le 1 ] || exit $rc
+  V=$PWD/gym-td_amd/lib/variants
+  for r in 1 2; do for v in prod noearly early_end; do
+    lib=$V/libtdstep_$v.so; [ $v = prod ] && lib=$PWD/gym-td_amd/lib/libtdstep.so
+    for bb in 8192 4096 16384; do
+      TDSTEP_LIB=$lib run ${v}_${bb}_$r 200 python bench.py --global-batch $bb --no-cpu-baseline --steps 2000 --timing none || exit 1; line ${v}_${bb}_$r
+    done
+    TDSTEP_LIB=$lib run ${v}_l30_$r 300 python bench.py --workload def-large --global-batch 16384 --no-cpu-baseline --steps 200 --timing none || exit 1; line ${v}_l30_$r
+  done; done
+  TDSTEP_LIB=$PWD/gym-td_amd/lib/libtdstep_stamps.so run phases_8192 300 python scripts/probe_phases.py 8192 10 600 || exit 1
+  grep -E "rt |tail" $O/phases_8192.log
+  run launch_ramp 120 ./scripts/bin/launch_ramp || exit 1; cat $O/launch_ramp.log
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
