@@ -1792,6 +1792,9 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
 #endif
   constexpr bool EARLY_MT = SMALL && !SCAN && MODE != MODE_2P && TD_EARLY_MT;
   if constexpr (EARLY_MT) R.early_issue(x.lane);
+#ifdef TD_START_PRIO
+  __builtin_amdgcn_s_setprio(0);
+#endif
   STAMP(1);
   if (u.num_roads < 1 || u.num_roads > 3) {
     // never reset (its road generation failed): nothing to step
@@ -1863,8 +1866,8 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
       with_opp_rng(a, b, x.lane, R, [&](auto& G) { opponent_tower(S, u, x, G, a.difficulty); });
   }
   STAMP(12);
-#ifndef TD_EARLY_AT
-#define TD_EARLY_AT 1
+#ifndef TD_EARLY_AT  // 0: consumed after board_step (8,192: 32.6-32.7 vs 33.2-33.3 us at 1, r04/s13)
+#define TD_EARLY_AT 0
 #endif
   // (early pre-draw: the step's draws are done -- the window's words are consumed here,
   // before the step's first state store, and only the pre-drawn outputs live on)
@@ -2046,6 +2049,9 @@ __device__ __forceinline__ void step_kernel_body(const StepArgs& a) {
 #ifdef TD_STEP_PRIO  // A/B builds: step waves ahead of concurrent refill waves in issue arbitration
   __builtin_amdgcn_s_setprio(TD_STEP_PRIO);
 #endif
+#ifdef TD_START_PRIO  // A/B builds: a starting wave ahead of the resident ones until its board is in
+  __builtin_amdgcn_s_setprio(TD_START_PRIO);
+#endif
   stage_cfg(S, a.cfg);
   const int L = LT ? LT : a.L;
   const Ctx x{S.cfg, L, L * L, (int)(threadIdx.x & 63), a.cfgs, a.epoch};
@@ -2114,6 +2120,9 @@ __global__ __launch_bounds__(128) TD_SMALL2_ATTR void td_step_kernel_small2(Step
   if ((int)blockIdx.x >= a.B) return;
   const int b = ord_board(a, (int)blockIdx.x, 1);
   const int lane = (int)threadIdx.x & 63;
+#ifdef TD_START_PRIO
+  __builtin_amdgcn_s_setprio(TD_START_PRIO);
+#endif
   if (threadIdx.x < 64) {
     stage_cfg(S, a.cfg);
     const Ctx x{S.cfg, LT, NC, lane, a.cfgs, a.epoch};

@@ -19,9 +19,12 @@
   } while (0)
 
 // WORK: 0 none, 1 VALU loop (~10 us), 2 memory (16 loads + 18 1-KB stores), 3 s_sleep (~10 us)
-template <int LDS, int WORK>
+// PRIO: the wave raises its issue priority (s_setprio 3) until its start is stamped
+template <int LDS, int WORK, int PRIO = 0>
 __global__ __launch_bounds__(64) void k_ramp(uint64_t* t, float* buf, int iters) {
+  if constexpr (PRIO) __builtin_amdgcn_s_setprio(3);
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
   __shared__ float s[LDS > 0 ? LDS / 4 : 1];
   float acc = (float)threadIdx.x;
   if constexpr (LDS > 0) {
@@ -51,10 +54,10 @@ __global__ __launch_bounds__(64) void k_ramp(uint64_t* t, float* buf, int iters)
   if (acc == -1.0f) buf[0] = acc;  // keeps the work
 }
 
-template <int LDS, int WORK>
+template <int LDS, int WORK, int PRIO = 0>
 int run(const char* name, int grid, int iters, uint64_t* dt, float* buf) {
   for (int rep = 0; rep < 3; ++rep) {
-    hipLaunchKernelGGL((k_ramp<LDS, WORK>), dim3(grid), dim3(64), 0, 0, dt, buf, iters);
+    hipLaunchKernelGGL((k_ramp<LDS, WORK, PRIO>), dim3(grid), dim3(64), 0, 0, dt, buf, iters);
     CK(hipDeviceSynchronize());
   }
   std::vector<uint64_t> h(2 * (size_t)grid);
@@ -83,6 +86,9 @@ int main() {
     if (run<0, 0>("empty", grid, 0, dt, buf)) return 1;
     if (run<4968, 0>("lds4968", grid, 0, dt, buf)) return 1;
     if (run<0, 1>("valu", grid, 20000, dt, buf)) return 1;
+    if (run<0, 1, 1>("valu+startprio", grid, 20000, dt, buf)) return 1;
+    if (run<0, 1>("valu-short", grid, 500, dt, buf)) return 1;
+    if (run<0, 1, 1>("valu-short+startprio", grid, 500, dt, buf)) return 1;
     if (run<4968, 1>("lds4968+valu", grid, 20000, dt, buf)) return 1;
     if (run<0, 2>("memory", grid, 0, dt, buf)) return 1;
     if (run<4968, 2>("lds4968+memory", grid, 0, dt, buf)) return 1;

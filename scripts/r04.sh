@@ -234,5 +234,18 @@ s13)  # early opponent pre-draw (small kernels): GPU suite, A/B vs late (noearly
   grep -E "rt |tail" $O/phases_8192.log
   run launch_ramp 120 ./scripts/bin/launch_ramp || exit 1; cat $O/launch_ramp.log
   ;;
+s14)  # early pre-draw consumed after the board step (default now); start priority A/B; phases; launch ramp with start priority
+  gpusuite 900; rc=$?; [ $rc -le 1 ] || exit $rc
+  V=$PWD/gym-td_amd/lib/variants
+  for r in 1 2; do for v in prod sprio3 sprio1; do
+    lib=$V/libtdstep_$v.so; [ $v = prod ] && lib=$PWD/gym-td_amd/lib/libtdstep.so
+    for bb in 8192 4096 16384 65536; do
+      TDSTEP_LIB=$lib run ${v}_${bb}_$r 200 python bench.py --global-batch $bb --no-cpu-baseline --steps $((bb > 20000 ? 300 : 2000)) --timing none || exit 1; line ${v}_${bb}_$r
+    done
+  done; done
+  TDSTEP_LIB=$PWD/gym-td_amd/lib/libtdstep_stamps.so run phases_8192 300 python scripts/probe_phases.py 8192 10 600 || exit 1
+  grep -E "rt |tail" $O/phases_8192.log
+  run launch_ramp 120 ./scripts/bin/launch_ramp || exit 1; cat $O/launch_ramp.log
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
