@@ -45,6 +45,22 @@ __global__ __launch_bounds__(64) void k_ramp(uint64_t* t, float* buf, int iters)
       __builtin_nontemporal_store(f4{acc, acc, acc, acc}, reinterpret_cast<f4*>(out) + threadIdx.x + 64 * k);
   } else if constexpr (WORK == 3) {
     for (int i = 0; i < iters; ++i) __builtin_amdgcn_s_sleep(127);
+  } else if constexpr (WORK == 4) {  // SALU chain
+    uint32_t v = __builtin_amdgcn_readfirstlane((uint32_t)iters);
+    for (int i = 0; i < iters; ++i) asm volatile("s_mul_i32 %0, %0, 3\n s_add_u32 %0, %0, 1" : "+s"(v));
+    acc += (float)v;
+  } else if constexpr (WORK == 5) {  // dependent LDS round trips
+    __shared__ float q[64];
+    q[threadIdx.x] = acc;
+    for (int i = 0; i < iters; ++i) {
+      acc = q[(threadIdx.x + (int)acc) & 63] + 1.0f;
+      q[threadIdx.x] = acc;
+    }
+  } else if constexpr (WORK == 6) {  // VALU with a short sleep every 32 iterations
+    for (int i = 0; i < iters; ++i) {
+      acc = acc * 1.0001f + 0.5f;
+      if ((i & 31) == 31) __builtin_amdgcn_s_sleep(1);
+    }
   }
   const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
   if (threadIdx.x == 0) {
@@ -82,6 +98,12 @@ int main() {
   CK(hipMalloc(&dt, 2 * 65536 * 8));
   CK(hipMalloc(&buf, (size_t)8192 * (4096 + 4608) * 4));
   CK(hipMemset(buf, 0, (size_t)8192 * (4096 + 4608) * 4));
+  for (int grid : {8192}) {
+    if (run<0, 1>("valu-short", grid, 500, dt, buf)) return 1;
+    if (run<0, 6>("valu-short+sleep/32", grid, 500, dt, buf)) return 1;
+    if (run<0, 4>("salu", grid, 2000, dt, buf)) return 1;
+    if (run<0, 5>("lds-chain", grid, 200, dt, buf)) return 1;
+  }
   for (int grid : {4096, 8192}) {
     if (run<0, 0>("empty", grid, 0, dt, buf)) return 1;
     if (run<4968, 0>("lds4968", grid, 0, dt, buf)) return 1;

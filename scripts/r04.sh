@@ -247,5 +247,11 @@ s14)  # early pre-draw consumed after the board step (default now); start priori
   grep -E "rt |tail" $O/phases_8192.log
   run launch_ramp 120 ./scripts/bin/launch_ramp || exit 1; cat $O/launch_ramp.log
   ;;
+s15)  # launch ramp by work kind (SALU / LDS chain / VALU with sleeps); PMC bytes of the early-pre-draw build at 8,192 / 4,096
+  run launch_ramp 120 ./scripts/bin/launch_ramp || exit 1; cat $O/launch_ramp.log
+  for bb in 8192 4096; do
+    OUT=$O/pmc NAME=prod_$bb B=$bb run pmc_$bb 600 bash scripts/pmc_ab.sh || exit 1; tail -1 $O/pmc_$bb.log
+  done
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
