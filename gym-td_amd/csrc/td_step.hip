@@ -2241,6 +2241,9 @@ __device__ int wave_layout(LayoutSmem<NC>& G, const StepArgs& a, int b, int retr
 #ifdef TD_GEN_STAMPS
   const uint64_t wl_t0 = __builtin_amdgcn_s_memtime();
 #endif
+  // (the walk budget and the retry count bound the draw's loop: wave-uniform, SGPRs)
+  budget = (int)__builtin_amdgcn_readfirstlane((uint32_t)budget);
+  retries = (int)__builtin_amdgcn_readfirstlane((uint32_t)retries);
   uint32_t* gmt = a.np_mt + (size_t)b * OPP_WORDS;
   RoadResume* ghdr = resume_hdr(a, b);
   uint8_t* gscr = a.scratch + (size_t)b * a.scratch_stride + sizeof(RoadResume);
@@ -2530,8 +2533,8 @@ __global__ __launch_bounds__(64) void td_refill_kernel(StepArgs a, int guard) {
         }
         if (!got) continue;
       }
-      uint32_t t = ld_relaxed(a.lay_tail + bb);
-      const uint32_t h = ld_relaxed(a.lay_head + bb);
+      uint32_t t = __builtin_amdgcn_readfirstlane(ld_relaxed(a.lay_tail + bb));  // (wave-uniform: SGPRs)
+      const uint32_t h = __builtin_amdgcn_readfirstlane(ld_relaxed(a.lay_head + bb));
 #pragma nounroll
       while (t - h < level) {
         uint32_t* slot = a.nxt + ((size_t)bb * NSLOT + t % NSLOT) * a.slot_words;

@@ -382,7 +382,11 @@ struct WaveRoadGen {
       }
       cw[p] = w;
     }
-    if ((uint32_t)(tot - 1) > *maxdist) *maxdist = (uint32_t)(tot - 1);
+    // (readfirstlane: written as a plain if, the update was merged into the join of the
+    // lane < tot branch above and read as divergent; every value the draw's loop carries
+    // then followed -- the stream position and the draw's state in VGPRs behind exec-masked
+    // branches, 6.7 k cycles per walk in r04/s12)
+    *maxdist = __builtin_amdgcn_readfirstlane((uint32_t)(tot - 1) > *maxdist ? (uint32_t)(tot - 1) : *maxdist);
     sync();
   }
 

@@ -253,5 +253,15 @@ s15)  # launch ramp by work kind (SALU / LDS chain / VALU with sleeps); PMC byte
     OUT=$O/pmc NAME=prod_$bb B=$bb run pmc_$bb 600 bash scripts/pmc_ab.sh || exit 1; tail -1 $O/pmc_$bb.log
   done
   ;;
+s16)  # generator draw state uniform (SGPRs): GPU suite, draw cycles by part, the step rate beside the refills
+  gpusuite 900; rc=$?; [ $rc -le 1 ] || exit $rc
+  V=$PWD/gym-td_amd/lib/variants
+  TDSTEP_LIB=$V/libtdstep_gs.so run parts_gs 300 python scripts/probe_draw_parts.py 1024 10 || exit 1; grep -v amdgpu $O/parts_gs.log
+  for r in 1 2; do for bb in 8192 4096 16384 65536; do
+    run prod_${bb}_$r 200 python bench.py --global-batch $bb --no-cpu-baseline --steps $((bb > 20000 ? 300 : 2000)) --timing none || exit 1; line prod_${bb}_$r
+  done; done
+  run line_p2 300 python bench.py --workload 2p-middle-multi --no-cpu-baseline --steps 200 || exit 1; line line_p2
+  run line_l30 300 python bench.py --workload def-large --global-batch 16384 --no-cpu-baseline --steps 200 || exit 1; line line_l30
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
