@@ -486,14 +486,16 @@ __device__ __forceinline__ int defender_op(Smem<NC>& S, U& u, const Ctx& x, int 
 // Skipped cells would only have produced failures, which leave no trace in
 // multi-action mode.  The real actions (grp[1]) go out as int64 (6, L, L) in
 // 128-B-aligned windows, like the observation.
+// (In the two-wave kernel the second wave folds the flags while the first loads the
+// board, and writes the real actions out after the step's actions: scan_fold /
+// scan_write_real below, handed over at barriers.)
+// The flags folded into grp[0] (grp[1] cleared); true when a flag is not 0 / 1 / 2.
 template <int NC>
-__device__ __forceinline__ void defender_scan(Smem<NC>& S, U& u, const Ctx& x, const int64_t* A, int64_t* R, bool active) {
-  const TdDevCfg& C = x.C;
-  const int ncr = x.NCr, n = 6 * ncr;
+__device__ __forceinline__ bool scan_fold(Smem<NC>& S, int lane, int ncr, const int64_t* A) {
+  const int n = 6 * ncr;
   uint8_t* flag = &S.grp[0][0];
-  uint8_t* real = &S.grp[1][0];
   uint32_t* fw = reinterpret_cast<uint32_t*>(flag);
-  for (int i = x.lane; i < (2 * NC) / 4; i += 64) fw[i] = 0u;  // grp[0] and grp[1]
+  for (int i = lane; i < (2 * NC) / 4; i += 64) fw[i] = 0u;  // grp[0] and grp[1]
   wsync();
   bool bad = false;
   if ((ncr & 1) == 0 && (reinterpret_cast<uintptr_t>(A) & 15u) == 0) {  // 16-B units of two cells of one plane
@@ -508,12 +510,12 @@ __device__ __forceinline__ void defender_scan(Smem<NC>& S, U& u, const Ctx& x, c
       i64x2 v[K];
 #pragma unroll
       for (int k = 0; k < K; ++k) {
-        const int e = base + 64 * k + x.lane;
+        const int e = base + 64 * k + lane;
         v[k] = e < n2 ? __builtin_nontemporal_load(A2 + e) : i64x2{0, 0};
       }
 #pragma unroll
       for (int k = 0; k < K; ++k) {
-        const int e = base + 64 * k + x.lane;
+        const int e = base + 64 * k + lane;
         if (e < n2) {
           const int pl = (2 * e) / ncr, c = 2 * e - pl * ncr;
           bad |= (unsigned long long)v[k].x > 2ull || (unsigned long long)v[k].y > 2ull;
@@ -524,15 +526,58 @@ __device__ __forceinline__ void defender_scan(Smem<NC>& S, U& u, const Ctx& x, c
       }
     }
   } else {
-    for (int e = x.lane; e < n; e += 64) {
+    for (int e = lane; e < n; e += 64) {
       const int64_t v = A[e];
       const int pl = e / ncr, c = e - pl * ncr;
       bad |= v < 0 || v > 2;
       if (v == 1) atomicOr(&fw[c >> 2], (1u << pl) << (8 * (c & 3)));
     }
   }
-  if (ballot(bad)) u.flags |= FLAG_BAD_ACTION;
+  const bool any_bad = ballot(bad) != 0ull;
   wsync();
+  return any_bad;
+}
+
+// The real actions (grp[1]) out as int64 (6, L, L) in 128-B-aligned windows.
+template <int NC>
+__device__ __forceinline__ void scan_write_real(const Smem<NC>& S, int lane, int ncr, int64_t* R) {
+  const int n = 6 * ncr;
+  const uint8_t* real = &S.grp[1][0];
+  if ((ncr & 1) == 0 && (reinterpret_cast<uintptr_t>(R) & 15u) == 0) {
+    typedef long long i64x2 __attribute__((ext_vector_type(2)));
+    i64x2* R2 = reinterpret_cast<i64x2*>(R);
+    const int n2 = n / 2, mis = (int)((reinterpret_cast<uintptr_t>(R2) >> 4) & 7u);
+    for (int e = lane - mis; e < n2; e += 64) {
+      if (e < 0) continue;
+      const int pl = (2 * e) / ncr, c = 2 * e - pl * ncr;
+      const uint32_t r2 = *reinterpret_cast<const uint16_t*>(real + c);
+      __builtin_nontemporal_store(i64x2{(long long)((r2 >> pl) & 1u), (long long)((r2 >> (8 + pl)) & 1u)}, R2 + e);
+    }
+  } else {
+    for (int e = lane; e < n; e += 64) {
+      const int pl = e / ncr;
+      R[e] = (real[e - pl * ncr] >> pl) & 1u;
+    }
+  }
+}
+
+// Two-wave kernel, multi-action scan: the second wave folds the flags and writes the
+// real actions (TD_SCAN_SPLIT=0: the stepping wave does both, A/B builds).
+#ifndef TD_SCAN_SPLIT
+#define TD_SCAN_SPLIT 1
+#endif
+constexpr bool kScanSplit = TD_SCAN_SPLIT != 0;
+// FOLD: the flags are folded here (else by the second wave, `bad` its verdict); WRITE:
+// the real actions are written here (else by the second wave after barrier (A)).
+template <int NC, bool FOLD = true, bool WRITE = true>
+__device__ __forceinline__ void defender_scan(Smem<NC>& S, U& u, const Ctx& x, const int64_t* A, int64_t* R, bool active,
+                                              bool bad = false) {
+  const TdDevCfg& C = x.C;
+  const int ncr = x.NCr;
+  uint8_t* flag = &S.grp[0][0];
+  uint8_t* real = &S.grp[1][0];
+  if constexpr (FOLD) bad = scan_fold(S, x.lane, ncr, A);
+  if (bad) u.flags |= FLAG_BAD_ACTION;
   for (int base = 0; base < ncr && active; base += 64) {
     const int cell = base + x.lane;
     const bool valid = cell < ncr;
@@ -573,24 +618,7 @@ __device__ __forceinline__ void defender_scan(Smem<NC>& S, U& u, const Ctx& x, c
     }
   }
   wsync();
-  if (R) {
-    if ((ncr & 1) == 0 && (reinterpret_cast<uintptr_t>(R) & 15u) == 0) {
-      typedef long long i64x2 __attribute__((ext_vector_type(2)));
-      i64x2* R2 = reinterpret_cast<i64x2*>(R);
-      const int n2 = n / 2, mis = (int)((reinterpret_cast<uintptr_t>(R2) >> 4) & 7u);
-      for (int e = x.lane - mis; e < n2; e += 64) {
-        if (e < 0) continue;
-        const int pl = (2 * e) / ncr, c = 2 * e - pl * ncr;
-        const uint32_t r2 = *reinterpret_cast<const uint16_t*>(real + c);
-        __builtin_nontemporal_store(i64x2{(long long)((r2 >> pl) & 1u), (long long)((r2 >> (8 + pl)) & 1u)}, R2 + e);
-      }
-    } else {
-      for (int e = x.lane; e < n; e += 64) {
-        const int pl = e / ncr;
-        R[e] = (real[e - pl * ncr] >> pl) & 1u;
-      }
-    }
-  }
+  if (WRITE && R) scan_write_real(S, x.lane, ncr, R);
 }
 
 // ---------------------------------------------------------------------------
@@ -1486,6 +1514,7 @@ struct StepOut {
   int64_t real_def;
   int32_t ep_steps, fail_def;
   uint32_t done, win, allow, cool;
+  uint32_t scan_bad;  // second wave, multi-action scan: a flag was not 0 / 1 / 2 (scan_fold)
   uint32_t go;   // second wave: 0 nothing (a board never reset wrote its own outputs), 1 store and write
                  // half of the late windows, 2 store only (an auto-reset board: the stepping wave writes every window)
   uint32_t any;  // the board has enemies (enemy windows read the group statistics)
@@ -1792,6 +1821,7 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
 #endif
   constexpr bool EARLY_MT = SMALL && !SCAN && MODE != MODE_2P && TD_EARLY_MT;
   if constexpr (EARLY_MT) R.early_issue(x.lane);
+  constexpr bool SCAN2 = SPLIT && SCAN && kScanSplit;
 #ifdef TD_START_PRIO
   __builtin_amdgcn_s_setprio(0);
 #endif
@@ -1821,6 +1851,7 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
     if (a.real_atk && x.lane < 24) a.real_atk[(size_t)b * 24 + x.lane] = 4;
     if constexpr (SPLIT) {
       if (x.lane == 0) { S.early_go = 0u; so->go = 0u; }
+      if constexpr (SCAN2) __syncthreads();  // (A0)
       __syncthreads();  // (A)
       __syncthreads();  // (B)
       __syncthreads();  // (C)
@@ -1838,7 +1869,10 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
 
   // ---- defender
   if (MODE != MODE_ATK) {
-    if (SCAN) {
+    if constexpr (SCAN2) {
+      __syncthreads();  // (A0) the second wave has folded the flags
+      defender_scan<NC, false, false>(S, u, x, nullptr, nullptr, u.def_cd == 0, so->scan_bad != 0u);
+    } else if (SCAN) {
       defender_scan(S, u, x, a.def_act + (size_t)b * 6 * x.NCr,
                     a.real_def ? a.real_def + (size_t)b * 6 * x.NCr : nullptr, u.def_cd == 0);
     } else {
@@ -2090,8 +2124,11 @@ template <int LT>
 constexpr int small_waves() { return LT == 10 ? 8 : LT == 20 ? 5 : 3; }
 template <int LT>
 constexpr int small2_waves() { return LT == 30 ? 6 : 8; }
+#ifndef TD_SCAN2_CAP  // A/B builds: residency of the 20x20 two-wave multi-action kernel
+#define TD_SCAN2_CAP 5
+#endif
 template <int LT, int MODE, bool SCAN>
-constexpr int small2_cap() { return LT == 20 && SCAN ? 5 : LT == 20 && MODE == MODE_ATK ? 6 : 8; }
+constexpr int small2_cap() { return LT == 20 && SCAN ? TD_SCAN2_CAP : LT == 20 && MODE == MODE_ATK ? 6 : 8; }
 #ifdef TD_DRY_DRAW
 #define TD_SMALL_ATTR __attribute__((amdgpu_waves_per_eu(small_waves<LT>(), small_waves<LT>())))
 #define TD_SMALL2_ATTR __attribute__((amdgpu_waves_per_eu(small2_waves<LT>(), small2_waves<LT>())))
@@ -2131,7 +2168,16 @@ __global__ __launch_bounds__(128) TD_SMALL2_ATTR void td_step_kernel_small2(Step
     step_board<NC, LT, MODE, SCAN, true, true>(S, x, a, b, P, (int)blockIdx.x, &SO);
   } else {
     float* const obs = a.obs + (size_t)b * NCH * NC;
+    constexpr bool SCAN2 = SCAN && kScanSplit;
+    if constexpr (SCAN2) {  // the multi-action flags, folded while the first wave loads the board
+      const bool bad = scan_fold(S, lane, NC, a.def_act + (size_t)b * 6 * NC);
+      if (lane == 0) SO.scan_bad = bad ? 1u : 0u;
+      __syncthreads();  // (A0)
+    }
     __syncthreads();  // (A) actions and towers final, cells packed
+    if constexpr (SCAN2) {  // the real actions, beside the step (grp[1] is not touched before (B))
+      if (S.early_go && a.real_def) scan_write_real(S, lane, NC, a.real_def + (size_t)b * 6 * NC);
+    }
     if (S.early_go) {
       write_obs_lines<NC, LT, 0, -1, 4, 1>(S, lane, obs, false, a.obs_wt != 0, a.edge_wt != 0);
       // landed before (B): after an auto-reset the first wave rewrites these windows

@@ -263,5 +263,15 @@ s16)  # generator draw state uniform (SGPRs): GPU suite, draw cycles by part, th
   run line_p2 300 python bench.py --workload 2p-middle-multi --no-cpu-baseline --steps 200 || exit 1; line line_p2
   run line_l30 300 python bench.py --workload def-large --global-batch 16384 --no-cpu-baseline --steps 200 || exit 1; line line_l30
   ;;
+s17)  # 2p multi-action: the second wave folds the flags and writes the real actions (prod) vs the stepping wave (noss), 6 waves/SIMD (cap6)
+  gpusuite 900; rc=$?; [ $rc -le 1 ] || exit $rc
+  V=$PWD/gym-td_amd/lib/variants
+  for r in 1 2; do for v in prod noss cap6; do
+    lib=$V/libtdstep_$v.so; [ $v = prod ] && lib=$PWD/gym-td_amd/lib/libtdstep.so
+    TDSTEP_LIB=$lib run ${v}_p2_$r 300 python bench.py --workload 2p-middle-multi --no-cpu-baseline --steps 200 --timing none || exit 1; line ${v}_p2_$r
+    TDSTEP_LIB=$lib run ${v}_p2_4096_$r 300 python bench.py --workload 2p-middle-multi --global-batch 4096 --no-cpu-baseline --steps 500 --timing none || exit 1; line ${v}_p2_4096_$r
+  done; done
+  run prod_8192 200 python bench.py --global-batch 8192 --no-cpu-baseline --steps 2000 --timing none || exit 1; line prod_8192
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
