@@ -1819,7 +1819,10 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
 #ifndef TD_EARLY_MT
 #define TD_EARLY_MT 1
 #endif
-  constexpr bool EARLY_MT = SMALL && !SCAN && MODE != MODE_2P && TD_EARLY_MT;
+#ifndef TD_EARLY_LARGE  // A/B builds: the early window in the large kernel too (a refill every step)
+#define TD_EARLY_LARGE 0
+#endif
+  constexpr bool EARLY_MT = (SMALL || TD_EARLY_LARGE) && !SCAN && MODE != MODE_2P && TD_EARLY_MT;
   if constexpr (EARLY_MT) R.early_issue(x.lane);
   constexpr bool SCAN2 = SPLIT && SCAN && kScanSplit;
 #ifdef TD_START_PRIO
@@ -1915,7 +1918,7 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
   pack_obs_cells(S, x);
   // pre-draw the next step's words: loads issued now, consumed at the end of the step
   // (the step's draws are done: refill the pre-drawn outputs if the next step may run short)
-  const bool refill = MODE != MODE_2P && (!LAZY_HOT || R.cached_left() < (uint32_t)HOT_REFILL);
+  const bool refill = MODE != MODE_2P && (EARLY_MT || !LAZY_HOT || R.cached_left() < (uint32_t)HOT_REFILL);
   // (the multi-action kernels have no registers to carry the loads across the step: at once)
   if (refill && !EARLY_MT) {
     if constexpr (SCAN) R.prefetch(x.lane);

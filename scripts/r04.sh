@@ -273,5 +273,18 @@ s17)  # 2p multi-action: the second wave folds the flags and writes the real act
   done; done
   run prod_8192 200 python bench.py --global-batch 8192 --no-cpu-baseline --steps 2000 --timing none || exit 1; line prod_8192
   ;;
+s18)  # the early opponent window in the large kernel too (a refill every step) vs lazy refills: step time and bytes
+  V=$PWD/gym-td_amd/lib/variants
+  for r in 1 2; do for v in prod early_large; do
+    lib=$V/libtdstep_$v.so; [ $v = prod ] && lib=$PWD/gym-td_amd/lib/libtdstep.so
+    for bb in 65536 32768; do
+      TDSTEP_LIB=$lib run ${v}_${bb}_$r 200 python bench.py --global-batch $bb --no-cpu-baseline --steps 300 --timing none || exit 1; line ${v}_${bb}_$r
+    done
+  done; done
+  for v in prod early_large; do
+    lib=$V/libtdstep_$v.so; [ $v = prod ] && lib=$PWD/gym-td_amd/lib/libtdstep.so
+    TDSTEP_LIB=$lib OUT=$O/pmc NAME=${v}_65536 B=65536 run pmc_$v 600 bash scripts/pmc_ab.sh || exit 1; tail -1 $O/pmc_$v.log
+  done
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
