@@ -299,5 +299,16 @@ s19)  # final build: GPU suite, smoke, profiles of five workloads (kernel trace,
   run line_l30 300 python bench.py --workload def-large --global-batch 16384 --no-cpu-baseline --steps 200 || exit 1; line line_l30
   run bench_driver 300 python bench.py --gpus 1 --steps 20 --warmup 5 || exit 1; grep '^{' $O/bench_driver.log; line bench_driver
   ;;
+s20)  # shared observation lines: write-through (TD_EDGE_WT=1, product) vs plain write-back stores merged in the XCD's L2 (2)
+  for r in 1 2; do for e in 1 2; do
+    for bb in 65536 32768 16384; do
+      TD_EDGE_WT=$e run e${e}_${bb}_$r 200 python bench.py --global-batch $bb --no-cpu-baseline --steps $((bb > 20000 ? 300 : 1000)) --timing none || exit 1; line e${e}_${bb}_$r
+    done
+    TD_EDGE_WT=$e run e${e}_p2_$r 300 python bench.py --workload 2p-middle-multi --no-cpu-baseline --steps 200 --timing none || exit 1; line e${e}_p2_$r
+    TD_EDGE_WT=$e run e${e}_l30_$r 300 python bench.py --workload def-large --global-batch 16384 --no-cpu-baseline --steps 200 --timing none || exit 1; line e${e}_l30_$r
+  done; done
+  TD_EDGE_WT=2 OUT=$O/pmc NAME=e2_65536 B=65536 run pmc_e2 600 bash scripts/pmc_ab.sh || exit 1; tail -1 $O/pmc_e2.log
+  TD_EDGE_WT=2 run pytest_edge2 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -q -x --timeout 400 --timeout-method thread -p no:cacheprovider || exit 1; tail -1 $O/pytest_edge2.log
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
