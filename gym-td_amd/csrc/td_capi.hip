@@ -126,8 +126,9 @@ struct td_handle {
   int ord_stride = 0;
   int ord_on = 0;  // TD_ORDER=1: longest-work-first order (A/B runs; slower, profiles/r04/s2)
   int xcd_map = 1;  // XCD-contiguous board map (td_step.hip xcd_board; TD_XCD_MAP=0: block i = board i)
-  int edge_wt = 1;  // observation lines shared with a neighbour written write-through (TD_EDGE_WT=0: non-temporal,
-                    // A/B runs: 233 vs 212 us at 65,536 boards even with both halves on one XCD, profiles/r04/s4)
+  int edge_wt = 2;  // observation lines shared with a neighbour: plain write-back stores, merged in the XCD's L2
+                    // (1.088x vs 1.093x the algorithmic bytes at 65,536 boards, step time +-0, profiles/r04/s20);
+                    // TD_EDGE_WT=1: write-through (sc1); 0: non-temporal (233 vs 212 us, profiles/r04/s4)
   long long ord_steps = 0;
 };
 
@@ -442,7 +443,7 @@ td_handle* td_create(const td_config* cfg, int map_size, int n_boards, int mode,
   rc |= dalloc(&h->d_epstats, 2);
   rc |= dalloc(&h->d_lastep, B);
   if (const char* e = std::getenv("TD_XCD_MAP")) h->xcd_map = std::atoi(e) ? 1 : 0;  // A/B runs
-  if (const char* e = std::getenv("TD_EDGE_WT")) h->edge_wt = std::atoi(e) ? 1 : 0;
+  if (const char* e = std::getenv("TD_EDGE_WT")) h->edge_wt = std::atoi(e) == 2 ? 2 : std::atoi(e) ? 1 : 0;
   h->ord_stride = ord_stride(n_boards);
   rc |= dalloc(&h->d_ord, (size_t)2 * ORD_XCD * h->ord_stride);
   rc |= dalloc(&h->d_ord_cnt, (size_t)2 * ORD_CNT_WORDS);

@@ -82,7 +82,7 @@ struct StepArgs {
   // chunk counters per XCD, one 128-B line each: [0] heavy, [1] light).  ord_clr: the other
   // parity's counters, zeroed by block 0 for the step after this one.
   int xcd_map;   // large kernel: block i steps board xcd_board(i, B) (else board i)
-  int edge_wt;   // observation lines shared with a neighbouring board stored write-through (write_obs_lines)
+  int edge_wt;   // observation lines shared with a neighbouring board: 2 plain, 1 write-through, 0 non-temporal (write_obs_lines)
   const uint32_t* ord_in;
   uint32_t* ord_out;
   uint32_t* ord_cnt;

@@ -1215,13 +1215,15 @@ struct ObsWinTab {
 // PASS: 0 every window; 1 only the windows of binary planes alone (ObsWinTab class 0:
 // roads, end, starts, buildable, tower level / type -- final once the step's actions
 // are, td_step_kernel_small2 writes them early); 2 every other window.
-// edge_wt: the two lines the board shares with its neighbours go write-through (sc1): the
-// neighbours' waves run on other XCDs (board i on XCD i % 8); with the XCD-contiguous board
-// map (StepArgs::xcd_map) they share this XCD's L2, which merges the two halves, and the
-// lines go out like the whole ones.
+// edge_wt: how the two lines the board shares with its neighbours are stored.  2 (default):
+// plain write-back stores -- with the XCD-contiguous board map (StepArgs::xcd_map) the
+// neighbours' waves run on this XCD and its L2 merges the two halves into one line write
+// (a pair split across two XCDs is written back byte-masked by both L2s); 1: write-through
+// (sc1); 0: non-temporal (partial lines straight to HBM: slow).  2 vs 1 at 65,536 boards:
+// 1.088x vs 1.093x the algorithmic bytes, step time +-0 (profiles/r04/s20).
 template <int NC, int LT, int KB = 0, int KE = -1, int G = 4, int PASS = 0>
 __device__ __forceinline__ void write_obs_lines(const Smem<NC>& S, int lane, float* out, bool any_enemy, bool wt,
-                                                bool edge_wt = true) {
+                                                int edge_wt = 1) {
   static_assert(LT >= 8, "a 128-B line spans at most two channel planes");
   constexpr int Q = LT * LT / 4, N4 = NCH * Q;
   constexpr int K = KE >= 0 ? KE : (N4 + 7 + 63) / 64;  // windows [KB, K) of the board's (N4 + 7 + 63) / 64
@@ -1324,7 +1326,10 @@ __device__ __forceinline__ void write_obs_lines(const Smem<NC>& S, int lane, flo
       } else {
         const bool shared = i < head || i >= tail;  // a line shared with a neighbouring board
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, val), rs, shared ? OOB : off, 0, 2 /* nt */);
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, val), rs, shared ? off : OOB, 0, 16 /* sc1 */);
+        if (edge_wt == 2)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, val), rs, shared ? off : OOB, 0, 0 /* plain */);
+        else
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, val), rs, shared ? off : OOB, 0, 16 /* sc1 */);
       }
     }
   }
@@ -2021,8 +2026,8 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
     STAMP(14);
     __syncthreads();
     STAMP(6);
-    if (was_reset) write_obs_lines<NC, LT>(S, x.lane, obs, u.n > 0, wt, a.edge_wt != 0);
-    else write_obs_lines<NC, LT, 0, obs_late_half<LT>(), 4, 2>(S, x.lane, obs, u.n > 0, wt, a.edge_wt != 0);
+    if (was_reset) write_obs_lines<NC, LT>(S, x.lane, obs, u.n > 0, wt, a.edge_wt);
+    else write_obs_lines<NC, LT, 0, obs_late_half<LT>(), 4, 2>(S, x.lane, obs, u.n > 0, wt, a.edge_wt);
   } else {
     enemy_stats(S, u, x);  // no-op for a board without enemies (e.g. just reset)
     STAMP(13);
@@ -2039,7 +2044,7 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
     if constexpr (LT != 0) {
       if ((reinterpret_cast<uintptr_t>(a.obs) & 15u) == 0) {
 #ifndef TD_DIAG_NO_OBS  // diagnostic builds only: the step without its observation
-        write_obs_lines<NC, LT>(S, x.lane, obs, u.n > 0, wt, a.edge_wt != 0);
+        write_obs_lines<NC, LT>(S, x.lane, obs, u.n > 0, wt, a.edge_wt);
 #endif
       } else {
         write_obs<NC, LT>(S, x, obs, u.n > 0);
@@ -2182,7 +2187,7 @@ __global__ __launch_bounds__(128) TD_SMALL2_ATTR void td_step_kernel_small2(Step
       if (S.early_go && a.real_def) scan_write_real(S, lane, NC, a.real_def + (size_t)b * 6 * NC);
     }
     if (S.early_go) {
-      write_obs_lines<NC, LT, 0, -1, 4, 1>(S, lane, obs, false, a.obs_wt != 0, a.edge_wt != 0);
+      write_obs_lines<NC, LT, 0, -1, 4, 1>(S, lane, obs, false, a.obs_wt != 0, a.edge_wt);
       // landed before (B): after an auto-reset the first wave rewrites these windows
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -2197,7 +2202,7 @@ __global__ __launch_bounds__(128) TD_SMALL2_ATTR void td_step_kernel_small2(Step
     __syncthreads();  // (C) statistics and broadcast channels in LDS
     if (go == 1u)
       write_obs_lines<NC, LT, obs_late_half<LT>(), -1, 4, 2>(S, lane, obs, SO.any != 0u, a.obs_wt != 0,
-                                                            a.edge_wt != 0);
+                                                            a.edge_wt);
   }
 }
 

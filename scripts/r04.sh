@@ -310,5 +310,18 @@ s20)  # shared observation lines: write-through (TD_EDGE_WT=1, product) vs plain
   TD_EDGE_WT=2 OUT=$O/pmc NAME=e2_65536 B=65536 run pmc_e2 600 bash scripts/pmc_ab.sh || exit 1; tail -1 $O/pmc_e2.log
   TD_EDGE_WT=2 run pytest_edge2 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -q -x --timeout 400 --timeout-method thread -p no:cacheprovider || exit 1; tail -1 $O/pytest_edge2.log
   ;;
+s21)  # final build (plain shared observation lines): as s19
+  gpusuite 900; rc=$?; [ $rc -le 1 ] || exit $rc
+  run smoke 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" || exit 1
+  for wb in "def-small 65536" "def-small 8192" "def-small 4096" "2p-middle-multi 16384" "def-large 16384"; do set -- $wb
+    NO_PHASES=1 PROF_DIR=$O/prof_$1_$2 WL=$1 B=$2 run prof_$1_$2 900 bash scripts/profile_session.sh || exit 1
+  done
+  for bb in 65536 32768 16384 8192 4096; do
+    run line_$bb 200 python bench.py --global-batch $bb --no-cpu-baseline --steps $((bb > 20000 ? 300 : 2000)) || exit 1; line line_$bb
+  done
+  run line_p2 300 python bench.py --workload 2p-middle-multi --no-cpu-baseline --steps 200 || exit 1; line line_p2
+  run line_l30 300 python bench.py --workload def-large --global-batch 16384 --no-cpu-baseline --steps 200 || exit 1; line line_l30
+  run bench_driver 300 python bench.py --gpus 1 --steps 20 --warmup 5 || exit 1; grep '^{' $O/bench_driver.log; line bench_driver
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
