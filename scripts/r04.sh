@@ -323,5 +323,12 @@ s21)  # final build (plain shared observation lines): as s19
   run line_l30 300 python bench.py --workload def-large --global-batch 16384 --no-cpu-baseline --steps 200 || exit 1; line line_l30
   run bench_driver 300 python bench.py --gpus 1 --steps 20 --warmup 5 || exit 1; grep '^{' $O/bench_driver.log; line bench_driver
   ;;
+s22)  # the 30x30 step time by buffer placement (probe_alloc), repeated 30x30 lines; store-policy parity test
+  run alloc_l30 600 python scripts/probe_alloc.py 30 16384 3 6 || exit 1; grep -v amdgpu $O/alloc_l30.log
+  for r in 1 2 3 4; do
+    run l30_$r 300 python bench.py --workload def-large --global-batch 16384 --no-cpu-baseline --steps 200 || exit 1; line l30_$r
+  done
+  run pytest_store 600 python -u -m pytest tests/test_gpu_store_policy.py -m gpu -v -x --timeout 500 --timeout-method thread -p no:cacheprovider || exit 1; tail -4 $O/pytest_store.log
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
