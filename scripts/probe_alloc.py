@@ -40,7 +40,37 @@ def obs_info(t):
     return "base %#x (mod 2M %#x)" % (p, p % (2 << 20))
 
 
+MODE = os.environ.get("PROBE_MODE", "torch")
 g = torch.Generator(device="cuda").manual_seed(5)
+if MODE == "hip":  # raw allocations: hipExtMallocWithFlags default (0) vs contiguous (4)
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    seeds = np.arange(B)
+    eng = TDEngine(L, B, "def", False, 1, np_seeds=seeds, py_seeds=seeds, autoreset=True)
+    eng.reset_all()
+    for _ in range(4):
+        timed(eng, g, 50)
+    print("engine (%s): own obs %s  %.1f us" % (eng.step_kernel_name, obs_info(eng.obs), timed(eng, g)), flush=True)
+    own = eng._io.obs
+    nbytes = B * 45 * L * L * 4
+    held = []
+    for rep in range(3):
+        for flags in (0, 4):
+            ptr = ctypes.c_void_p()
+            rc = hip.hipExtMallocWithFlags(ctypes.byref(ptr), ctypes.c_size_t(nbytes), ctypes.c_uint(flags))
+            if rc != 0:
+                print("  flags %d: hipExtMallocWithFlags rc %d" % (flags, rc), flush=True)
+                continue
+            held.append(ptr)
+            eng._io.obs = ptr.value
+            timed(eng, g, 10)
+            print("  flags %d: base %#x  %.1f us" % (flags, ptr.value, timed(eng, g)), flush=True)
+    eng._io.obs = own
+    torch.cuda.synchronize()
+    for ptr in held:
+        hip.hipFree(ptr)
+    eng.close()
+    sys.exit(0)
 for ei in range(NE):
     seeds = np.arange(B) + 100 * ei
     eng = TDEngine(L, B, "def", False, 1, np_seeds=seeds, py_seeds=seeds, autoreset=True)

@@ -330,5 +330,9 @@ s22)  # the 30x30 step time by buffer placement (probe_alloc), repeated 30x30 li
   done
   run pytest_store 600 python -u -m pytest tests/test_gpu_store_policy.py -m gpu -v -x --timeout 500 --timeout-method thread -p no:cacheprovider || exit 1; tail -4 $O/pytest_store.log
   ;;
+s23)  # 30x30 step time over raw allocations: default vs contiguous (hipDeviceMallocContiguous)
+  PROBE_MODE=hip run alloc_hip 600 python scripts/probe_alloc.py 30 16384 || exit 1; grep -v amdgpu $O/alloc_hip.log
+  run alloc_l30 600 python scripts/probe_alloc.py 30 16384 2 6 || exit 1; grep -v amdgpu $O/alloc_l30.log
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
