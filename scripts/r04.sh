@@ -334,5 +334,10 @@ s23)  # 30x30 step time over raw allocations: default vs contiguous (hipDeviceMa
   PROBE_MODE=hip run alloc_hip 600 python scripts/probe_alloc.py 30 16384 || exit 1; grep -v amdgpu $O/alloc_hip.log
   run alloc_l30 600 python scripts/probe_alloc.py 30 16384 2 6 || exit 1; grep -v amdgpu $O/alloc_l30.log
   ;;
+s24)  # default vs contiguous observation allocations at 10x10 / 65,536 and 8,192, 20x20 / 16,384, 30x30 again
+  for lb in "10 65536" "10 8192" "20 16384" "30 16384"; do set -- $lb
+    PROBE_MODE=hip run alloc_hip_$1_$2 600 python scripts/probe_alloc.py $1 $2 || exit 1; grep -v amdgpu $O/alloc_hip_$1_$2.log
+  done
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
