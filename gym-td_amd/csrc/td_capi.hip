@@ -191,9 +191,27 @@ int check_cfg(const td_config& c) {
   return 0;
 }
 
+// Device allocations are physically contiguous where the driver can give it
+// (hipDeviceMallocContiguous), else plain: the step's write streams then cover large page
+// fragments -- a contiguous observation buffer measured 4-5 % faster steps at 10x10 /
+// 65,536, 20x20 and 30x30 / 16,384 boards than default allocations (profiles/r04/s24).
+// TD_CONTIG=0: plain hipMalloc (A/B runs).
+static bool contig_on() {
+  static const int on = [] {
+    const char* e = std::getenv("TD_CONTIG");
+    return e ? (std::atoi(e) != 0 ? 1 : 0) : 1;
+  }();
+  return on != 0;
+}
+static hipError_t dev_malloc(void** p, size_t bytes) {
+  if (contig_on() && hipExtMallocWithFlags(p, bytes, hipDeviceMallocContiguous) == hipSuccess) return hipSuccess;
+  (void)hipGetLastError();  // (a refused contiguous request is not the caller's error)
+  return hipMalloc(p, bytes);
+}
+
 template <class T>
 int dalloc(T** p, size_t n) {
-  HIP_OK(hipMalloc((void**)p, std::max<size_t>(n, 1) * sizeof(T)));
+  HIP_OK(dev_malloc((void**)p, std::max<size_t>(n, 1) * sizeof(T)));
   HIP_OK(hipMemset(*p, 0, std::max<size_t>(n, 1) * sizeof(T)));
   return 0;
 }
@@ -341,6 +359,26 @@ extern "C" {
 int td_abi_version(void) { return TD_ABI_VERSION; }
 
 int td_step_io_size(void) { return (int)sizeof(td_step_io); }
+
+int td_alloc_device(size_t bytes, int device, void** out) {
+  if (!out || bytes == 0) return fail("td_alloc_device: bad arguments");
+  *out = nullptr;
+  HIP_OK(hipSetDevice(device));
+  HIP_OK(dev_malloc(out, bytes));
+  const hipError_t e = hipMemset(*out, 0, bytes);
+  if (e != hipSuccess) {
+    (void)hipFree(*out);
+    *out = nullptr;
+    return fail("td_alloc_device: %s", hipGetErrorString(e));
+  }
+  HIP_OK(hipDeviceSynchronize());  // zeroed before any stream uses it
+  return 0;
+}
+
+int td_free_device(void* p) {
+  if (p) HIP_OK(hipFree(p));
+  return 0;
+}
 
 void td_step_io_init(td_step_io* io) {
   if (!io) return;

@@ -24,6 +24,49 @@ HDR_DTYPE = np.dtype([
 assert HDR_DTYPE.itemsize == _lib.HDR_BYTES
 
 
+class _DeviceBlock(object):
+    """A td_alloc_device block seen by torch through __cuda_array_interface__.  The
+    tensor keeps this object alive; the block is freed when the last tensor (or view)
+    using it is gone."""
+
+    def __init__(self, ptr, shape, typestr):
+        self.ptr = ptr
+        self.__cuda_array_interface__ = {"shape": tuple(int(n) for n in shape), "typestr": typestr,
+                                         "data": (int(ptr), False), "version": 2, "strides": None}
+
+    def __del__(self):
+        try:
+            if self.ptr:
+                _lib.lib.td_free_device(self.ptr)
+                self.ptr = None
+        except Exception:  # (interpreter shutdown)
+            pass
+
+
+_TYPESTR = {torch.float32: "<f4", torch.int64: "<i8"}
+
+
+def device_zeros(shape, dtype, device):
+    """A zeroed device tensor in td_alloc_device memory (physically contiguous where the
+    driver can give it: the step writes its observation 4-5 % faster there than into a
+    default allocation, profiles/r04/s24); torch.zeros if torch cannot adopt the block."""
+    dev = torch.device(device)
+    n = int(np.prod(shape)) * torch.tensor([], dtype=dtype).element_size()
+    p = _lib.ctypes.c_void_p()
+    if _lib.lib.td_alloc_device(n, dev.index or 0, _lib.ctypes.byref(p)) != 0 or not p.value:
+        return torch.zeros(shape, dtype=dtype, device=dev)
+    blk = _DeviceBlock(p.value, shape, _TYPESTR[dtype])
+    try:
+        t = torch.as_tensor(blk, device=dev)
+    except Exception:
+        t = None
+    if t is None or t.data_ptr() != p.value or t.dtype != dtype or tuple(t.shape) != tuple(shape):
+        del blk  # (frees the block)
+        return torch.zeros(shape, dtype=dtype, device=dev)
+    t._td_block = True  # (tests: the block was adopted)
+    return t
+
+
 def _u32(a):
     return np.ascontiguousarray(a, dtype=np.uint32)
 
@@ -82,7 +125,9 @@ class TDEngine(object):
         dev = torch.device("cpu") if self.host_io else self.device
         zeros = (lambda shape, dtype: torch.zeros(shape, dtype=dtype).pin_memory()) if self.host_io else \
             (lambda shape, dtype: torch.zeros(shape, dtype=dtype, device=dev))
-        self.obs = zeros((B, _lib.NCH, L, L), torch.float32)
+        # the observation, the step's write stream: contiguous device memory (td_alloc_device)
+        self.obs = zeros((B, _lib.NCH, L, L), torch.float32) if self.host_io else \
+            device_zeros((B, _lib.NCH, L, L), torch.float32, self.device)
         self.reward = zeros(B, torch.float64)
         self.done = zeros(B, torch.uint8)
         self.info_enabled = bool(info)
@@ -96,7 +141,8 @@ class TDEngine(object):
             self.ep_len = zeros(B, torch.int32)
             if mode != "atk":
                 shape = (B, 6, L, L) if self.multi else (B,)
-                self.real_def = zeros(shape, torch.int64)
+                self.real_def = zeros(shape, torch.int64) if self.host_io or not self.multi else \
+                    device_zeros(shape, torch.int64, self.device)
                 self.fail_def = zeros(B, torch.int32)
             if mode != "def":
                 self.real_atk = zeros((B, 3, 8), torch.int64)

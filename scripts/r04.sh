@@ -339,5 +339,15 @@ s24)  # default vs contiguous observation allocations at 10x10 / 65,536 and 8,19
     PROBE_MODE=hip run alloc_hip_$1_$2 600 python scripts/probe_alloc.py $1 $2 || exit 1; grep -v amdgpu $O/alloc_hip_$1_$2.log
   done
   ;;
+s25)  # contiguous device allocations (library state + the engine's observation): GPU suite, A/B vs TD_CONTIG=0
+  gpusuite 900; rc=$?; [ $rc -le 1 ] || exit $rc
+  for r in 1 2; do for c in 1 0; do
+    for bb in 65536 32768 16384 8192 4096; do
+      TD_CONTIG=$c run c${c}_${bb}_$r 200 python bench.py --global-batch $bb --no-cpu-baseline --steps $((bb > 20000 ? 300 : 2000)) --timing none || exit 1; line c${c}_${bb}_$r
+    done
+    TD_CONTIG=$c run c${c}_p2_$r 300 python bench.py --workload 2p-middle-multi --no-cpu-baseline --steps 200 --timing none || exit 1; line c${c}_p2_$r
+    TD_CONTIG=$c run c${c}_l30_$r 300 python bench.py --workload def-large --global-batch 16384 --no-cpu-baseline --steps 200 --timing none || exit 1; line c${c}_l30_$r
+  done; done
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac

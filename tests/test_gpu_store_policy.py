@@ -62,3 +62,32 @@ def test_shared_line_policies_agree(L, B, steps):
     finally:
         for e in engs:
             e.close()
+
+
+def test_engine_observation_block():
+    """The engine's observation lives in a td_alloc_device block adopted by torch
+    (contiguous device memory), is freed with its last tensor, and steps give the same
+    bytes as into a torch-allocated buffer."""
+    L, B = 10, 512
+    seeds = np.arange(B) + 900
+    a = TDEngine(L, B, "def", False, 1, np_seeds=seeds, py_seeds=seeds, autoreset=True)
+    b = TDEngine(L, B, "def", False, 1, np_seeds=seeds, py_seeds=seeds, autoreset=True)
+    try:
+        assert getattr(a.obs, "_td_block", False), "torch did not adopt the td_alloc_device block"
+        b.obs = torch.zeros_like(b.obs)
+        b._io.obs = b.obs.data_ptr()
+        a.reset_all()
+        b.reset_all()
+        g = torch.Generator(device="cuda").manual_seed(3)
+        for k in range(60):
+            d = torch.randint(0, 6 * L * L + 1, (B,), device="cuda", generator=g, dtype=torch.int64)
+            a.step(def_act=d)
+            b.step(def_act=d)
+            assert torch.equal(a.obs, b.obs), k
+        view = a.obs[3]
+        keep = view.clone()
+    finally:
+        a.close()
+        b.close()
+    torch.cuda.synchronize()
+    assert torch.equal(view, keep)  # a view keeps the block alive after the engine closed
