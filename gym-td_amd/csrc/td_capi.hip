@@ -363,15 +363,18 @@ int td_step_io_size(void) { return (int)sizeof(td_step_io); }
 int td_alloc_device(size_t bytes, int device, void** out) {
   if (!out || bytes == 0) return fail("td_alloc_device: bad arguments");
   *out = nullptr;
+  int prev = 0;
+  HIP_OK(hipGetDevice(&prev));
   HIP_OK(hipSetDevice(device));
-  HIP_OK(dev_malloc(out, bytes));
-  const hipError_t e = hipMemset(*out, 0, bytes);
+  hipError_t e = dev_malloc(out, bytes);
+  if (e == hipSuccess) e = hipMemset(*out, 0, bytes);
+  if (e == hipSuccess) e = hipDeviceSynchronize();  // zeroed before any stream uses it
+  (void)hipSetDevice(prev);  // (the caller's current device is left as it was)
   if (e != hipSuccess) {
-    (void)hipFree(*out);
+    if (*out) (void)hipFree(*out);
     *out = nullptr;
     return fail("td_alloc_device: %s", hipGetErrorString(e));
   }
-  HIP_OK(hipDeviceSynchronize());  // zeroed before any stream uses it
   return 0;
 }
 
