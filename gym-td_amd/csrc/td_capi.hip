@@ -191,27 +191,26 @@ int check_cfg(const td_config& c) {
   return 0;
 }
 
-// Device allocations are physically contiguous where the driver can give it
-// (hipDeviceMallocContiguous), else plain: the step's write streams then cover large page
-// fragments -- a contiguous observation buffer measured 4-5 % faster steps at 10x10 /
-// 65,536, 20x20 and 30x30 / 16,384 boards than default allocations (profiles/r04/s24).
-// TD_CONTIG=0: plain hipMalloc (A/B runs).
+// Device allocations: plain hipMalloc.  TD_CONTIG=1 (A/B runs): physically contiguous where
+// the driver can give it (hipDeviceMallocContiguous) -- every state array of the engine
+// contiguous measured slower at most sizes (8,192 boards 35.1 vs 32.5 us, 65,536 215.0 vs
+// 210.4; 30x30 498 vs 519, profiles/r04/s25).  Callers' output buffers: td_alloc_device.
 static bool contig_on() {
   static const int on = [] {
     const char* e = std::getenv("TD_CONTIG");
-    return e ? (std::atoi(e) != 0 ? 1 : 0) : 1;
+    return e && std::atoi(e) != 0 ? 1 : 0;
   }();
   return on != 0;
 }
-static hipError_t dev_malloc(void** p, size_t bytes) {
-  if (contig_on() && hipExtMallocWithFlags(p, bytes, hipDeviceMallocContiguous) == hipSuccess) return hipSuccess;
+static hipError_t dev_malloc(void** p, size_t bytes, bool contiguous) {
+  if (contiguous && hipExtMallocWithFlags(p, bytes, hipDeviceMallocContiguous) == hipSuccess) return hipSuccess;
   (void)hipGetLastError();  // (a refused contiguous request is not the caller's error)
   return hipMalloc(p, bytes);
 }
 
 template <class T>
 int dalloc(T** p, size_t n) {
-  HIP_OK(dev_malloc((void**)p, std::max<size_t>(n, 1) * sizeof(T)));
+  HIP_OK(dev_malloc((void**)p, std::max<size_t>(n, 1) * sizeof(T), contig_on()));
   HIP_OK(hipMemset(*p, 0, std::max<size_t>(n, 1) * sizeof(T)));
   return 0;
 }
@@ -360,13 +359,13 @@ int td_abi_version(void) { return TD_ABI_VERSION; }
 
 int td_step_io_size(void) { return (int)sizeof(td_step_io); }
 
-int td_alloc_device(size_t bytes, int device, void** out) {
+int td_alloc_device(size_t bytes, int device, int contiguous, void** out) {
   if (!out || bytes == 0) return fail("td_alloc_device: bad arguments");
   *out = nullptr;
   int prev = 0;
   HIP_OK(hipGetDevice(&prev));
   HIP_OK(hipSetDevice(device));
-  hipError_t e = dev_malloc(out, bytes);
+  hipError_t e = dev_malloc(out, bytes, contiguous != 0);
   if (e == hipSuccess) e = hipMemset(*out, 0, bytes);
   if (e == hipSuccess) e = hipDeviceSynchronize();  // zeroed before any stream uses it
   (void)hipSetDevice(prev);  // (the caller's current device is left as it was)

@@ -62,7 +62,7 @@ def _load():
         "td_abi_version": (ctypes.c_int, []),
         "td_step_io_size": (ctypes.c_int, []),
         "td_step_io_init": (None, [ctypes.POINTER(TdStepIO)]),
-        "td_alloc_device": (ctypes.c_int, [ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+        "td_alloc_device": (ctypes.c_int, [ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
         "td_free_device": (ctypes.c_int, [ctypes.c_void_p]),
         "td_last_error": (ctypes.c_char_p, []),
         "td_config_default": (None, [ctypes.POINTER(TdConfig)]),

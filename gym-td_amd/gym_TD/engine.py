@@ -6,6 +6,7 @@ outputs are torch tensors on the engine's device; every step is one kernel
 launch on torch's current stream.
 """
 import copy
+import os
 import types
 
 import numpy as np
@@ -46,14 +47,19 @@ class _DeviceBlock(object):
 _TYPESTR = {torch.float32: "<f4", torch.int64: "<i8"}
 
 
-def device_zeros(shape, dtype, device):
-    """A zeroed device tensor in td_alloc_device memory (physically contiguous where the
-    driver can give it: the step writes its observation 4-5 % faster there than into a
-    default allocation, profiles/r04/s24); torch.zeros if torch cannot adopt the block."""
+# The engine's observation in physically contiguous device memory (TD_CONTIG_OBS=1) or a
+# plain allocation (0); see DESIGN.md section 3 for the measurements behind the default.
+CONTIG_OBS = int(os.environ.get("TD_CONTIG_OBS", "1")) != 0
+
+
+def device_zeros(shape, dtype, device, contiguous=None):
+    """A zeroed device tensor in td_alloc_device memory (contiguous: physically contiguous
+    where the driver can give it); torch.zeros if torch cannot adopt the block."""
     dev = torch.device(device)
     n = int(np.prod(shape)) * torch.tensor([], dtype=dtype).element_size()
     p = _lib.ctypes.c_void_p()
-    if _lib.lib.td_alloc_device(n, dev.index or 0, _lib.ctypes.byref(p)) != 0 or not p.value:
+    contig = CONTIG_OBS if contiguous is None else bool(contiguous)
+    if _lib.lib.td_alloc_device(n, dev.index or 0, int(contig), _lib.ctypes.byref(p)) != 0 or not p.value:
         return torch.zeros(shape, dtype=dtype, device=dev)
     blk = _DeviceBlock(p.value, shape, _TYPESTR[dtype])
     try:

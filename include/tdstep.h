@@ -114,14 +114,15 @@ typedef struct td_handle td_handle;
 int td_abi_version(void);
 /* sizeof(td_step_io) as this library was built (120 on LP64 at ABI 3). */
 int td_step_io_size(void);
-/* Device memory for a caller's output buffers (the observation above all): zeroed, and
- * physically contiguous where the driver can give it (hipDeviceMallocContiguous), else a
- * plain allocation.  The step's observation stream then covers large page fragments: 4-5 %
- * faster steps than a default allocation at 10x10 / 65,536 boards and at 20x20 / 30x30
- * (profiles/r04/s24).  The reference allocates its observation per call (np.zeros in
- * TDBoard.get_states, gym_TD/envs/TDBoard.py:85-112); no counterpart.  td_free_device
- * releases it (after the work that writes it is done). */
-int td_alloc_device(size_t bytes, int device, void** out);
+/* Device memory for a caller's output buffers (the observation above all), zeroed;
+ * contiguous != 0: physically contiguous where the driver can give it
+ * (hipDeviceMallocContiguous), else a plain allocation.  A contiguous observation stepped
+ * 4-5 % faster than a default allocation at 10x10 / 65,536 and 20x20 / 30x30 boards in
+ * one probe (profiles/r04/s24); TDEngine's choice is TD_CONTIG_OBS (gym_TD/engine.py).
+ * The reference allocates its observation per call (np.zeros in TDBoard.get_states,
+ * gym_TD/envs/TDBoard.py:85-112); no counterpart.  td_free_device releases it (after the
+ * work that writes it is done). */
+int td_alloc_device(size_t bytes, int device, int contiguous, void** out);
 int td_free_device(void* p);
 /* Zero *io and set its size / abi words (a C caller's initialiser; writes td_step_io_size()
  * bytes, so io must be this header's td_step_io). */

@@ -349,5 +349,19 @@ s25)  # contiguous device allocations (library state + the engine's observation)
     TD_CONTIG=$c run c${c}_l30_$r 300 python bench.py --workload def-large --global-batch 16384 --no-cpu-baseline --steps 200 --timing none || exit 1; line c${c}_l30_$r
   done; done
   ;;
+s26)  # plain state arrays; the engine's observation contiguous (TD_CONTIG_OBS=1, default) vs plain: GPU suite, A/B, final profiles
+  gpusuite 900; rc=$?; [ $rc -le 1 ] || exit $rc
+  for c in 1 0; do
+    for bb in 65536 32768 16384 8192 4096; do
+      TD_CONTIG_OBS=$c run o${c}_${bb} 200 python bench.py --global-batch $bb --no-cpu-baseline --steps $((bb > 20000 ? 300 : 2000)) --timing none || exit 1; line o${c}_${bb}
+    done
+    TD_CONTIG_OBS=$c run o${c}_p2 300 python bench.py --workload 2p-middle-multi --no-cpu-baseline --steps 200 --timing none || exit 1; line o${c}_p2
+    TD_CONTIG_OBS=$c run o${c}_l30 300 python bench.py --workload def-large --global-batch 16384 --no-cpu-baseline --steps 200 --timing none || exit 1; line o${c}_l30
+  done
+  for wb in "def-small 65536" "def-small 8192" "def-small 4096" "2p-middle-multi 16384" "def-large 16384"; do set -- $wb
+    NO_PHASES=1 PROF_DIR=$O/prof_$1_$2 WL=$1 B=$2 run prof_$1_$2 900 bash scripts/profile_session.sh || exit 1
+  done
+  run bench_driver 300 python bench.py --gpus 1 --steps 20 --warmup 5 || exit 1; grep '^{' $O/bench_driver.log; line bench_driver
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
