@@ -47,9 +47,19 @@ class _DeviceBlock(object):
 _TYPESTR = {torch.float32: "<f4", torch.int64: "<i8"}
 
 
-# The engine's observation in physically contiguous device memory (TD_CONTIG_OBS=1) or a
-# plain allocation (0); see DESIGN.md section 3 for the measurements behind the default.
-CONTIG_OBS = int(os.environ.get("TD_CONTIG_OBS", "1")) != 0
+# The engine's observation in physically contiguous device memory or a plain allocation.
+# auto (default): contiguous from CONTIG_OBS_MIN bytes on -- faster there (32,768 boards at
+# 10x10, 590 MB: 112.5 vs 115.5 us; 30x30 / 16,384, 2.65 GB: 498.7 vs 517.6; 65,536 +-0),
+# slower below (16,384 / 8,192 / 4,096 boards: +0.6-2.2 %), profiles/r04/s26.
+# TD_CONTIG_OBS=1 / 0 forces it.
+CONTIG_OBS = os.environ.get("TD_CONTIG_OBS", "auto")
+CONTIG_OBS_MIN = 512 << 20
+
+
+def _contig_obs(nbytes):
+    if CONTIG_OBS == "auto":
+        return nbytes >= CONTIG_OBS_MIN
+    return int(CONTIG_OBS) != 0
 
 
 def device_zeros(shape, dtype, device, contiguous=None):
@@ -58,7 +68,7 @@ def device_zeros(shape, dtype, device, contiguous=None):
     dev = torch.device(device)
     n = int(np.prod(shape)) * torch.tensor([], dtype=dtype).element_size()
     p = _lib.ctypes.c_void_p()
-    contig = CONTIG_OBS if contiguous is None else bool(contiguous)
+    contig = _contig_obs(n) if contiguous is None else bool(contiguous)
     if _lib.lib.td_alloc_device(n, dev.index or 0, int(contig), _lib.ctypes.byref(p)) != 0 or not p.value:
         return torch.zeros(shape, dtype=dtype, device=dev)
     blk = _DeviceBlock(p.value, shape, _TYPESTR[dtype])

@@ -363,5 +363,15 @@ s26)  # plain state arrays; the engine's observation contiguous (TD_CONTIG_OBS=1
   done
   run bench_driver 300 python bench.py --gpus 1 --steps 20 --warmup 5 || exit 1; grep '^{' $O/bench_driver.log; line bench_driver
   ;;
+s27)  # the engine's observation contiguous from 512 MiB on (auto rule): GPU suite, smoke, bench lines, the driver's command
+  gpusuite 900; rc=$?; [ $rc -le 1 ] || exit $rc
+  run smoke 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" || exit 1
+  for bb in 65536 32768 16384 8192 4096; do
+    run line_$bb 200 python bench.py --global-batch $bb --no-cpu-baseline --steps $((bb > 20000 ? 300 : 2000)) || exit 1; line line_$bb
+  done
+  run line_p2 300 python bench.py --workload 2p-middle-multi --no-cpu-baseline --steps 200 || exit 1; line line_p2
+  run line_l30 300 python bench.py --workload def-large --global-batch 16384 --no-cpu-baseline --steps 200 || exit 1; line line_l30
+  run bench_driver 300 python bench.py --gpus 1 --steps 20 --warmup 5 || exit 1; grep '^{' $O/bench_driver.log; line bench_driver
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
