@@ -54,8 +54,9 @@ if MODE == "hip":  # raw allocations: hipExtMallocWithFlags default (0) vs conti
     own = eng._io.obs
     nbytes = B * 45 * L * L * 4
     held = []
-    for rep in range(3):
-        for flags in (0, 4):
+    flag_set = [int(f) for f in os.environ.get("PROBE_FLAGS", "0,4").split(",")]
+    for rep in range(int(os.environ.get("PROBE_REPS", "3"))):
+        for flags in flag_set:
             ptr = ctypes.c_void_p()
             rc = hip.hipExtMallocWithFlags(ctypes.byref(ptr), ctypes.c_size_t(nbytes), ctypes.c_uint(flags))
             if rc != 0:

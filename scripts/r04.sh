@@ -373,5 +373,10 @@ s27)  # the engine's observation contiguous from 512 MiB on (auto rule): GPU sui
   run line_l30 300 python bench.py --workload def-large --global-batch 16384 --no-cpu-baseline --steps 200 || exit 1; line line_l30
   run bench_driver 300 python bench.py --gpus 1 --steps 20 --warmup 5 || exit 1; grep '^{' $O/bench_driver.log; line bench_driver
   ;;
+s28)  # observation allocation kinds: default 0, contiguous 4, fine-grained 1, uncached 3 (30x30 and 10x10 / 65,536)
+  for lb in "30 16384" "10 65536"; do set -- $lb
+    PROBE_MODE=hip PROBE_FLAGS=0,4,1,3 PROBE_REPS=2 run alloc_kinds_$1_$2 600 python scripts/probe_alloc.py $1 $2 || exit 1; grep -v amdgpu $O/alloc_kinds_$1_$2.log
+  done
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
