@@ -157,22 +157,23 @@ def kernel_source_hash():
     return h.hexdigest()[:16]
 
 
-def measured_traffic(workload, boards, kernel=None):
+def measured_traffic(workload, boards, kernel, obs_alloc, path=None):
     """(bytes per launch, source) from profiles/pmc_traffic.json when that file holds a
-    PMC measurement of this workload at these boards per GPU on this build and, when the
-    record names one, this step kernel."""
-    tp = os.path.join(HERE, "profiles", "pmc_traffic.json")
+    PMC measurement of this workload at these boards per GPU on this build (kernel source
+    hash), of this step kernel, with the observation allocated the same way (contiguous /
+    plain: the write stream's placement changes the kernel).  Else (None, None)."""
+    tp = path or os.path.join(HERE, "profiles", "pmc_traffic.json")
     try:
         rec = json.load(open(tp)).get("%s_B%d" % (workload, boards))
     except Exception:  # noqa: BLE001
         return None, None
     if not rec or rec.get("kernel_src") != kernel_source_hash():
         return None, None
-    if kernel is not None and rec.get("kernel") not in (None, kernel):
+    if rec.get("kernel") != kernel or rec.get("obs_alloc") != obs_alloc:
         return None, None
     return rec["hbm_bytes_per_launch"], "profiles/pmc_traffic.json[%s_B%d] (%s, rocprofv3 --pmc FETCH_SIZE / " \
-        "WRITE_SIZE passes of bench.py at the same boards per GPU, kernel sources %s)" % (
-            workload, boards, rec.get("round", "?"), rec["kernel_src"])
+        "WRITE_SIZE passes of bench.py at the same boards per GPU, kernel sources %s, %s observation)" % (
+            workload, boards, rec.get("round", "?"), rec["kernel_src"], obs_alloc)
 
 
 # --------------------------------------------------------------------------- CPU baseline
@@ -314,6 +315,33 @@ def check_world(gpus, env):
     return None if gpus > 1 else 1
 
 
+# --------------------------------------------------------------------------- ranks
+def init_dist(gpu, backend="nccl"):
+    """The rank's process group (RANK / WORLD_SIZE / MASTER_* from the launcher's env): RCCL
+    (backend "nccl") bound to the rank's GPU, or gloo for CPU-side rehearsals.  Returns the
+    device the collectives' tensors live on.  tests/test_gpu_rccl.py runs this very call at
+    world size 1 on the GPU box."""
+    torch.cuda.set_device(gpu)
+    if backend == "nccl":
+        dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        return torch.device("cuda", gpu)
+    dist.init_process_group(backend)
+    return torch.device("cpu")
+
+
+def collect(elapsed, avg_kernel_s, sample_step_s, ep_stats, ep_recs, coll):
+    """After the timed region: the MAX of the clocks over ranks (one all_reduce) and the
+    timed steps' episode statistics (per-rank count / return sum, f64 [2]) and per-board
+    last-episode records (16 B per board) gathered to rank 0 -- the only exchange of a run,
+    over RCCL on GPUs.  Returns ((elapsed, avg_kernel_s, sample_step_s), per_rank [W, 2],
+    (ret, length, win)); the last two are None off rank 0."""
+    from gym_TD import shard
+    t = shard.max_over_ranks(torch.tensor([elapsed, avg_kernel_s, sample_step_s], dtype=torch.float64, device=coll))
+    per_rank = shard.gather_stats(ep_stats.to(coll))
+    recs = shard.gather_episode_records(*[x.to(coll) for x in ep_recs])
+    return tuple(float(v) for v in t.cpu()), per_rank, recs
+
+
 # --------------------------------------------------------------------------- main
 def main():
     ap = argparse.ArgumentParser()
@@ -354,14 +382,8 @@ def main():
     # flow with every rank on cuda:0 of a one-GPU box (never the measured configuration)
     backend = os.environ.get("TD_BENCH_DIST_BACKEND", "nccl")
     gpu = 0 if os.environ.get("TD_BENCH_SAME_DEVICE") == "1" else local
-    if world > 1:
-        torch.cuda.set_device(gpu)
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
-        else:
-            dist.init_process_group(backend)
     dev = torch.device("cuda", gpu if world > 1 else 0)
-    coll = dev if backend == "nccl" else torch.device("cpu")  # where the collectives' tensors live
+    coll = init_dist(gpu, backend) if world > 1 else dev  # where the collectives' tensors live
     torch.cuda.set_device(dev)
 
     from gym_TD.engine import TDEngine
@@ -469,12 +491,8 @@ def main():
     avg_kernel_s = float(np.mean(kern_ms)) / 1e3
     # after timing: MAX of the clocks over ranks, and the episode statistics of the
     # timed steps gathered to rank 0 (the only exchange; RCCL on GPUs)
-    t = shard.max_over_ranks(torch.tensor([elapsed, avg_kernel_s, sample_wall / n_sample_steps], dtype=torch.float64,
-                                          device=coll))
-    per_rank = shard.gather_stats(ep_stats.to(coll))
-    # the per-board payload (16 B per board: last episode's return, length, win)
-    recs = shard.gather_episode_records(*[t.to(coll) for t in ep_recs])
-    elapsed, avg_kernel_s, sample_step_s = float(t[0]), float(t[1]), float(t[2])
+    (elapsed, avg_kernel_s, sample_step_s), per_rank, recs = collect(
+        elapsed, avg_kernel_s, sample_wall / n_sample_steps, ep_stats, ep_recs, coll)
     reported_world = dist.get_world_size() if world > 1 else 1  # what the process group (RCCL) reports
 
     if rank == 0:
@@ -483,7 +501,7 @@ def main():
         bpe = algorithmic_bytes(L, mode, multi)
         achieved = B * bpe / avg_kernel_s / 1e9
         exceeds, why = kernel_vs_step(avg_kernel_s * 1e6, sample_step_s * 1e6)
-        traffic, traffic_src = measured_traffic(args.workload, B, eng.step_kernel_name)
+        traffic, traffic_src = measured_traffic(args.workload, B, eng.step_kernel_name, eng.obs_alloc)
         out = {
             "metric": metric,
             "value": value, "unit": "env-steps/s", "n_gpus": world, "world_size_reported": reported_world,
@@ -495,7 +513,7 @@ def main():
                                    "auto-reset, burn-in %d steps%s"
                                    % (ENV_ID[args.workload], L, L, global_batch, world, B, scaling, base_cfg,
                                       args.burnin, ", episode phases staggered" if args.stagger else ""),
-                       "global_batch": global_batch, "boards_per_gpu": B,
+                       "global_batch": global_batch, "boards_per_gpu": B, "obs_alloc": eng.obs_alloc,
                        "map_size": L, "parallelism": "boards sharded per GPU (dp%d), no data-path collective" % world},
             "roofline": {"bound": "hbm", "achieved": None if exceeds else achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": None if exceeds else achieved / HBM_PEAK_GBS,

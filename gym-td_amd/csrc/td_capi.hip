@@ -104,14 +104,11 @@ struct td_handle {
   // per-board claims keep concurrent refills apart).
   hipStream_t side[kSideStreams] = {};
   hipEvent_t ev_main = nullptr;  // orders a refill after a reset kernel (system-scope fence)
-  hipEvent_t ev_step = nullptr;  // orders a refill after the previous step (TD_EVENT_FENCE A/B: its fence scope)
+  hipEvent_t ev_step = nullptr;  // orders a refill after the previous step (no system-scope fence)
   int next_side = 0;
   int refill_every = kRefillEvery;  // 0: no refill launches (td_set_refill_interval)
   int refill_waves = kRefillWaves;  // waves per refill launch
-  int n_side = kSideStreams;  // A/B knob (TD_SIDE_STREAMS)
-  int refill_serial = 0;      // A/B knob (TD_REFILL_SERIAL=1): refills on the step stream, between steps
-  int refill_walks = 0;  // walks per board per refill launch (0: 12 per step of interval; TD_REFILL_WALKS)
-  int guard_every = kGuardEvery;  // ring guard cadence (<= NSLOT; 0 only in TD_GUARD_EVERY=0 A/B runs)
+  int guard_every = kGuardEvery;  // ring guard cadence
   int since_guard = kGuardEvery;  // steps launched since the last ring guard (>= guard_every: guard first)
   // td_kernel_timing: event pairs bound to the next `tev_cap` step-kernel dispatches
   std::vector<hipEvent_t> tev;
@@ -119,17 +116,11 @@ struct td_handle {
   long long tev_from = 0;  // h->steps when td_kernel_timing was called
   long long steps = 0;
   std::vector<int32_t> last_reset_failed;
-  // longest-work-first board order of the small kernels (td_step.hip ord_*): two lists
-  // (this step's, the next step's) and two sets of chunk counters, by parity of ord_steps
-  uint32_t* d_ord = nullptr;
-  uint32_t* d_ord_cnt = nullptr;
-  int ord_stride = 0;
-  int ord_on = 0;  // TD_ORDER=1: longest-work-first order (A/B runs; slower, profiles/r04/s2)
-  int xcd_map = 1;  // XCD-contiguous board map (td_step.hip xcd_board; TD_XCD_MAP=0: block i = board i)
+  uint32_t* d_guard_to = nullptr;  // [1] ring-guard claim waits that gave up (td_guard_timeouts)
+  int xcd_map = 1;  // XCD-contiguous board map (td_kernels.h xcd_board; td_set_store_policy)
   int edge_wt = 2;  // observation lines shared with a neighbour: plain write-back stores, merged in the XCD's L2
                     // (1.088x vs 1.093x the algorithmic bytes at 65,536 boards, step time +-0, profiles/r04/s20);
-                    // TD_EDGE_WT=1: write-through (sc1); 0: non-temporal (233 vs 212 us, profiles/r04/s4)
-  long long ord_steps = 0;
+                    // 1: write-through (sc1), the reference form of tests/test_gpu_store_policy.py
 };
 
 namespace {
@@ -191,17 +182,9 @@ int check_cfg(const td_config& c) {
   return 0;
 }
 
-// Device allocations: plain hipMalloc.  TD_CONTIG=1 (A/B runs): physically contiguous where
-// the driver can give it (hipDeviceMallocContiguous) -- every state array of the engine
-// contiguous measured slower at most sizes (8,192 boards 35.1 vs 32.5 us, 65,536 215.0 vs
-// 210.4; 30x30 498 vs 519, profiles/r04/s25).  Callers' output buffers: td_alloc_device.
-static bool contig_on() {
-  static const int on = [] {
-    const char* e = std::getenv("TD_CONTIG");
-    return e && std::atoi(e) != 0 ? 1 : 0;
-  }();
-  return on != 0;
-}
+// Device allocations.  The library's own arrays are plain hipMalloc: every state array
+// physically contiguous as well measured slower at most sizes (8,192 boards 35.1 vs 32.5
+// us, 65,536 215.0 vs 210.4, profiles/r04/s25).  Callers' output buffers: td_alloc_device.
 static hipError_t dev_malloc(void** p, size_t bytes, bool contiguous) {
   if (contiguous && hipExtMallocWithFlags(p, bytes, hipDeviceMallocContiguous) == hipSuccess) return hipSuccess;
   (void)hipGetLastError();  // (a refused contiguous request is not the caller's error)
@@ -210,7 +193,7 @@ static hipError_t dev_malloc(void** p, size_t bytes, bool contiguous) {
 
 template <class T>
 int dalloc(T** p, size_t n) {
-  HIP_OK(dev_malloc((void**)p, std::max<size_t>(n, 1) * sizeof(T), contig_on()));
+  HIP_OK(hipMalloc((void**)p, std::max<size_t>(n, 1) * sizeof(T)));
   HIP_OK(hipMemset(*p, 0, std::max<size_t>(n, 1) * sizeof(T)));
   return 0;
 }
@@ -235,7 +218,8 @@ StepArgs base_args(td_handle* h) {
   a.slot_words = slot_words(h->L);
   a.refill_grp = refill_group(h->B, h->refill_waves);
   a.refill_waves = h->refill_waves;
-  a.refill_walks = h->refill_walks > 0 ? h->refill_walks : kWalksPerStep * (h->refill_every > 0 ? h->refill_every : kRefillEvery);
+  a.refill_walks = kWalksPerStep * (h->refill_every > 0 ? h->refill_every : kRefillEvery);
+  a.guard_to = h->d_guard_to;
   a.reset_fail = h->d_fail; a.cfg = h->d_cfg + h->epoch; a.cfgs = h->d_cfg; a.epoch = h->epoch;
   return a;
 }
@@ -253,25 +237,6 @@ void parallel_for(int n, F fn) {
   for (auto& t : pool) t.join();
 }
 
-// The board-order lists of the small kernels (td_step.hip ord_*) for the kernel now chosen:
-// both start as the board map (virtual block vb steps board xcd_board_v(vb) -- or vb
-// without the XCD map -- with the kernel's boards per workgroup), the chunk counters at
-// zero.  Called with the device idle (td_create, td_set_step_kernel).
-int ord_init(td_handle* h) {
-  const int bpw = h->small == 1 ? kSmallBPW : 1;
-  std::vector<uint32_t> ord((size_t)2 * ORD_XCD * h->ord_stride, 0u);
-  for (int vb = 0; vb < h->B; ++vb) {
-    int x, slot;
-    ord_pos(vb, bpw, x, slot);
-    const uint32_t b = (uint32_t)(h->xcd_map ? xcd_board_v(vb, h->B, bpw) : vb);
-    for (int p = 0; p < 2; ++p) ord[((size_t)p * ORD_XCD + x) * h->ord_stride + slot] = b;
-  }
-  HIP_OK(hipMemcpy(h->d_ord, ord.data(), ord.size() * 4, hipMemcpyHostToDevice));
-  HIP_OK(hipMemset(h->d_ord_cnt, 0, (size_t)2 * ORD_CNT_WORDS * 4));
-  h->ord_steps = 0;
-  return 0;
-}
-
 // The step kernel (td_set_step_kernel): small = 0 large, 1 small, 2 small2.  Write-through
 // observation stores go with the small kernels where the batch's observation fits the
 // 256-MiB Infinity Cache (scripts/storepol.hip: 21.8 vs 30.0 us at 8,192 boards).
@@ -281,13 +246,12 @@ int apply_kernel(td_handle* h, int small) {
   // (Write-through beyond the Infinity Cache -- any kernel, TD_OBS_WT=1 -- measured 1.5-1.7x
   // slower steps at 16,384-65,536 boards, profiles/r03/s21.)
   h->obs_wt = h->small && obs_bytes <= 192.0 * 1024 * 1024 ? 1 : 0;
-  if (const char* e = std::getenv("TD_OBS_WT")) h->obs_wt = std::atoi(e) ? 1 : 0;  // A/B runs
   const bool has_small = h->L == 10 || h->L == 20 || h->L == 30;
   const char* k = !has_small || small == 0 ? "td_step_kernel" : small == 1 ? "td_step_kernel_small" : "td_step_kernel_small2";
   char buf[96];
   std::snprintf(buf, sizeof buf, "%s<%d, %d, %s>", k, has_small ? h->L : 0, h->mode, h->multi ? "true" : "false");
   h->kernel_name = buf;
-  return ord_init(h);
+  return 0;
 }
 
 // Drop staged layouts: they were drawn from a stream that has been replaced.
@@ -326,15 +290,11 @@ int drop_all_staged(td_handle* h) {
 int start_refill(td_handle* h, hipStream_t s, bool after_step = false) {
   const int q = h->next_side;
   StepArgs a = base_args(h);
-  if (h->refill_serial) {
-    HIP_OK(launch_refill(a, s));
-    return 0;
-  }
   hipEvent_t ev = after_step ? h->ev_step : h->ev_main;
   HIP_OK(hipEventRecord(ev, s));
   HIP_OK(hipStreamWaitEvent(h->side[q], ev, 0));
   HIP_OK(launch_refill(a, h->side[q]));
-  h->next_side = (q + 1) % h->n_side;
+  h->next_side = (q + 1) % kSideStreams;
   return 0;
 }
 
@@ -482,12 +442,7 @@ td_handle* td_create(const td_config* cfg, int map_size, int n_boards, int mode,
   rc |= dalloc(&h->d_stage, (size_t)h->stage_cap * h->lw);
   rc |= dalloc(&h->d_epstats, 2);
   rc |= dalloc(&h->d_lastep, B);
-  if (const char* e = std::getenv("TD_XCD_MAP")) h->xcd_map = std::atoi(e) ? 1 : 0;  // A/B runs
-  if (const char* e = std::getenv("TD_EDGE_WT")) h->edge_wt = std::atoi(e) == 2 ? 2 : std::atoi(e) ? 1 : 0;
-  h->ord_stride = ord_stride(n_boards);
-  rc |= dalloc(&h->d_ord, (size_t)2 * ORD_XCD * h->ord_stride);
-  rc |= dalloc(&h->d_ord_cnt, (size_t)2 * ORD_CNT_WORDS);
-  if (const char* e = std::getenv("TD_ORDER")) h->ord_on = std::atoi(e) ? 1 : 0;  // A/B runs
+  rc |= dalloc(&h->d_guard_to, 1);
   if (rc) {  // name the footprint (the staged-layout rings are most of it at large L)
     const double ring = (double)B * NSLOT * slot_words(map_size) * 4.0;
     const double total = (double)B * (sizeof(TdHdr) + ECAP * 20 + TCAP * 12 + (size_t)h->NC * 4 + 2 * OPP_WORDS * 4 +
@@ -503,28 +458,9 @@ td_handle* td_create(const td_config* cfg, int map_size, int n_boards, int mode,
       rc = fail("episode records init");
   }
   if (!rc && hipMemcpy(h->d_cfg, &h->dcfg, sizeof(TdDevCfg), hipMemcpyHostToDevice) != hipSuccess) rc = fail("cfg upload");
-  // Side streams (layout refills): TD_SIDE_PRIO=1 creates them at the device's least
-  // priority, TD_SIDE_CUS=n restricts them to n CUs (A/B knobs; default: plain streams).
-  {
-    const char* ep = std::getenv("TD_SIDE_PRIO");
-    const char* ec = std::getenv("TD_SIDE_CUS");
-    const int ncu = ec ? std::atoi(ec) : 0;
-    int least = 0, greatest = 0;
-    (void)hipDeviceGetStreamPriorityRange(&least, &greatest);
-    for (int q = 0; q < kSideStreams && !rc; ++q) {
-      hipError_t e;
-      if (ncu > 0) {
-        std::vector<uint32_t> mask(16, 0u);
-        // spread the CUs over the mask (the bit order interleaves XCDs / SEs)
-        for (int i = 0; i < ncu && i < 512; ++i) { const int bit = (i * 37) % 256; mask[bit / 32] |= 1u << (bit % 32); }
-        e = hipExtStreamCreateWithCUMask(&h->side[q], 8, mask.data());
-      } else if (ep && std::atoi(ep)) {
-        e = hipStreamCreateWithPriority(&h->side[q], hipStreamNonBlocking, least);
-      } else {
-        e = hipStreamCreateWithFlags(&h->side[q], hipStreamNonBlocking);
-      }
-      if (e != hipSuccess) rc = fail("side stream: %s", hipGetErrorString(e));
-    }
+  for (int q = 0; q < kSideStreams && !rc; ++q) {  // side streams (layout refills)
+    const hipError_t e = hipStreamCreateWithFlags(&h->side[q], hipStreamNonBlocking);
+    if (e != hipSuccess) rc = fail("side stream: %s", hipGetErrorString(e));
   }
   if (!rc && hipEventCreateWithFlags(&h->ev_main, hipEventDisableTiming) != hipSuccess) rc = fail("event");
   {
@@ -532,10 +468,8 @@ td_handle* td_create(const td_config* cfg, int map_size, int n_boards, int mode,
     // everything a refill reads of a step (lay_head) and publishes (slots, tags, claims,
     // the stream) goes through write-through / atomic accesses.  Without the event's
     // system-scope fence (a cache writeback): -0.6 % / -0.8 % per step at 8,192 / 4,096
-    // boards (profiles/r03/s17).  TD_EVENT_FENCE (A/B runs): 0 system, 1 device-scope release.
-    unsigned fl = hipEventDisableTiming | hipEventDisableSystemFence;
-    if (const char* e = std::getenv("TD_EVENT_FENCE"))
-      fl = hipEventDisableTiming | (std::atoi(e) == 1 ? hipEventReleaseToDevice : std::atoi(e) == 2 ? hipEventDisableSystemFence : 0u);
+    // boards (profiles/r03/s17).
+    const unsigned fl = hipEventDisableTiming | hipEventDisableSystemFence;
     if (!rc && hipEventCreateWithFlags(&h->ev_step, fl) != hipSuccess) rc = fail("event");
   }
   if (rc) { std::string e = g_err; td_destroy(h); g_err = e; return nullptr; }
@@ -557,12 +491,6 @@ td_handle* td_create(const td_config* cfg, int map_size, int n_boards, int mode,
     const int rounds2 = h->multi ? (h->L == 20 && h->mode == TD_MODE_2P ? 8 : 0) : h->L == 10 ? 3 : h->L == 30 ? 10 : 0;
     h->small_auto = n_boards <= resident2 ? 2 : n_boards <= resident ? 1 : n_boards <= rounds2 * resident ? 2 : 0;
     if (apply_kernel(h, h->small_auto)) { std::string e = g_err; td_destroy(h); g_err = e; return nullptr; }
-    if (const char* e = std::getenv("TD_REFILL_EVERY")) h->refill_every = std::max(0, std::atoi(e));  // A/B runs
-    if (const char* e = std::getenv("TD_REFILL_WAVES")) h->refill_waves = std::max(1, std::atoi(e));
-    if (const char* e = std::getenv("TD_REFILL_WALKS")) h->refill_walks = std::max(1, std::atoi(e));
-    if (const char* e = std::getenv("TD_GUARD_EVERY")) h->guard_every = std::min(kGuardEvery, std::max(0, std::atoi(e)));  // A/B runs
-    if (const char* e = std::getenv("TD_SIDE_STREAMS")) h->n_side = std::min(kSideStreams, std::max(1, std::atoi(e)));
-    if (const char* e = std::getenv("TD_REFILL_SERIAL")) h->refill_serial = std::atoi(e) ? 1 : 0;
   }
   std::vector<uint32_t> seeds(B);
   for (size_t b = 0; b < B; ++b) seeds[b] = (uint32_t)b;
@@ -577,7 +505,7 @@ void td_destroy(td_handle* h) {
   void* dptrs[] = {h->d_cfg, h->d_hdr, h->d_en_lp, h->d_en_mg, h->d_en_inf, h->d_tw_cd, h->d_tw_inf,
                    h->d_cells, h->d_opp, h->d_hot, h->d_np, h->d_nxt, h->d_scratch, h->d_lay_head, h->d_lay_tail,
                    h->d_lay_claim, h->d_ovr_idx, h->d_mask, h->d_fail, h->d_stage, h->d_epstats, h->d_lastep,
-                   h->d_ord, h->d_ord_cnt};
+                   h->d_guard_to};
   for (void* p : dptrs)
     if (p) (void)hipFree(p);
   if (h->ev_main) (void)hipEventDestroy(h->ev_main);
@@ -825,20 +753,7 @@ int td_step(td_handle* h, const td_step_io* io, void* stream) {
     e1 = h->tev[2 * (size_t)h->tev_n + 1];
     h->tev_n += 1;
   }
-  // the small kernels (launched for a 16-B-aligned observation, launch2) step their boards
-  // in the order the previous small-kernel step left
-  const bool ordered = h->ord_on && (h->small || kOrderLarge) && ((reinterpret_cast<uintptr_t>(io->obs) & 15u) == 0);
-  if (ordered) {
-    const int p = (int)(h->ord_steps & 1);
-    const size_t span = (size_t)ORD_XCD * h->ord_stride;
-    a.ord_in = h->d_ord + (size_t)p * span;
-    a.ord_out = h->d_ord + (size_t)(1 - p) * span;
-    a.ord_cnt = h->d_ord_cnt + (size_t)p * ORD_CNT_WORDS;
-    a.ord_clr = h->d_ord_cnt + (size_t)(1 - p) * ORD_CNT_WORDS;
-    a.ord_stride = h->ord_stride;
-  }
   HIP_OK(launch_step(a, s, false, e0, e1));
-  if (ordered) h->ord_steps += 1;
   if (h->autoreset && h->opp_np) HIP_OK(launch_autoreset(a, s));
   h->steps += 1;
   h->since_guard += 1;
@@ -870,9 +785,8 @@ int td_kernel_timing(td_handle* h, int max_launches, int every) {
   // Timing events without the system-scope release at the timed kernel's end: the cache
   // write-back it implies lengthens the very kernel being timed (4,096 boards: sampled
   // kernels 21.9 us = the 21.9-us step with it, 20.6 us in a 21.3-us step without;
-  // profiles/r04/s2).  TD_TEV_FLAGS=0 (A/B runs): default events.
-  const char* tf = std::getenv("TD_TEV_FLAGS");
-  const unsigned flags = tf && std::atoi(tf) == 0 ? hipEventDefault : hipEventDisableSystemFence;
+  // profiles/r04/s2).
+  const unsigned flags = hipEventDisableSystemFence;
   while ((int)h->tev.size() < 2 * max_launches) {
     hipEvent_t e = nullptr;
     HIP_OK(hipEventCreateWithFlags(&e, flags));
@@ -1057,10 +971,38 @@ int td_debug_ring(td_handle* h, int b, uint32_t* out, int cap) {
   return 3 + NSLOT;
 }
 
+// Diagnostic: hold (1) or give back (0) board b's refill claim, as a refill wave drawing
+// its layouts would (tests: a claim held past the ring guard's 1-s wait).
+int td_debug_set_claim(td_handle* h, int b, int held) {
+  if (!h || b < 0 || b >= h->B) return fail("td_debug_set_claim: bad board");
+  HIP_OK(hipDeviceSynchronize());
+  const uint32_t v = held ? 1u : 0u;
+  HIP_OK(hipMemcpy(h->d_lay_claim + b, &v, 4, hipMemcpyHostToDevice));
+  return 0;
+}
+
+int td_guard_timeouts(td_handle* h, int clear) {
+  if (!h) return fail("NULL handle");
+  uint32_t n = 0;
+  HIP_OK(hipDeviceSynchronize());
+  HIP_OK(hipMemcpy(&n, h->d_guard_to, 4, hipMemcpyDeviceToHost));
+  if (clear) HIP_OK(hipMemset(h->d_guard_to, 0, 4));
+  return (int)std::min<uint32_t>(n, 0x7fffffffu);
+}
+
+int td_set_store_policy(td_handle* h, int xcd_map, int edge_wt) {
+  if (!h || (xcd_map != 0 && xcd_map != 1) || (edge_wt != 1 && edge_wt != 2))
+    return fail("td_set_store_policy: xcd_map must be 0 / 1 and edge_wt 1 / 2");
+  HIP_OK(hipDeviceSynchronize());
+  h->xcd_map = xcd_map;
+  h->edge_wt = edge_wt;
+  return 0;
+}
+
 int td_board_map(int n_boards, int kind, int xcd_map, int32_t* out) {
   if (n_boards < 1 || !out || kind < 0 || kind > 1) return fail("td_board_map: bad arguments");
   for (int i = 0; i < n_boards; ++i)
-    out[i] = !xcd_map ? i : kind == 0 ? xcd_board(i, n_boards) : xcd_board_v(i, n_boards, 1);
+    out[i] = xcd_map ? xcd_board(i, n_boards) : i;
   return 0;
 }
 

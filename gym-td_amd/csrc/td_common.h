@@ -33,6 +33,7 @@ enum : int {
   FLAG_BAD_ACTION = 1 << 2,
   FLAG_NO_LAYOUT = 1 << 3,
   FLAG_BAD_MOVE = 1 << 4,
+  FLAG_CLAIM_TIMEOUT = 1 << 5,  // a wait for the board's refill claim gave up (1 s): its ring may run short
 };
 
 struct alignas(16) TdHdr {  // 96 bytes

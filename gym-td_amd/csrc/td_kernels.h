@@ -9,18 +9,10 @@ namespace td {
 
 // opponent hot record: [0] position, [1] lazy-twist boundary, [2] pre-drawn count,
 // [3] position of the first pre-drawn output, [4..4+HOT_CACHE) pre-drawn tempered outputs for
-// positions [3] .. [3]+count-1.  A step refills them (from its position on) only when fewer
-// than HOT_REFILL remain unused: the stream's words are then read once per refill instead of
-// once per step (TD_HOT_CACHE / TD_HOT_REFILL A/B builds).
-#ifndef TD_HOT_CACHE
-#define TD_HOT_CACHE 8
-#endif
-#ifndef TD_HOT_REFILL
-#define TD_HOT_REFILL TD_HOT_CACHE
-#endif
-constexpr int HOT_CACHE = TD_HOT_CACHE, HOT_REFILL = TD_HOT_REFILL;
+// positions [3] .. [3]+count-1.  The large kernel refills them (from its position on) only
+// when fewer than HOT_REFILL remain unused; the small kernels every step.
+constexpr int HOT_CACHE = 8, HOT_REFILL = 8;
 constexpr int HOT_WORDS = 4 + HOT_CACHE;
-static_assert(HOT_CACHE >= 8 && HOT_CACHE <= 32 && HOT_REFILL <= HOT_CACHE, "hot record");
 
 struct StepArgs {
   int B, L, mode, multi, difficulty, autoreset;
@@ -53,6 +45,7 @@ struct StepArgs {
   uint8_t* scratch;     // [B][scratch_stride] a pending layout draw: RoadResume header + generator arrays
   size_t scratch_stride;
   uint8_t* reset_fail;  // [B] reset kernel: road generation failed (board left unchanged)
+  uint32_t* guard_to;   // [1] ring-guard claim waits that gave up (td_guard_timeouts)
   const int32_t* ovr_idx;   // reset kernel, td_reset_layouts: [B] record index in ovr_rec, or -1
   const uint32_t* ovr_rec;  // caller-supplied layout records (layout_words(L) each)
   uint64_t* stamps;     // TD_STAMPS diagnostic builds only: [B][16] s_memtime per phase
@@ -76,66 +69,11 @@ struct StepArgs {
   double* ep_stats;  // [2]: finished episodes, sum of their returns (accumulated by the step kernel)
   td_episode_record* last_ep;  // [B]: each board's last finished episode (written on done)
   const uint8_t* reset_mask;  // reset kernel only (nullptr = all boards)
-  // Longest-work-first board order (small kernels, td_capi.hip): block i steps board
-  // ord_in[(i % 8) * ord_stride + i / 8] (nullptr: board i); each board then claims its slot
-  // in the next step's order -- boards with enemies first -- through ord_cnt (ORD_CHUNKS
-  // chunk counters per XCD, one 128-B line each: [0] heavy, [1] light).  ord_clr: the other
-  // parity's counters, zeroed by block 0 for the step after this one.
-  int xcd_map;   // large kernel: block i steps board xcd_board(i, B) (else board i)
-  int edge_wt;   // observation lines shared with a neighbouring board: 2 plain, 1 write-through, 0 non-temporal (write_obs_lines)
-  const uint32_t* ord_in;
-  uint32_t* ord_out;
-  uint32_t* ord_cnt;
-  uint32_t* ord_clr;
-  int ord_stride;
+  int xcd_map;   // block i steps board xcd_board(i, B) (else board i)
+  int edge_wt;   // observation lines shared with a neighbouring board: 2 plain, 1 write-through (write_obs_lines)
 };
 
-// Board order: 8 XCD lists (block i runs on XCD i % 8, slot i / 8 of its list), each split
-// into ORD_CHUNKS interleaved chunks (slot s in chunk s % ORD_CHUNKS) so no counter sees more
-// than B / 8 / ORD_CHUNKS returning atomics per step.
-constexpr int ORD_XCD = 8, ORD_CHUNKS = 16, ORD_LINE = 32;
-constexpr int ORD_CNT_WORDS = ORD_XCD * ORD_CHUNKS * ORD_LINE;  // per parity
-
-// Boards per workgroup of td_step_kernel_small (one wave each; TD_BPW A/B builds): a
-// one-round grid of B boards then has B / BPW workgroups to dispatch.  Board slots are
-// "virtual blocks" vb = workgroup * BPW + wave: XCD (vb / BPW) % 8, slot
-// (vb / BPW / 8) * BPW + vb % BPW of that XCD's list.
-// TD_ORDER_LARGE A/B builds: the large kernel follows the board order too.
-#ifndef TD_ORDER_LARGE
-#define TD_ORDER_LARGE 0
-#endif
-constexpr bool kOrderLarge = TD_ORDER_LARGE != 0;
-#ifndef TD_BPW
-#define TD_BPW 1
-#endif
-constexpr int kSmallBPW = TD_BPW;
-__host__ __device__ inline void ord_pos(int vb, int bpw, int& xcd, int& slot) {
-  const int blk = vb / bpw;
-  xcd = blk & (ORD_XCD - 1);
-  slot = (blk / ORD_XCD) * bpw + vb % bpw;
-}
-// Slots of XCD x's list: every workgroup on XCD x holds bpw boards but the grid's last one.
-__host__ __device__ inline int ord_nx(int x, int B, int bpw) {
-  const int nb = (B + bpw - 1) / bpw;
-  if (x >= nb) return 0;
-  const int nbx = (nb - 1 - x) / ORD_XCD + 1;
-  return nbx * bpw - (((nb - 1) & (ORD_XCD - 1)) == x ? nb * bpw - B : 0);
-}
-// Words per XCD list: the longest list (ord_nx), for either boards-per-workgroup count.
-__host__ __device__ inline int ord_stride(int B) {
-  const int nb = (B + kSmallBPW - 1) / kSmallBPW;
-  const int a = (nb + ORD_XCD - 1) / ORD_XCD * kSmallBPW, b1 = (B + ORD_XCD - 1) / ORD_XCD;
-  return a > b1 ? a : b1;
-}
-// The XCD-contiguous board of virtual block vb: XCD x's slots hold the boards after those
-// of XCDs 0 .. x-1 (for bpw = 1 the same map as xcd_board).
-__host__ __device__ inline int xcd_board_v(int vb, int B, int bpw) {
-  int x, slot;
-  ord_pos(vb, bpw, x, slot);
-  int pre = 0;
-  for (int y = 0; y < x; ++y) pre += ord_nx(y, B, bpw);
-  return pre + slot;
-}
+constexpr int NXCD = 8;  // XCDs of an MI355X: block i runs on XCD i % 8
 
 // The XCD-contiguous board map: block i (XCD i % 8, slot i / 8) steps board
 // prefix(i % 8) + i / 8, so XCD x steps the contiguous range of boards after those of
@@ -143,8 +81,8 @@ __host__ __device__ inline int xcd_board_v(int vb, int B, int bpw) {
 // arrays (header, hot record, reward, done, info) and the observation lines two boards
 // share are written whole by one XCD instead of in pieces by several.
 __host__ __device__ inline int xcd_board(int i, int B) {
-  const int x = i & (ORD_XCD - 1), q = B / ORD_XCD, r = B % ORD_XCD;
-  return x * q + (x < r ? x : r) + i / ORD_XCD;
+  const int x = i & (NXCD - 1), q = B / NXCD, r = B % NXCD;
+  return x * q + (x < r ? x : r) + i / NXCD;
 }
 
 

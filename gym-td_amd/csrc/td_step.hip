@@ -149,43 +149,8 @@ struct WaveMt {
   uint32_t* w;
   uint32_t pos, tw;
   uint32_t cache = 0, cbase = 0, cn = 0;  // lane j: tempered output for position cbase + j (j < cn)
-  // block_tw: at a block wrap the whole next block is twisted at once, in place (the large
-  // kernel): later draws and pre-draws of the block then read its words as they are --
-  // one line per pre-draw instead of three, and no partial-line stores of lazily twisted
-  // words every step.  Otherwise (the small kernels: latency-bound, where three dependent
-  // round trips in one wave would lengthen the grid's tail) words are twisted as drawn.
-  bool block_tw = false;
-
-  // CPython's twist of the whole block (w[0..624) -> the next block), by the wave in three
-  // dependent phases: new[i] needs old[i], old[i+1] and old[i+397] (i < 227) or new[i-227].
-  // The wave's own completed stores are visible to its later loads (vmcnt(0) between phases).
-  static __device__ __forceinline__ uint32_t twist1(uint32_t a, uint32_t b, uint32_t far) {
-    const uint32_t yy = (a & 0x80000000u) | (b & 0x7fffffffu);
-    return far ^ (yy >> 1) ^ ((yy & 1u) ? 0x9908b0dfu : 0u);
-  }
-  __device__ __forceinline__ void twist_block(int lane) {
-    constexpr int P0 = MT_N - MT_M, P1 = 2 * (MT_N - MT_M);  // 227, 454
-#pragma unroll
-    for (int ph = 0; ph < 3; ++ph) {
-      const int lo = ph == 0 ? 0 : ph == 1 ? P0 : P1, hi = ph == 0 ? P0 : ph == 1 ? P1 : MT_N;
-      uint32_t y[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {  // every load of the phase before any of its stores
-        const int i = lo + lane + 64 * k;
-        y[k] = 0u;
-        if (i < hi) y[k] = twist1(w[i], w[i == MT_N - 1 ? 0 : i + 1], w[ph == 0 ? i + MT_M : i - P0]);
-      }
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int i = lo + lane + 64 * k;
-        if (i < hi) w[i] = y[k];
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-  }
-  __device__ __forceinline__ void wrap(int lane) {
-    if (block_tw) { twist_block(lane); tw = MT_N; }
-    else tw = 0;
+  __device__ __forceinline__ void wrap() {
+    tw = 0;
     pos = 0;
   }
 
@@ -200,7 +165,7 @@ struct WaveMt {
   uint32_t pa = 0, pnb = 0, pfar = 0;
   bool plazy = false, pmine = false;
   __device__ __forceinline__ void prefetch_issue(int lane) {
-    if (pos >= (uint32_t)MT_N) wrap(lane);
+    if (pos >= (uint32_t)MT_N) wrap();
     cbase = pos;
     cn = (uint32_t)MT_N - pos < (uint32_t)HOT_CACHE ? (uint32_t)MT_N - pos : (uint32_t)HOT_CACHE;
     const uint32_t q = pos + (uint32_t)lane;
@@ -231,7 +196,7 @@ struct WaveMt {
     prefetch_finish(lane);
   }
 
-  // Early pre-draw (the small kernels, TD_EARLY_MT): the loads of the window [p0, p0 + 16)
+  // Early pre-draw (the small kernels): the loads of the window [p0, p0 + 16)
   // at the position p0 the step starts from are issued right after the hot record is in,
   // before any of the step's stores -- their wait at the step's end then neither waits on
   // the memory latency nor, through the in-order vmcnt, on the step's own stores.  The step
@@ -288,7 +253,7 @@ struct WaveMt {
       ++pos;
       return rdl(cache, (int)d);  // d is wave-uniform: a scalar read, no LDS round trip
     }
-    if (pos >= (uint32_t)MT_N) { wrap((int)(threadIdx.x & 63)); cn = 0; }
+    if (pos >= (uint32_t)MT_N) { wrap(); cn = 0; }
     uint32_t y;
     if (pos >= tw) {
       const uint32_t a = w[pos];
@@ -502,10 +467,7 @@ __device__ __forceinline__ bool scan_fold(Smem<NC>& S, int lane, int ncr, const 
     typedef long long i64x2 __attribute__((ext_vector_type(2)));
     const i64x2* A2 = reinterpret_cast<const i64x2*>(A);
     const int n2 = n / 2;
-#ifndef TD_SCAN_K
-#define TD_SCAN_K 8
-#endif
-    constexpr int K = TD_SCAN_K;  // 16-B loads in flight per lane
+    constexpr int K = 8;  // 16-B loads in flight per lane
     for (int base = 0; base < n2; base += 64 * K) {
       i64x2 v[K];
 #pragma unroll
@@ -561,12 +523,6 @@ __device__ __forceinline__ void scan_write_real(const Smem<NC>& S, int lane, int
   }
 }
 
-// Two-wave kernel, multi-action scan: the second wave folds the flags and writes the
-// real actions (TD_SCAN_SPLIT=0: the stepping wave does both, A/B builds).
-#ifndef TD_SCAN_SPLIT
-#define TD_SCAN_SPLIT 1
-#endif
-constexpr bool kScanSplit = TD_SCAN_SPLIT != 0;
 // FOLD: the flags are folded here (else by the second wave, `bad` its verdict); WRITE:
 // the real actions are written here (else by the second wave after barrier (A)).
 template <int NC, bool FOLD = true, bool WRITE = true>
@@ -1082,21 +1038,13 @@ __device__ __forceinline__ float obs_value(const Smem<NC>& S, int ch, int cell, 
 // Observation stores are non-temporal: 1.2 GB per launch written once and never
 // read back by the kernel; as plain stores the dirty lines fill the XCD L2s and
 // every state load behind them waits on a write-back (measured: 16 % slower).
-#ifdef TD_OBS_PLAIN  // A/B diagnostic builds only
-__device__ __forceinline__ void obs_store(f32x4* p, f32x4 v) { *p = v; }
-#else
 __device__ __forceinline__ void obs_store(f32x4* p, f32x4 v) { __builtin_nontemporal_store(v, p); }
-#endif
 // The two lines a board shares with its neighbours (written half by this wave, half
 // by a wave on another XCD) are stored write-through (sc1) instead: two non-temporal
 // partial writes of one line cost ~7 % of the whole stream (scripts/storepol.hip:
 // 234 us with nt partial lines, 218 us with sc1 ones = the whole-lines-only bound).
 __device__ __forceinline__ void obs_store_shared(__amdgpu_buffer_rsrc_t r, int off, f32x4 v) {
-#ifdef TD_OBS_SHARED_NT  // A/B diagnostic builds only
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, 2);
-#else
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, 16);  // aux 16 = sc1
-#endif
 }
 
 // The (45, L, L) float32 observation of one board.  The wave writes the batch's
@@ -1219,8 +1167,8 @@ struct ObsWinTab {
 // plain write-back stores -- with the XCD-contiguous board map (StepArgs::xcd_map) the
 // neighbours' waves run on this XCD and its L2 merges the two halves into one line write
 // (a pair split across two XCDs is written back byte-masked by both L2s); 1: write-through
-// (sc1); 0: non-temporal (partial lines straight to HBM: slow).  2 vs 1 at 65,536 boards:
-// 1.088x vs 1.093x the algorithmic bytes, step time +-0 (profiles/r04/s20).
+// (sc1).  2 vs 1 at 65,536 boards: 1.088x vs 1.093x the algorithmic bytes, step time +-0
+// (profiles/r04/s20); non-temporal partial lines measured 233 vs 212 us (r04/s4).
 template <int NC, int LT, int KB = 0, int KE = -1, int G = 4, int PASS = 0>
 __device__ __forceinline__ void write_obs_lines(const Smem<NC>& S, int lane, float* out, bool any_enemy, bool wt,
                                                 int edge_wt = 1) {
@@ -1243,9 +1191,6 @@ __device__ __forceinline__ void write_obs_lines(const Smem<NC>& S, int lane, flo
   // only a window at either end of the board holds lanes outside it (i < 0, i >= N4):
   // clamp there, so every lane reads LDS inside the board image
   auto unit = [&](int i, uint32_t wc) { return (wc & 4u) ? (i < 0 ? 0 : (i > N4 - 1 ? N4 - 1 : i)) : i; };
-#ifdef TD_OBS_NOUNROLL  // A/B builds: one copy of the G-window group (code size)
-#pragma nounroll
-#endif
   for (int k0 = KB; k0 < K; k0 += G) {
     uint4 A[G];
     uint32_t W[G];
@@ -1321,7 +1266,7 @@ __device__ __forceinline__ void write_obs_lines(const Smem<NC>& S, int lane, flo
       const uint32_t off = (uint32_t)i * 16u;  // i < 0 or i >= N4: out of range already
       if (wt) {  // wave-uniform
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, val), rs, off, 0, 16 /* sc1 */);
-      } else if (!edge || !edge_wt) {  // whole lines of this board only (or the neighbours share this L2)
+      } else if (!edge) {  // whole lines of this board only
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, val), rs, off, 0, 2 /* nt */);
       } else {
         const bool shared = i < head || i >= tail;  // a line shared with a neighbouring board
@@ -1351,10 +1296,7 @@ struct Prefetch {
 // arguments below).  The small-batch kernel (latency-bound) takes 16 of each up front;
 // the large-batch kernel (HBM-bound) takes none and loads exactly the live slots once
 // the header's counts are in (one dependent round trip, hidden by the other waves).
-#ifndef TD_LARGE_PF
-#define TD_LARGE_PF 0
-#endif
-constexpr int PF_ACT = 24, PF_HOT = 26, PF_SMALL = 16, PF_LARGE = TD_LARGE_PF;
+constexpr int PF_ACT = 24, PF_HOT = 26, PF_SMALL = 16, PF_LARGE = 0;
 static_assert(offsetof(TdHdr, steps) == 24 && offsetof(TdHdr, start_cell) == 56 && offsetof(TdHdr, episodes) == 76 &&
                   offsetof(TdHdr, max_cost) == 80 && offsetof(TdHdr, max_base_LP) == 88,
               "Prefetch header word map");
@@ -1512,7 +1454,7 @@ __device__ __forceinline__ void store_board(const Smem<NC>& S, const U& u, const
 // td_step_kernel_small2 the stepping wave hands them to the second wave in LDS, which
 // stores them (store_board, store_outputs) while the stepping wave computes the group
 // statistics and broadcast channels -- off the board's critical path.
-struct StepOut {
+struct alignas(16) StepOut {
   TdHdr hdr;           // the board's header after the step (6 lanes copy it out, 16 B each)
   int32_t nt, tw_dirty;
   double reward, ep_ret;
@@ -1565,9 +1507,6 @@ __device__ __forceinline__ void opponent_enemy(Smem<NC>& S, U& u, const Ctx& x, 
   uint32_t types = 0;
   int road;
   if (difficulty == 0) {
-#ifdef TD_OBS_NOUNROLL
-#pragma nounroll
-#endif
     for (int k = 0; k < 8; ++k) types |= (uint32_t)R.slot(4) << (4 * k);
     road = (int)R.ri(0, u.num_roads - 1);
   } else {
@@ -1722,8 +1661,7 @@ __device__ __forceinline__ void attacker_actions(Smem<NC>& S, U& u, const Ctx& x
 // layout and tower planes at the start of the step, before the step logic, was
 // measured slower at 4,096 and 8,192 boards: 36.3 / 53.1 vs 25.7 / 38.3 us.)
 // A board whose ring of staged layouts is empty at its episode end (td_step.hip below).
-template <int NC, bool SMALL>
-__device__ __forceinline__ bool take_dry_ring(const StepArgs& a, int b, uint32_t head, int lane);
+__device__ __forceinline__ bool take_dry_ring(const StepArgs& a, int b, uint32_t head, int* flags);
 
 // Observation windows written by the stepping wave of a two-wave board (the first half).
 template <int LT>
@@ -1744,48 +1682,12 @@ constexpr int obs_late_half() {
   return K;
 }
 
-// Longest-work-first board order (StepArgs::ord_*).  Block i of a small-kernel step runs
-// on XCD i % 8, slot i / 8 of that XCD's list; its board is ord_in[that slot].  A step
-// grid of one round of waves ends with its last wave, and the waves start over the grid's
-// ~8-us dispatch window in block order: boards with enemies (the longest steps: sort,
-// targeting, march, group statistics) are listed first, so they start at the window's
-// head instead of anywhere in it.  Each board claims its slot in the next step's list of
-// the same XCD (heavy from the front, light from the back of its chunk) with one
-// returning atomic, issued once its header is in and consumed phases later.
-__device__ __forceinline__ int ord_board(const StepArgs& a, int vb, int bpw) {
-  int xcd, slot;
-  ord_pos(vb, bpw, xcd, slot);
-  if (!a.ord_in) return !a.xcd_map ? vb : bpw == 1 ? xcd_board(vb, a.B) : xcd_board_v(vb, a.B, bpw);
-  return (int)a.ord_in[xcd * a.ord_stride + slot];
-}
-// Claim: heavy = the board has enemies now (its next step will: enemies live tens of steps).
-__device__ __forceinline__ uint32_t ord_claim(const StepArgs& a, bool heavy, int lane, int vb, int bpw) {
-  uint32_t r = 0;
-  if (!a.ord_in) return r;
-  int xcd, slot;
-  ord_pos(vb, bpw, xcd, slot);
-  if (lane == 0) r = atomicAdd(a.ord_cnt + (xcd * ORD_CHUNKS + slot % ORD_CHUNKS) * ORD_LINE + (heavy ? 0 : 1), 1u);
-  if (vb == 0)  // the other parity's counters start the step after this one at zero
-    for (int w = lane; w < ORD_XCD * ORD_CHUNKS; w += 64) { a.ord_clr[w * ORD_LINE] = 0u; a.ord_clr[w * ORD_LINE + 1] = 0u; }
-  return r;
-}
-__device__ __forceinline__ void ord_place(const StepArgs& a, int b, bool heavy, uint32_t r, int lane, int vb, int bpw) {
-  if (!a.ord_in || lane != 0) return;
-  int xcd, slot;
-  ord_pos(vb, bpw, xcd, slot);
-  const int c = slot % ORD_CHUNKS;
-  const int nx = ord_nx(xcd, a.B, bpw);                        // slots of this XCD's list
-  const int cs = (nx - c + ORD_CHUNKS - 1) / ORD_CHUNKS;       // of them in chunk c
-  const int pos = heavy ? (int)r : cs - 1 - (int)r;
-  a.ord_out[xcd * a.ord_stride + c + ORD_CHUNKS * pos] = (uint32_t)b;
-}
-
 // SPLIT: the board's workgroup has a second wave (td_step_kernel_small2) that waits at
 // the one workgroup barrier of this path and then writes the second half of the
 // observation windows.
-template <int NC, int LT, int MODE, bool SCAN, bool SMALL, bool SPLIT = false, int BPW = 1>
+template <int NC, int LT, int MODE, bool SCAN, bool SMALL, bool SPLIT = false>
 __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const StepArgs& a, int b, const Prefetch& P,
-                                           int vb, StepOut* so = nullptr) {
+                                           StepOut* so = nullptr) {
   const TdDevCfg& C = x.C;
   uint32_t* const opp = a.opp_mt + (size_t)b * OPP_WORDS;
   uint32_t* const hot = a.opp_hot + (size_t)b * HOT_WORDS;
@@ -1794,10 +1696,6 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
   STAMP(0);
   constexpr int PF = SMALL ? PF_SMALL : PF_LARGE;
   load_board<NC, PF, PF>(S, u, x, a, b, P);
-  const bool ord_heavy = u.n > 0;
-  // (the multi-action scan has no register to hold the claim across it: claimed at the place)
-  constexpr bool ORD = SMALL || kOrderLarge;
-  uint32_t ord_r = ORD && !SCAN ? ord_claim(a, ord_heavy, x.lane, vb, BPW) : 0u;
   const int64_t act_in = (int64_t)(((uint64_t)lane_word(P.w, PF_ACT + 1) << 32) | lane_word(P.w, PF_ACT));
   // built-in opponent stream: position, lazy-twist boundary and the next draws
   // (pre-computed by the previous step) come from the board's hot record
@@ -1805,10 +1703,7 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
   // The large kernel refills the pre-drawn outputs only when they run short (lazy); the
   // small kernels (no SGPR to spare at 8 waves per SIMD) refill every step and use a cache
   // only if it starts at the current position.
-#ifndef TD_LAZY_HOT_SMALL
-#define TD_LAZY_HOT_SMALL 0
-#endif
-  constexpr bool LAZY_HOT = !SMALL || TD_LAZY_HOT_SMALL;
+  constexpr bool LAZY_HOT = !SMALL;
   if constexpr (LAZY_HOT) {
     R.cn = lane_word(P.w, PF_HOT + 2);
     R.cbase = lane_word(P.w, PF_HOT + 3);
@@ -1817,27 +1712,13 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
     R.cbase = R.pos;
   }
   R.cache = __shfl(P.w, PF_HOT + 4 + (x.lane < HOT_CACHE ? x.lane : 0));
-#ifndef TD_BLOCK_TWIST
-#define TD_BLOCK_TWIST 0
-#endif
-  R.block_tw = !SMALL && TD_BLOCK_TWIST;
-#ifndef TD_EARLY_MT
-#define TD_EARLY_MT 1
-#endif
-#ifndef TD_EARLY_LARGE  // A/B builds: the early window in the large kernel too (a refill every step)
-#define TD_EARLY_LARGE 0
-#endif
-  constexpr bool EARLY_MT = (SMALL || TD_EARLY_LARGE) && !SCAN && MODE != MODE_2P && TD_EARLY_MT;
+  // (the early window in the large kernel too: +-0, reads +29 B per board, r04/s18)
+  constexpr bool EARLY_MT = SMALL && !SCAN && MODE != MODE_2P;
   if constexpr (EARLY_MT) R.early_issue(x.lane);
-  constexpr bool SCAN2 = SPLIT && SCAN && kScanSplit;
-#ifdef TD_START_PRIO
-  __builtin_amdgcn_s_setprio(0);
-#endif
+  constexpr bool SCAN2 = SPLIT && SCAN;
   STAMP(1);
   if (u.num_roads < 1 || u.num_roads > 3) {
     // never reset (its road generation failed): nothing to step
-    if constexpr (ORD && SCAN) ord_r = ord_claim(a, ord_heavy, x.lane, vb, BPW);
-    if constexpr (ORD) ord_place(a, b, ord_heavy, ord_r, x.lane, vb, BPW);
     const int nf = NCH * x.NCr;
     float* o = a.obs + (size_t)b * nf;
     for (int i = x.lane; i < nf; i += 64) o[i] = 0.0f;
@@ -1908,14 +1789,6 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
       with_opp_rng(a, b, x.lane, R, [&](auto& G) { opponent_tower(S, u, x, G, a.difficulty); });
   }
   STAMP(12);
-#ifndef TD_EARLY_AT  // 0: consumed after board_step (8,192: 32.6-32.7 vs 33.2-33.3 us at 1, r04/s13)
-#define TD_EARLY_AT 0
-#endif
-  // (early pre-draw: the step's draws are done -- the window's words are consumed here,
-  // before the step's first state store, and only the pre-drawn outputs live on)
-  if constexpr (EARLY_MT && TD_EARLY_AT == 1) R.early_finish(x.lane);
-  if constexpr (ORD && SCAN) ord_r = ord_claim(a, ord_heavy, x.lane, vb, BPW);
-  if constexpr (ORD) ord_place(a, b, ord_heavy, ord_r, x.lane, vb, BPW);
   // the towers and map[6] are final: cell words back to HBM if they changed, then
   // packed for the rest of the step (board_step reads the packed direction and distance)
   store_cells(S, u, x, a, b);
@@ -1945,8 +1818,9 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
   // acknowledgement (s_waitcnt vmcnt(0)).  (Holding every state store back to the end
   // of the step, next to the observation, measured slower: 219 vs 216 us at 65,536
   // boards, 35.8 vs 34.9 at 8,192, profiles/r03/s16.)
+  // (consumed here rather than before the board step: 8,192 boards 32.6-32.7 vs 33.2-33.3 us, r04/s13)
   if constexpr (EARLY_MT) {
-    if constexpr (TD_EARLY_AT == 0) R.early_finish(x.lane);
+    R.early_finish(x.lane);
   } else if (!SCAN && refill) R.prefetch_finish(x.lane);
   if (MODE == MODE_ATK) reward = -reward;                   // TDAttack.py:50
   const bool done = (u.base_LP <= 0) || (u.steps >= C.max_episode_steps);  // :384-385
@@ -1977,7 +1851,7 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
     const uint32_t want = slot_tag(lay_head);
     bool ready = ld_relaxed(rec) == want;
     // a dry ring: wait for the refill drawing this layout, or draw it now
-    if (!ready) ready = take_dry_ring<NC, SMALL>(a, b, lay_head, x.lane);
+    if (!ready) ready = take_dry_ring(a, b, lay_head, &u.flags);
     if (ready) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       reset_board(S, u, x, rec);
@@ -2043,9 +1917,7 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
     STAMP(6);
     if constexpr (LT != 0) {
       if ((reinterpret_cast<uintptr_t>(a.obs) & 15u) == 0) {
-#ifndef TD_DIAG_NO_OBS  // diagnostic builds only: the step without its observation
         write_obs_lines<NC, LT>(S, x.lane, obs, u.n > 0, wt, a.edge_wt);
-#endif
       } else {
         write_obs<NC, LT>(S, x, obs, u.n > 0);
       }
@@ -2067,12 +1939,8 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
 // to 83 SGPRs, ran 8 waves per SIMD and lost 4.6 % at 65,536 boards).  The StepArgs must
 // be the kernel's first argument (kernarg offset 0).
 __device__ __forceinline__ const StepArgs& kargs(const StepArgs& a) {
-#ifdef TD_KARG_BYVAL  // A/B builds: the by-value argument as the compiler keeps it
-  return a;
-#else
   (void)a;
   return *(const StepArgs*)__builtin_amdgcn_kernarg_segment_ptr();  // (C cast: leaves the constant address space)
-#endif
 }
 
 // One workgroup (one wave) per board.  (A persistent variant that prefetched the
@@ -2081,43 +1949,23 @@ __device__ __forceinline__ const StepArgs& kargs(const StepArgs& a) {
 template <int LT, int MODE, bool SCAN, bool SMALL>
 __device__ __forceinline__ void step_kernel_body(const StepArgs& a) {
   constexpr int NC = LT ? LT * LT : MAX_KERNEL_L * MAX_KERNEL_L;
-  constexpr int BPW = SMALL ? kSmallBPW : 1;  // boards (waves) per workgroup
-  __shared__ Smem<NC> SS[BPW];
-  const int w = BPW > 1 ? (int)(threadIdx.x >> 6) : 0;
-  const int vb = (int)blockIdx.x * BPW + w;  // the board slot of this wave
-  if (vb >= a.B) return;
-  Smem<NC>& S = SS[w];
-  const int b = SMALL || kOrderLarge ? ord_board(a, vb, BPW) : a.xcd_map ? xcd_board(vb, a.B) : vb;
-#ifdef TD_STEP_PRIO  // A/B builds: step waves ahead of concurrent refill waves in issue arbitration
-  __builtin_amdgcn_s_setprio(TD_STEP_PRIO);
-#endif
-#ifdef TD_START_PRIO  // A/B builds: a starting wave ahead of the resident ones until its board is in
-  __builtin_amdgcn_s_setprio(TD_START_PRIO);
-#endif
+  __shared__ Smem<NC> S;
+  const int i = (int)blockIdx.x;
+  if (i >= a.B) return;
+  const int b = a.xcd_map ? xcd_board(i, a.B) : i;
   stage_cfg(S, a.cfg);
   const int L = LT ? LT : a.L;
   const Ctx x{S.cfg, L, L * L, (int)(threadIdx.x & 63), a.cfgs, a.epoch};
   Prefetch P;
   constexpr int PF = SMALL ? PF_SMALL : PF_LARGE;
   prefetch_issue<PF, PF>(P, a, b, x.lane, x.NCr, MODE != MODE_ATK && !a.multi);
-  step_board<NC, LT, MODE, SCAN, SMALL, false, BPW>(S, x, a, b, P, vb);
+  step_board<NC, LT, MODE, SCAN, SMALL>(S, x, a, b, P);
 }
 
 // Large batches (several rounds of waves, HBM-write bound): 6 waves per SIMD at
 // L = 10 (106 SGPRs), no register pressure beyond the step's own.
-template <int LT>
-constexpr int large_waves() { return LT == 10 ? 7 : LT == 20 ? 5 : 3; }  // LDS-bound residency per SIMD
-#ifdef TD_DRY_DRAW
-#define TD_LARGE_ATTR __attribute__((amdgpu_waves_per_eu(large_waves<LT>())))
-#else
-#define TD_LARGE_ATTR
-#endif
-#if defined(TD_SCAN_WAVES) && !defined(TD_DRY_DRAW)  // A/B builds: residency of the multi-action kernels
-#undef TD_LARGE_ATTR
-#define TD_LARGE_ATTR __attribute__((amdgpu_waves_per_eu(SCAN ? TD_SCAN_WAVES : 1)))
-#endif
 template <int LT, int MODE, bool SCAN>
-__global__ __launch_bounds__(64) TD_LARGE_ATTR void td_step_kernel(StepArgs a) {
+__global__ __launch_bounds__(64) void td_step_kernel(StepArgs a) {
   step_kernel_body<LT, MODE, SCAN, false>(a);  // by value (see kargs)
 }
 
@@ -2126,29 +1974,15 @@ __global__ __launch_bounds__(64) TD_LARGE_ATTR void td_step_kernel(StepArgs a) {
 // limit for 8 resident waves (MI355X_MICROARCH.md, residency), so 8,192 boards -- 8
 // GPUs' share of BASELINE's 65,536 -- run as ONE round instead of 6,144 + 2,048.  At
 // 65,536 boards the same build is 7 % slower (SGPR spill code), hence two kernels.
-// (TD_DRY_DRAW A/B builds: per-L residency, which bounds the registers of the dry-ring
-// draw the kernels then call -- see take_dry_ring.)
-template <int LT>
-constexpr int small_waves() { return LT == 10 ? 8 : LT == 20 ? 5 : 3; }
-template <int LT>
-constexpr int small2_waves() { return LT == 30 ? 6 : 8; }
-#ifndef TD_SCAN2_CAP  // A/B builds: residency of the 20x20 two-wave multi-action kernel
-#define TD_SCAN2_CAP 5
-#endif
-template <int LT, int MODE, bool SCAN>
-constexpr int small2_cap() { return LT == 20 && SCAN ? TD_SCAN2_CAP : LT == 20 && MODE == MODE_ATK ? 6 : 8; }
-#ifdef TD_DRY_DRAW
-#define TD_SMALL_ATTR __attribute__((amdgpu_waves_per_eu(small_waves<LT>(), small_waves<LT>())))
-#define TD_SMALL2_ATTR __attribute__((amdgpu_waves_per_eu(small2_waves<LT>(), small2_waves<LT>())))
-#else
-#define TD_SMALL_ATTR __attribute__((amdgpu_waves_per_eu(8, 8)))
 // The two-wave 20x20 kernels of the multi-action scan and of TD-atk do not fit 64 VGPRs:
 // at 8 waves per SIMD they spilled (112-116 / 8 B of scratch per lane; the scan still
 // spilled at 6), so 5 / 6.
-#define TD_SMALL2_ATTR __attribute__((amdgpu_waves_per_eu(small2_cap<LT, MODE, SCAN>(), small2_cap<LT, MODE, SCAN>())))
-#endif
 template <int LT, int MODE, bool SCAN>
-__global__ __launch_bounds__(64 * kSmallBPW) TD_SMALL_ATTR void td_step_kernel_small(StepArgs a) {
+constexpr int small2_cap() { return LT == 20 && SCAN ? 5 : LT == 20 && MODE == MODE_ATK ? 6 : 8; }
+#define TD_SMALL_ATTR __attribute__((amdgpu_waves_per_eu(8, 8)))
+#define TD_SMALL2_ATTR __attribute__((amdgpu_waves_per_eu(small2_cap<LT, MODE, SCAN>(), small2_cap<LT, MODE, SCAN>())))
+template <int LT, int MODE, bool SCAN>
+__global__ __launch_bounds__(64) TD_SMALL_ATTR void td_step_kernel_small(StepArgs a) {
   step_kernel_body<LT, MODE, SCAN, true>(kargs(a));
 }
 
@@ -2163,20 +1997,17 @@ __global__ __launch_bounds__(128) TD_SMALL2_ATTR void td_step_kernel_small2(Step
   __shared__ Smem<NC> S;
   __shared__ StepOut SO;
   if ((int)blockIdx.x >= a.B) return;
-  const int b = ord_board(a, (int)blockIdx.x, 1);
+  const int b = a.xcd_map ? xcd_board((int)blockIdx.x, a.B) : (int)blockIdx.x;
   const int lane = (int)threadIdx.x & 63;
-#ifdef TD_START_PRIO
-  __builtin_amdgcn_s_setprio(TD_START_PRIO);
-#endif
   if (threadIdx.x < 64) {
     stage_cfg(S, a.cfg);
     const Ctx x{S.cfg, LT, NC, lane, a.cfgs, a.epoch};
     Prefetch P;
     prefetch_issue<PF_SMALL, PF_SMALL>(P, a, b, lane, NC, MODE != MODE_ATK && !a.multi);
-    step_board<NC, LT, MODE, SCAN, true, true>(S, x, a, b, P, (int)blockIdx.x, &SO);
+    step_board<NC, LT, MODE, SCAN, true, true>(S, x, a, b, P, &SO);
   } else {
     float* const obs = a.obs + (size_t)b * NCH * NC;
-    constexpr bool SCAN2 = SCAN && kScanSplit;
+    constexpr bool SCAN2 = SCAN;
     if constexpr (SCAN2) {  // the multi-action flags, folded while the first wave loads the board
       const bool bad = scan_fold(S, lane, NC, a.def_act + (size_t)b * 6 * NC);
       if (lane == 0) SO.scan_bad = bad ? 1u : 0u;
@@ -2194,7 +2025,8 @@ __global__ __launch_bounds__(128) TD_SMALL2_ATTR void td_step_kernel_small2(Step
     __syncthreads();  // (B) the board after the step and its outputs are in SO
     const uint32_t go = SO.go;
     if (go) {
-      static_assert(sizeof(TdHdr) == 6 * 16 && offsetof(StepOut, hdr) == 0, "header copied as 6 x 16 B");
+      static_assert(sizeof(TdHdr) == 6 * 16 && offsetof(StepOut, hdr) == 0 && alignof(StepOut) >= 16,
+                    "header copied as 6 x 16-B LDS reads");
       if (lane < 6) reinterpret_cast<uint4*>(a.hdr + b)[lane] = reinterpret_cast<const uint4*>(&SO.hdr)[lane];
       store_towers(S, SO.nt, SO.tw_dirty != 0, lane, a, b);
       store_outputs(a, b, SO, lane);
@@ -2287,7 +2119,7 @@ __device__ __forceinline__ RoadResume* resume_hdr(const StepArgs& a, int b) {
 // stream: plain stores, every lane's vmcnt(0), the barrier, ONE agent-scope
 // release, then the tag by an sc1 store (MI355X_MICROARCH.md § visibility, "Valid
 // forms", producer bullet).  Returns the road status of the last draw.
-template <int NC, bool SB = false, bool SBP = false>
+template <int NC, bool SBP = false>
 __device__ int wave_layout(LayoutSmem<NC>& G, const StepArgs& a, int b, int retries, uint32_t* slot, uint32_t n,
                            int budget) {
   const int lane = (int)threadIdx.x, L = a.L, lw = LAYOUT_HDR + L * L;
@@ -2312,7 +2144,7 @@ __device__ int wave_layout(LayoutSmem<NC>& G, const StepArgs& a, int b, int retr
   }
   int st = ROAD_ERR_BOUND;
   {
-    WaveRoadGen<NC, false, SB, SBP> g;
+    WaveRoadGen<NC, SBP> g;
     g.carve(G.scratch, L * L);
     g.mt = G.mt; g.rec = G.rec; g.L = L; g.lane = lane;
     // the stream position and the resume state are wave-uniform: SGPRs
@@ -2354,80 +2186,24 @@ __device__ int wave_layout(LayoutSmem<NC>& G, const StepArgs& a, int b, int retr
   return st;
 }
 
-// TDGymBasic.reset's draws (:42-51) for board b as layout number n of its stream, run by
-// the step wave that found the board's ring empty at its episode end (TD_DRY_DRAW A/B
-// builds, see take_dry_ring): the same draws as
-// wave_layout (a pending draw continues; failing draws skipped up to kLayoutRetries
-// times; no walk budget), by the whole wave but in place in global memory -- the
-// stream in np_mt, the record in the ring slot, the generator's arrays in the board's
-// scratch -- since the step's LDS holds the board image (and a second wave may share
-// the workgroup: wave-level syncs only).  Not inlined: the generator's registers would
-// cost the step kernels occupancy on every step; as a call its spills stay inside
-// this rarely run function.  The caller holds the board's claim.
-template <int NC, bool SMALL>
-__device__ __attribute__((noinline)) int draw_in_place(const StepArgs& a, int b, uint32_t* slot, uint32_t n) {
-  const int lane = (int)(threadIdx.x & 63), L = a.L;
-  uint32_t* gmt = a.np_mt + (size_t)b * OPP_WORDS;
-  uint32_t* ghdr = reinterpret_cast<uint32_t*>(resume_hdr(a, b));
-  static_assert(sizeof(RoadResume) == 64, "resume header: 16 words");
-  WaveRoadGen<NC, true> g;
-  g.carve(a.scratch + (size_t)b * a.scratch_stride + sizeof(RoadResume), L * L);
-  g.mt = gmt; g.rec = slot; g.L = L; g.lane = lane;
-  g.pos = __builtin_amdgcn_readfirstlane(gmt[MT_N]);
-  g.tw = __builtin_amdgcn_readfirstlane(gmt[MT_N + 1]);
-  g.base = g.pos; g.n = 0; g.win = 0;
-  const uint32_t hw = lane < 16 ? ghdr[lane] : 0u;
-  RoadResume res;
-  for (int i = 0; i < 16; ++i) reinterpret_cast<uint32_t*>(&res)[i] = rdl(hw, i);
-  g.load_maps(res.phase != RP_NEW);  // the bitmaps of the draw a refill left pending (its partial record is in the slot)
-  const int st = g.draw(res, 0x7fffffff, kRoadAttempts, kLayoutRetries);
-  g.sync();
-  if (lane == 0) { gmt[MT_N] = g.pos; gmt[MT_N + 1] = g.tw; }
-  if (lane < 16) ghdr[lane] = reinterpret_cast<const uint32_t*>(&res)[lane];  // phase RP_NEW: nothing pending
-  if (st == ROAD_OK) {
-    g.sync();
-    if (lane == 0) slot[0] = slot_tag(n);
-  }
-  g.sync();
-  return st;
-}
-
 // The step wave of board b found layout `head` unpublished at the episode end.  If a
 // refill wave holds the board's claim it is drawing exactly this layout (an empty ring
-// is urgent: its draw runs to the end): wait for the tag, bounded.  Otherwise the ring
-// ran dry with no refill beside the step: the board is flagged no_layout (product).
-// TD_DRY_DRAW A/B builds claim the board instead and draw the layout now
-// (draw_in_place), so an episode end never depends on the refill cadence; the plain
-// stores of the draw are published by one release fence before the claim is given
-// back.  Measured (profiles/r03/s4): bit-exact (the refill-interval-0 auto-reset tests
-// pass on all three step kernels), but the called draw spills (0.5-1 KB of scratch per
-// lane in every step kernel) and every step ran 4.5x slower (65,536 boards: 1,018 vs
-// 223 us; 8,192: 163 vs 36 us) -- inlined, it costs the kernels their occupancy.
-// True when layout `head` is ready in its slot.
-template <int NC, bool SMALL>
-__device__ __forceinline__ bool take_dry_ring(const StepArgs& a, int b, uint32_t head, int lane) {
+// is urgent: its draw runs to the end): wait for the tag, bounded (1 s; a wait that gives
+// up sets FLAG_CLAIM_TIMEOUT in *flags).  Otherwise the ring ran dry with no refill beside
+// the step: the board is flagged no_layout by the caller.  (The step wave drawing the
+// layout itself measured 4.5x slower steps: the called draw spills 0.5-1 KB of scratch
+// per lane in every step kernel, profiles/r03/s4.)  True when layout `head` is ready.
+__device__ __forceinline__ bool take_dry_ring(const StepArgs& a, int b, uint32_t head, int* flags) {
   uint32_t* const slot = a.nxt + ((size_t)b * NSLOT + head % NSLOT) * a.slot_words;
   const uint32_t want = slot_tag(head);
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   for (;;) {
-#ifndef TD_DRY_DRAW  // product: no claim holder -- the board is flagged no_layout
     if (ld_relaxed(a.lay_claim + b) == 0u) return ld_relaxed(slot) == want;
-#else
-    if (claim_board(a.lay_claim + b, lane)) {
-      bool ok = ld_relaxed(slot) == want;  // published before the claim was taken
-      if (!ok && ld_relaxed(a.lay_tail + b) == head) {
-        ok = draw_in_place<NC, SMALL>(a, b, slot, head) == ROAD_OK;
-        if (ok && lane == 0) st_relaxed(a.lay_tail + b, head + 1u);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      }
-      __builtin_amdgcn_wave_barrier();
-      if (lane == 0) st_relaxed(a.lay_claim + b, 0u);
-      return ok;
-    }
-#endif
     if (ld_relaxed(slot) == want) return true;
-    if (__builtin_amdgcn_s_memrealtime() - t0 >= kTakeSpinTicks) return false;
+    if (__builtin_amdgcn_s_memrealtime() - t0 >= kTakeSpinTicks) {
+      *flags |= FLAG_CLAIM_TIMEOUT;
+      return false;
+    }
     __builtin_amdgcn_s_sleep(64);
   }
 }
@@ -2585,7 +2361,13 @@ __global__ __launch_bounds__(64) void td_refill_kernel(StepArgs a, int guard) {
           __builtin_amdgcn_s_sleep(8);
           got = claim_board(a.lay_claim + bb, lane);
         }
-        if (!got) continue;
+        if (!got) {  // visible: the board's flag and the engine's counter (td_guard_timeouts)
+          if (lane == 0) {
+            atomicOr(&a.hdr[bb].flags, FLAG_CLAIM_TIMEOUT);
+            if (a.guard_to) atomicAdd(a.guard_to, 1u);
+          }
+          continue;
+        }
       }
       uint32_t t = __builtin_amdgcn_readfirstlane(ld_relaxed(a.lay_tail + bb));  // (wave-uniform: SGPRs)
       const uint32_t h = __builtin_amdgcn_readfirstlane(ld_relaxed(a.lay_head + bb));
@@ -2594,7 +2376,7 @@ __global__ __launch_bounds__(64) void td_refill_kernel(StepArgs a, int guard) {
         uint32_t* slot = a.nxt + ((size_t)bb * NSLOT + t % NSLOT) * a.slot_words;
         // an empty ring is urgent (the board needs this layout at its next episode end):
         // its draw runs to the end; otherwise at most a.refill_walks walks this launch
-        const int st = wave_layout<NC, kGenSB && NC <= 128, kGenSBProof && NC <= 128>(
+        const int st = wave_layout<NC, kGenSBProof && NC <= 128>(
             G, a, bb, kLayoutRetries, slot, t, t == h || guard ? 0x7fffffff : a.refill_walks);
         __syncthreads();
         if (st != ROAD_OK) break;  // out of walks (continued next launch), or 65 failing draws in a row
@@ -2631,25 +2413,18 @@ static hipError_t launch2(const StepArgs& a, hipStream_t s, bool reset, hipEvent
     if (ev0) hipExtLaunchKernelGGL(k, dim3(a.B), dim3(128), 0, s, ev0, ev1, 0, a);       \
     else hipLaunchKernelGGL(k, dim3(a.B), dim3(128), 0, s, a);                           \
   } while (0)
-#define TD_LAUNCHS(k)                                                                                      \
-  do {                                                                                                     \
-    const dim3 g((a.B + kSmallBPW - 1) / kSmallBPW), t(64 * kSmallBPW);                                    \
-    if (ev0) hipExtLaunchKernelGGL(k, g, t, 0, s, ev0, ev1, 0, a);                                         \
-    else hipLaunchKernelGGL(k, g, t, 0, s, a);                                                             \
-  } while (0)
   const bool aligned = (reinterpret_cast<uintptr_t>(a.obs) & 15u) == 0;
   if (reset) {
     hipLaunchKernelGGL(td_reset_kernel<LT>, dim3(a.B), dim3(64), 0, s, a);
   } else if constexpr (LT != 0) {
     if (a.small == 2 && aligned) TD_STEP_DISPATCH(td_step_kernel_small2, LT, a, TD_LAUNCH2);
-    else if (a.small && aligned) TD_STEP_DISPATCH(td_step_kernel_small, LT, a, TD_LAUNCHS);
+    else if (a.small && aligned) TD_STEP_DISPATCH(td_step_kernel_small, LT, a, TD_LAUNCH);
     else TD_STEP_DISPATCH(td_step_kernel, LT, a, TD_LAUNCH);
   } else {
     TD_STEP_DISPATCH(td_step_kernel, LT, a, TD_LAUNCH);
   }
 #undef TD_LAUNCH
 #undef TD_LAUNCH2
-#undef TD_LAUNCHS
   return hipGetLastError();
 }
 
@@ -2659,13 +2434,13 @@ template <int LT>
 static int resident3(const StepArgs& a, int cus, int waves) {
   int n = 0;
   hipError_t e = hipErrorInvalidValue;
-#define TD_OCC(k) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, 64 * kSmallBPW, 0)
+#define TD_OCC(k) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, 64, 0)
 #define TD_OCC2(k) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, 128, 0)
   if (waves == 2) TD_STEP_DISPATCH(td_step_kernel_small2, LT, a, TD_OCC2);
   else TD_STEP_DISPATCH(td_step_kernel_small, LT, a, TD_OCC);
 #undef TD_OCC
 #undef TD_OCC2
-  return e == hipSuccess ? n * cus * (waves == 2 ? 1 : kSmallBPW) : 0;
+  return e == hipSuccess ? n * cus : 0;
 }
 
 int step_resident_boards(const StepArgs& a, int cus, int waves) {

@@ -6,8 +6,6 @@
 
 #include "td_kernels.h"
 
-#include <type_traits>
-
 namespace td {
 
 // ---------------------------------------------------------------------------
@@ -62,38 +60,20 @@ __device__ __forceinline__ void release_board(uint32_t* claim, int lane) {
   if (lane == 0) st_relaxed(claim, 0u);
 }
 
-// Per-board state and output stores.  TD_SST selects the cache policy (A/B builds):
-// 0 plain, 1 non-temporal, 2 write-through (sc1).  Plain is the product: these arrays
-// hold a few bytes per board, so a line is shared by boards on several XCDs and the
-// XCD L2s merge the plain stores; 65,536 boards at L = 10 measured 224 us plain,
-// 227 us sc1 and 287 us non-temporal (partial-line writes to HBM).
-#ifndef TD_SST
-#define TD_SST 0
-#endif
+// Per-board state and output stores: plain stores.  These arrays hold a few bytes per
+// board, so a line is shared by neighbouring boards and the XCD L2 merges the plain
+// stores; 65,536 boards at L = 10 measured 224 us plain, 227 us write-through and 287 us
+// non-temporal (partial-line writes to HBM, round 1).
 template <class T>
-__device__ __forceinline__ void sst(T* p, T v) {
-  if constexpr (TD_SST == 1) {
-    __builtin_nontemporal_store(v, p);
-  } else if constexpr (TD_SST == 2) {
-    using W = std::conditional_t<sizeof(T) == 8, uint64_t,
-              std::conditional_t<sizeof(T) == 4, uint32_t, std::conditional_t<sizeof(T) == 2, uint16_t, uint8_t>>>;
-    __hip_atomic_store(reinterpret_cast<W*>(p), __builtin_bit_cast(W, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  } else {
-    *p = v;
-  }
-}
+__device__ __forceinline__ void sst(T* p, T v) { *p = v; }
 
 // The step of one board runs in one wave: its LDS hand-offs between lanes need the
 // wave's LDS operations drained and the compiler kept from moving memory accesses
 // across, not a workgroup barrier -- so the small-batch kernel can give a board a
 // second wave that waits at one real barrier for the observation (td_step_kernel_small2).
 __device__ __forceinline__ void wsync() {
-#ifdef TD_WSYNC_BARRIER  // A/B builds: a workgroup barrier (one-wave workgroups only)
-  __syncthreads();
-#else
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_wave_barrier();
-#endif
 }
 
 }  // namespace td

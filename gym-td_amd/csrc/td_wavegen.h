@@ -30,33 +30,17 @@ struct LayoutSmem {
 // v_readlane.  Control flow is wave-uniform.  The road lists stay in LDS (the resumable
 // state); the main road, its branch points and the stamping of a road onto the record
 // run one cell per lane (an accepted road is shorter than 2L <= 64 cells).
-// SB: boards of at most 128 cells (L <= 11) keep both bitmaps as two wave-uniform 64-bit
-// words each (bit c of word c / 64): a walk step's test and set, the erase and the
-// branch-point scan are scalar bit operations, and the hopeless-branch search shifts a
-// 128-bit frontier instead of exchanging lane words.  Measured per draw (r04/s11,
-// probe_draw_parts, 1,024 boards at L = 10): the search 17.5 k -> 3.7 k cycles, but a
-// walk 6.8 k -> 7.3 k (64-bit maps held in VGPRs: the refill kernel has no SGPRs to spare),
-// 76.9 k -> 66.5 k per draw.  So the product keeps lane-word bitmaps for the walks and
-// runs only the search on scalar words (SBP, kGenSBProof); TD_GEN_SB=1 builds use SB for
-// all.  Both in the refill kernel only: the reset kernels have no registers to spare.
-#ifndef TD_GEN_SB
-#define TD_GEN_SB 0
-#endif
-constexpr bool kGenSB = TD_GEN_SB != 0;
-// The hopeless-branch search on scalar words at L <= 11 whatever form the bitmaps have
-// (TD_GEN_SB_PROOF=0: lane words, A/B builds).
-#ifndef TD_GEN_SB_PROOF
-#define TD_GEN_SB_PROOF 1
-#endif
-constexpr bool kGenSBProof = TD_GEN_SB_PROOF != 0;
-template <int NC, bool GM = false, bool SB = false, bool SBP = false>  // SBP: the search on scalar words
+// At L <= 11 (at most 128 cells) the hopeless-branch search runs on the field as two
+// wave-uniform 64-bit words (SBP): a 128-bit frontier is shifted instead of lane words
+// exchanged -- 17.5 k -> 3.7 k cycles per search (r04/s11, probe_draw_parts, 1,024 boards
+// at L = 10).  The walks keep the lane-word bitmaps (as scalar words they were slower:
+// 6.8 k -> 7.3 k cycles per walk, the refill kernel has no SGPRs to spare).  The refill
+// kernel only: the reset kernels have no registers to spare.
+constexpr bool kGenSBProof = true;
+template <int NC, bool SBP = false>  // SBP: the search on scalar words
 struct WaveRoadGen {
-  // GM: the stream, the record and the scratch arrays are in global memory, not LDS
-  // (td_step.hip draw_in_place): a hand-off between lanes then also waits for the
-  // wave's vector memory operations (a CU's own completed stores are visible to its loads).
   static __device__ __forceinline__ void sync() {
-    if constexpr (GM) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
   }
   static constexpr int NW = (NC + 31) / 32;  // bitmap words (at most)
@@ -67,8 +51,7 @@ struct WaveRoadGen {
   uint32_t *fieldw, *rotw;  // the bitmaps' resumable copies in the scratch
   int L, lane;
   uint32_t pos, tw, base, n, win;
-  uint32_t field, rot;          // lane-word form: lane j holds cells [32j, 32j + 32)
-  uint64_t fs0, fs1, rs0, rs1;  // SB form: cells [0, 64) and [64, 128)
+  uint32_t field, rot;  // lane j holds cells [32j, 32j + 32)
 #ifdef TD_GEN_STAMPS  // diagnostic builds: s_memtime cycles by part of the draw (scripts/probe_draw.py)
   uint64_t cyc[6] = {0, 0, 0, 0, 0, 0};  // walk, proof, stamp, erase, stream window, walks
 #define GEN_T0() const uint64_t gen_t0_ = __builtin_amdgcn_s_memtime()
@@ -91,7 +74,6 @@ struct WaveRoadGen {
   // ---- the numpy-legacy stream (LazyMt semantics, 64 words per refill) ----
   __device__ void refill() {
     GEN_T0();
-    if constexpr (GM) sync();  // the previous window's twisted words are stored
     if (pos >= (uint32_t)MT_N) { pos = 0; tw = 0; }
     base = pos;
     n = (uint32_t)MT_N - pos < 64u ? (uint32_t)MT_N - pos : 64u;
@@ -138,52 +120,20 @@ struct WaveRoadGen {
   __device__ __forceinline__ uint32_t without(uint32_t m, int c) const {
     return m & ~(lane == (c >> 5) ? 1u << (c & 31) : 0u);
   }
-  static __device__ __forceinline__ bool sbit(uint64_t w0, uint64_t w1, int c) {
-    return (((c < 64 ? w0 : w1) >> (c & 63)) & 1ull) != 0;
-  }
-  static __device__ __forceinline__ void sset(uint64_t& w0, uint64_t& w1, int c) {
-    if (c < 64) w0 |= 1ull << c; else w1 |= 1ull << (c - 64);
-  }
-  static __device__ __forceinline__ void sclr(uint64_t& w0, uint64_t& w1, int c) {
-    if (c < 64) w0 &= ~(1ull << c); else w1 &= ~(1ull << (c - 64));
-  }
-  __device__ __forceinline__ bool fbit(int c) const { if constexpr (SB) return sbit(fs0, fs1, c); else return bit(field, c); }
-  __device__ __forceinline__ bool rbit(int c) const { if constexpr (SB) return sbit(rs0, rs1, c); else return bit(rot, c); }
-  __device__ __forceinline__ void fset(int c) { if constexpr (SB) sset(fs0, fs1, c); else field = with(field, c); }
-  __device__ __forceinline__ void rset(int c) { if constexpr (SB) sset(rs0, rs1, c); else rot = with(rot, c); }
-  __device__ __forceinline__ void clear_maps() {
-    if constexpr (SB) fs0 = fs1 = rs0 = rs1 = 0ull;
-    else field = rot = 0u;
-  }
+  __device__ __forceinline__ bool fbit(int c) const { return bit(field, c); }
+  __device__ __forceinline__ bool rbit(int c) const { return bit(rot, c); }
+  __device__ __forceinline__ void fset(int c) { field = with(field, c); }
+  __device__ __forceinline__ void rset(int c) { rot = with(rot, c); }
+  __device__ __forceinline__ void clear_maps() { field = rot = 0u; }
   // The bitmaps from / to their resumable copies (fieldw / rotw: u32 word i = cells [32i, 32i + 32)).
   __device__ __forceinline__ void load_maps(bool resumed) {
     const int nw = (L * L + 31) / 32;
-    if constexpr (SB) {
-      fs0 = fs1 = rs0 = rs1 = 0ull;
-      if (resumed) {
-        sync();
-        uint32_t fw[4], rw[4];
-        for (int i = 0; i < 4; ++i) {
-          fw[i] = i < nw ? __builtin_amdgcn_readfirstlane(fieldw[i]) : 0u;
-          rw[i] = i < nw ? __builtin_amdgcn_readfirstlane(rotw[i]) : 0u;
-        }
-        fs0 = (uint64_t)fw[0] | ((uint64_t)fw[1] << 32); fs1 = (uint64_t)fw[2] | ((uint64_t)fw[3] << 32);
-        rs0 = (uint64_t)rw[0] | ((uint64_t)rw[1] << 32); rs1 = (uint64_t)rw[2] | ((uint64_t)rw[3] << 32);
-      }
-    } else {
-      field = resumed && lane < nw ? fieldw[lane] : 0u;
-      rot = resumed && lane < nw ? rotw[lane] : 0u;
-    }
+    field = resumed && lane < nw ? fieldw[lane] : 0u;
+    rot = resumed && lane < nw ? rotw[lane] : 0u;
   }
   __device__ __forceinline__ void save_maps() {
     const int nw = (L * L + 31) / 32;
-    if constexpr (SB) {
-      if (lane < nw) {
-        const uint64_t f = lane < 2 ? fs0 : fs1, r = lane < 2 ? rs0 : rs1;
-        fieldw[lane] = (uint32_t)(f >> (32 * (lane & 1)));
-        rotw[lane] = (uint32_t)(r >> (32 * (lane & 1)));
-      }
-    } else if (lane < nw) {
+    if (lane < nw) {
       fieldw[lane] = field;
       rotw[lane] = rot;
     }
@@ -259,14 +209,14 @@ struct WaveRoadGen {
   // from each candidate branch point picks[klo, khi) over the free cells, one frontier
   // bitmap step per walk length; true when no candidate reaches a border cell at
   // Manhattan distance >= 3L/4 from endc in fewer than 2L - (nm - index) cells.
-  // 128-bit shifts of an SB bitmap (0 < sh < 64)
+  // 128-bit shifts of a scalar-word bitmap (0 < sh < 64)
   static __device__ __forceinline__ void shl128(uint64_t& lo, uint64_t& hi, int sh) {
     hi = (hi << sh) | (lo >> (64 - sh)); lo <<= sh;
   }
   static __device__ __forceinline__ void shr128(uint64_t& lo, uint64_t& hi, int sh) {
     lo = (lo >> sh) | (hi << (64 - sh)); hi >>= sh;
   }
-  // (fs0, fs1: the field as scalar words -- SB form, or converted from the lane words)
+  // (fs0, fs1: the field as scalar words, converted from the lane words)
   __device__ bool hopeless_sb(int klo, int khi, int nm, int endc, uint64_t fs0, uint64_t fs1) {
     const int ncells = L * L, dmin = L * 3 / 4;
     // masks by ballot: lane l tests cells l and 64 + l
@@ -307,7 +257,6 @@ struct WaveRoadGen {
     return true;
   }
   __device__ bool hopeless(int klo, int khi, int nm, int endc) {
-    if constexpr (SB) return hopeless_sb(klo, khi, nm, endc, fs0, fs1);
     if constexpr (NC <= 128 && SBP) {
       // the lane-word field as two scalar words (lane l: cells l and 64 + l), then the
       // scalar search: 4.7x faster than the lane-word search (r04/s11 probe_draw_parts)
@@ -354,13 +303,8 @@ struct WaveRoadGen {
       const int m = cnt - i0 < 64 ? cnt - i0 : 64;
       for (int i = 0; i < m; ++i) {
         const int c = (int)rdl(cv, i);
-        if constexpr (SB) {
-          sclr(fs0, fs1, c);
-          sclr(rs0, rs1, c);
-        } else {
-          field = without(field, c);
-          rot = without(rot, c);
-        }
+        field = without(field, c);
+        rot = without(rot, c);
       }
     }
   }

@@ -99,6 +99,9 @@ def _load():
         "td_kernel_timing": (ctypes.c_int, [c_vp, ctypes.c_int, ctypes.c_int]),
         "td_kernel_times": (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_float), ctypes.c_int]),
         "td_board_map": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, c_i32p]),
+        "td_set_store_policy": (ctypes.c_int, [c_vp, ctypes.c_int, ctypes.c_int]),
+        "td_guard_timeouts": (ctypes.c_int, [c_vp, ctypes.c_int]),
+        "td_debug_set_claim": (ctypes.c_int, [c_vp, ctypes.c_int, ctypes.c_int]),
         "td_py_seed": (None, [c_u32p, ctypes.c_uint32]),
         "td_np_seed": (None, [c_u32p, ctypes.c_uint32]),
         "td_mt_next": (ctypes.c_uint32, [c_u32p]),

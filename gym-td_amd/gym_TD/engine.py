@@ -51,15 +51,30 @@ _TYPESTR = {torch.float32: "<f4", torch.int64: "<i8"}
 # auto (default): contiguous from CONTIG_OBS_MIN bytes on -- faster there (32,768 boards at
 # 10x10, 590 MB: 112.5 vs 115.5 us; 30x30 / 16,384, 2.65 GB: 498.7 vs 517.6; 65,536 +-0),
 # slower below (16,384 / 8,192 / 4,096 boards: +0.6-2.2 %), profiles/r04/s26.
-# TD_CONTIG_OBS=1 / 0 forces it.
-CONTIG_OBS = os.environ.get("TD_CONTIG_OBS", "auto")
+# TD_CONTIG_OBS=1 / 0 (or true / false, yes / no, on / off) forces it; any other value
+# warns once and keeps auto.
 CONTIG_OBS_MIN = 512 << 20
+
+
+def _parse_contig_obs(v):
+    v = (v or "auto").strip().lower()
+    if v in ("1", "true", "yes", "on"):
+        return True
+    if v in ("0", "false", "no", "off"):
+        return False
+    if v != "auto":
+        import warnings
+        warnings.warn("TD_CONTIG_OBS=%r is not auto / 0 / 1 / true / false: using auto" % v, RuntimeWarning)
+    return "auto"
+
+
+CONTIG_OBS = _parse_contig_obs(os.environ.get("TD_CONTIG_OBS"))
 
 
 def _contig_obs(nbytes):
     if CONTIG_OBS == "auto":
         return nbytes >= CONTIG_OBS_MIN
-    return int(CONTIG_OBS) != 0
+    return CONTIG_OBS
 
 
 def device_zeros(shape, dtype, device, contiguous=None):
@@ -80,6 +95,7 @@ def device_zeros(shape, dtype, device, contiguous=None):
         del blk  # (frees the block)
         return torch.zeros(shape, dtype=dtype, device=dev)
     t._td_block = True  # (tests: the block was adopted)
+    t._td_contig = contig  # (requested physically contiguous: TDEngine.obs_alloc)
     return t
 
 
@@ -144,6 +160,8 @@ class TDEngine(object):
         # the observation, the step's write stream: contiguous device memory (td_alloc_device)
         self.obs = zeros((B, _lib.NCH, L, L), torch.float32) if self.host_io else \
             device_zeros((B, _lib.NCH, L, L), torch.float32, self.device)
+        # how the observation was allocated (bench.py keys PMC traffic records by it)
+        self.obs_alloc = "host" if self.host_io else "contiguous" if getattr(self.obs, "_td_contig", False) else "plain"
         self.reward = zeros(B, torch.float64)
         self.done = zeros(B, torch.uint8)
         self.info_enabled = bool(info)
@@ -389,6 +407,17 @@ class TDEngine(object):
     def step_kernel_name(self):
         """Its name as rocprofv3 reports it, e.g. 'td_step_kernel_small<10, 0, false>'."""
         return _lib.lib.td_step_kernel_name(self._h).decode()
+
+    def set_store_policy(self, xcd_map=1, edge_wt=2):
+        """Board map and shared-line store policy of the step kernels (td_set_store_policy):
+        xcd_map 1 = XCD-contiguous boards, 0 = block i steps board i; edge_wt 2 = the lines a
+        board shares with its neighbours as plain write-back stores, 1 = write-through.  Every
+        policy gives the same bytes; the defaults are the fastest measured."""
+        _lib.check(_lib.lib.td_set_store_policy(self._h, int(xcd_map), int(edge_wt)))
+
+    def guard_timeouts(self, clear=False):
+        """Ring-guard waits for a board's refill claim that gave up (td_guard_timeouts)."""
+        return _lib.check(_lib.lib.td_guard_timeouts(self._h, int(bool(clear))))
 
     def set_refill_interval(self, steps):
         """Steps between layout-refill launches (auto-reset; 0 = none, rings only drain)."""

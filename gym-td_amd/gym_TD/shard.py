@@ -31,16 +31,21 @@ def episode_stats(done, ep_return):
     return torch.stack([n, s])
 
 
+def _group():
+    return dist.is_available() and dist.is_initialized()
+
+
 def max_over_ranks(t):
-    """In-place MAX over ranks (no-op without a process group)."""
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+    """In-place MAX over ranks (no-op without a process group; a group of one still runs
+    the collective, so the RCCL path is exercised at world size 1 too)."""
+    if _group():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return t
 
 
 def gather_stats(stats, dst=0):
     """Gather every rank's stats tensor on ``dst``; returns [W, ...] there, None elsewhere."""
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if not _group():
         return stats.unsqueeze(0)
     rank, world = dist.get_rank(), dist.get_world_size()
     out = [torch.zeros_like(stats) for _ in range(world)] if rank == dst else None
@@ -68,7 +73,7 @@ def gather_episode_records(ret, length, win, dst=0):
     (return f64, length i32, win i32), the per-board payload of SURVEY.md 8(e), once per
     reporting interval -- as [world * B] tensors in global board order.  None elsewhere."""
     raw = pack_episode_records(ret, length, win)
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if not _group():
         return unpack_episode_records(raw)
     rank, world = dist.get_rank(), dist.get_world_size()
     out = [torch.zeros_like(raw) for _ in range(world)] if rank == dst else None

@@ -52,7 +52,10 @@ enum td_board_flag {
   TD_FLAG_TW_OVERFLOW = 2, /* more than 32 towers: build refused */
   TD_FLAG_BAD_ACTION = 4,  /* action outside the action space (the reference asserts) */
   TD_FLAG_NO_LAYOUT = 8,   /* auto-reset found no staged layout */
-  TD_FLAG_BAD_MOVE = 16    /* an enemy walked off the board (corrupt layout) */
+  TD_FLAG_BAD_MOVE = 16,   /* an enemy walked off the board (corrupt layout) */
+  TD_FLAG_CLAIM_TIMEOUT = 32 /* a wait for the board's refill claim gave up after 1 s: the ring
+                                guard left its ring short, or its episode end found no layout
+                                (then TD_FLAG_NO_LAYOUT too); see td_guard_timeouts */
 };
 
 /* Game parameters: gym_TD/envs/TDParam.py:1-64 (Config) and :105-111 (HyperParameters).
@@ -276,10 +279,28 @@ int td_import_state(td_handle* h, int b0, int count, const void* host_src);
 int td_get_flags(td_handle* h, int32_t* host_flags);
 
 /* The board each step-kernel block steps (diagnostic; no GPU needed): out[i] for blocks
- * i in [0, n_boards).  kind 0: the large kernel's XCD-contiguous map (block i runs on XCD
- * i % 8 and steps the (i / 8)-th board of that XCD's contiguous range); kind 1: the same for
- * the small kernels' order lists at boards_per_workgroup = 1.  xcd_map = 0: block i = board i. */
+ * i in [0, n_boards): the XCD-contiguous map of every step kernel (block i runs on XCD
+ * i % 8 and steps the (i / 8)-th board of that XCD's contiguous range).  kind 0 and 1 give
+ * the same map (kind 1 named the small kernels' board-order lists, removed in round 5).
+ * xcd_map = 0: block i = board i. */
 int td_board_map(int n_boards, int kind, int xcd_map, int32_t* out);
+
+/* How the step kernels place boards and store the two observation lines a board shares
+ * with its neighbours (18,000 B per board at 10x10 is not a multiple of 128):
+ *   xcd_map 1 (default): the XCD-contiguous board map (td_board_map kind 0); 0: block i = board i;
+ *   edge_wt 2 (default): plain write-back stores, merged in the XCD's L2; 1: write-through.
+ * Results are the same bytes for every policy (tests/test_gpu_store_policy.py); the defaults
+ * are the fastest measured.  Synchronises the device. */
+int td_set_store_policy(td_handle* h, int xcd_map, int edge_wt);
+
+/* Ring-guard waits for a board's refill claim that gave up after 1 s (a claim never given
+ * back): the board is flagged TD_FLAG_CLAIM_TIMEOUT and its ring may run short.  Returns the
+ * count since the last clear (clear != 0 zeroes it).  Synchronous. */
+int td_guard_timeouts(td_handle* h, int clear);
+
+/* Diagnostic (tests): hold (held = 1) or give back (0) board b's refill claim, as a refill
+ * wave drawing its layouts holds it.  Synchronises the device. */
+int td_debug_set_claim(td_handle* h, int board, int held);
 
 /* Host-side RNG helpers (exposed for tests and for seeding from Python states). */
 void td_py_seed(uint32_t* mt625, uint32_t seed);

@@ -2,35 +2,60 @@
 
     python scripts/prune_profiles.py profiles/r02 profiles/r03
 
-Every <session>/<run>.log whose content holds a bench.py JSON line becomes one line of
-<session>/runs.jsonl ({"run": <run>, **that JSON}); the log itself is removed.  Logs
-without a bench line (pytest, smoke, phase stamps, traces) and every other file stay."""
+Every <session>/<run>.log that holds bench.py JSON lines and NOTHING else (blank lines
+aside) becomes lines of <session>/runs.jsonl ({"run": <run>, **that JSON}) and is removed.
+A log with any other output (rocprofv3 text, warnings, pytest, phase stamps), or with a
+JSON line that does not parse, is left as it is and contributes nothing.  runs.jsonl is
+rewritten keyed by run name, so folding a session twice changes nothing."""
 import json
 import os
 import sys
 
 
+def _bench_lines(path):
+    """The parsed bench lines of a log made only of them, else None."""
+    out = []
+    for ln in open(path, errors="replace"):
+        ln = ln.strip()
+        if not ln:
+            continue
+        if not ln.startswith('{"metric"'):
+            return None
+        try:
+            out.append(json.loads(ln))
+        except ValueError:
+            return None
+    return out or None
+
+
 def fold(session):
-    runs = []
+    jl = os.path.join(session, "runs.jsonl")
+    runs = {}
+    if os.path.exists(jl):
+        for ln in open(jl):
+            if ln.strip():
+                r = json.loads(ln)
+                runs.setdefault(r["run"], []).append(r)
+    folded = []
     for f in sorted(os.listdir(session)):
         p = os.path.join(session, f)
-        if not f.endswith(".log") or not os.path.isfile(p) or f.startswith(("pytest", "smoke", "phases", "session")):
+        if not f.endswith(".log") or not os.path.isfile(p):
             continue
-        lines = [l for l in open(p, errors="replace") if l.startswith('{"metric"')]
-        if not lines:
+        lines = _bench_lines(p)
+        if lines is None:
             continue
-        for l in lines:
-            try:
-                runs.append(dict(run=f[:-4], **json.loads(l)))
-            except ValueError:
-                break
-        else:
+        runs[f[:-4]] = [dict(run=f[:-4], **d) for d in lines]
+        folded.append(p)
+    if folded:
+        tmp = jl + ".tmp"
+        with open(tmp, "w") as out:
+            for name in sorted(runs):
+                for r in runs[name]:
+                    out.write(json.dumps(r) + "\n")
+        os.replace(tmp, jl)
+        for p in folded:  # removed only once runs.jsonl holds their lines
             os.remove(p)
-    if runs:
-        with open(os.path.join(session, "runs.jsonl"), "a") as out:
-            for r in runs:
-                out.write(json.dumps(r) + "\n")
-    return len(runs)
+    return len(folded)
 
 
 if __name__ == "__main__":

@@ -1,0 +1,30 @@
+#!/bin/bash
+# Round-5 GPU sessions: bash scripts/r05.sh <session>.  Every GPU step runs under its own
+# time limit; the session stops at the first crash / timeout (pytest's 1 = failures is
+# reported and the session goes on only where noted).
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+export TMPDIR=/tmp
+S=$1
+O=gpurun_out/r05_$S
+mkdir -p $O
+run() { local name=$1 secs=$2; shift 2; echo "== $name $(date +%T)"; timeout -k 10 "$secs" "$@" > "$O/$name.log" 2>&1; local rc=$?; echo "== $name rc=$rc"; [ $rc -ne 0 ] && tail -25 "$O/$name.log"; return $rc; }
+line() { grep -h '^{' "$O/$1.log" | python3 -c "import json,sys
+for l in sys.stdin: d=json.loads(l); r=d['roofline']; print('   %-18s' % '$1', round(d['value']/1e6,1), 'M/s  step', round(d['ms_per_step']*1e3,2), 'us  kernel', r['avg_kernel_us'] and round(r['avg_kernel_us'],2), 'frac', r['frac'] and round(r['frac'],3), r['kernel'], 'n', r['kernel_samples'], 'B/gpu', d['config']['boards_per_gpu'], 'flags', d.get('board_flags'), 'eps', d['episodes']['finished'])"; }
+gpusuite() { run pytest_gpu ${1:-900} python -u -m pytest tests -m gpu -q --timeout 400 --timeout-method thread -p no:cacheprovider; local rc=$?; grep -E "^(FAILED|E  )" $O/pytest_gpu.log | head -30; tail -1 $O/pytest_gpu.log; return $rc; }
+case $S in
+s1)  # the stripped build: GPU suite, smoke, the driver's command, every share, timing-event probe
+  gpusuite 900; rc=$?; [ $rc -le 1 ] || exit $rc
+  run smoke 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" || exit 1
+  run bench_driver 300 python bench.py --gpus 1 --steps 20 --warmup 5 || exit 1
+  grep '^{' $O/bench_driver.log; line bench_driver
+  run b65536 200 python bench.py --no-cpu-baseline --steps 300 --timing none || exit 1; line b65536
+  for bb in 8192 4096; do
+    run b$bb 200 python bench.py --global-batch $bb --no-cpu-baseline --steps 2000 --timing none || exit 1; line b$bb
+  done
+  run p2 300 python bench.py --workload 2p-middle-multi --no-cpu-baseline --steps 200 --timing none || exit 1; line p2
+  run l30 300 python bench.py --workload def-large --global-batch 16384 --no-cpu-baseline --steps 200 --timing none || exit 1; line l30
+  run probe_timing_65536 300 python scripts/probe_timing.py 65536 || exit 1; cat $O/probe_timing_65536.log | tail -1 | cut -c1-3000
+  run probe_timing_8192 300 python scripts/probe_timing.py 8192 || exit 1; cat $O/probe_timing_8192.log | tail -1 | cut -c1-3000
+  ;;
+*) echo "unknown session $S"; exit 2;;
+esac

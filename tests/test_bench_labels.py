@@ -29,10 +29,23 @@ def test_other_batches_are_not_labelled_as_the_metric():
         bench.partition("def-small", 3)
 
 
-def test_traffic_only_for_the_measured_build(tmp_path, monkeypatch):
-    # a record measured on other kernel sources (or at another batch) is never quoted
-    assert bench.measured_traffic("def-small", 12345) == (None, None)
+def test_traffic_only_for_the_measured_build(tmp_path):
+    # a record measured on other kernel sources, at another batch, of another kernel or with
+    # the observation allocated another way is never quoted
+    import json
+    k = "td_step_kernel<10, 0, false>"
+    assert bench.measured_traffic("def-small", 12345, k, "plain") == (None, None)
     assert len(bench.kernel_source_hash()) == 16
+    rec = {"hbm_bytes_per_launch": 1.0e9, "read": 1.0e8, "write": 9.0e8, "round": "rX", "kernel": k,
+           "kernel_src": bench.kernel_source_hash(), "obs_alloc": "contiguous"}
+    p = tmp_path / "pmc.json"
+    p.write_text(json.dumps({"def-small_B65536": rec}))
+    assert bench.measured_traffic("def-small", 65536, k, "contiguous", path=str(p))[0] == 1.0e9
+    assert bench.measured_traffic("def-small", 65536, k, "plain", path=str(p)) == (None, None)
+    assert bench.measured_traffic("def-small", 65536, "td_step_kernel_small<10, 0, false>", "contiguous",
+                                  path=str(p)) == (None, None)
+    p.write_text(json.dumps({"def-small_B65536": dict(rec, kernel_src="0" * 16)}))
+    assert bench.measured_traffic("def-small", 65536, k, "contiguous", path=str(p)) == (None, None)
 
 
 def test_world_must_match_gpus():

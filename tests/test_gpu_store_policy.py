@@ -2,15 +2,13 @@
 
 18,000 B (10x10) / 72,000 B (20x20) of observation per board is not a multiple of the
 128-B line, so each board shares its first and last line with the boards beside it.
-The product stores those halves with plain write-back stores (td_capi.hip edge_wt = 2):
-with the XCD-contiguous board map both halves meet in one XCD's L2; where a pair is split
-across two XCDs (the ends of the XCD blocks, or every pair with TD_XCD_MAP=0) both L2s
+The product stores those halves with plain write-back stores (td_set_store_policy edge_wt
+= 2): with the XCD-contiguous board map both halves meet in one XCD's L2; where a pair is
+split across two XCDs (the ends of the XCD blocks, or every pair with xcd_map = 0) both L2s
 write their dirty bytes back.  Every policy and map must give the same bytes as the
 write-through form (edge_wt = 1) on the same seeds and actions.  The batch is large
 enough that the observation is not stored write-through as a whole (it exceeds the
 256-MiB Infinity Cache), so the shared-line path is the one taken."""
-import os
-
 import numpy as np
 import pytest
 import torch
@@ -22,22 +20,14 @@ if not torch.cuda.is_available():  # collected on CPU too, so skip cleanly
 
 from gym_TD.engine import TDEngine  # noqa: E402
 
-# (TD_XCD_MAP, TD_EDGE_WT): the product first, then the reference form and the split pairs
-POLICIES = [("1", "2"), ("1", "1"), ("0", "2"), ("0", "1")]
+# (xcd_map, edge_wt): the product first, then the reference form and the split pairs
+POLICIES = [(1, 2), (1, 1), (0, 2), (0, 1)]
 
 
 def _engine(L, B, seeds, xcd, edge):
-    keys = ("TD_XCD_MAP", "TD_EDGE_WT")
-    old = {k: os.environ.get(k) for k in keys}
-    os.environ["TD_XCD_MAP"], os.environ["TD_EDGE_WT"] = xcd, edge
-    try:  # the knobs are read once, at td_create
-        return TDEngine(L, B, "def", False, 1, np_seeds=seeds, py_seeds=seeds, autoreset=True)
-    finally:
-        for k, v in old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
+    e = TDEngine(L, B, "def", False, 1, np_seeds=seeds, py_seeds=seeds, autoreset=True)
+    e.set_store_policy(xcd, edge)
+    return e
 
 
 @pytest.mark.parametrize("L,B,steps", [(20, 4096, 40), (10, 16384, 60)])
