@@ -20,6 +20,7 @@
 
 #include <hip/hip_ext.h>
 
+#include "td_board.h"
 #include "td_kernels.h"
 #include "td_layout.h"
 #include "td_rng.h"
@@ -39,10 +40,6 @@ namespace td {
 #define STAMP(i) do { } while (0)
 #define STAMP_RT(i) do { } while (0)
 #endif
-
-constexpr int MAX_KERNEL_L = 32;  // generic-L kernels: L <= 32
-
-enum : int { FC_OK = 0, FC_COST = 1, FC_POS = 2, FC_LVMAX = 3, FC_TARGET = 4, FC_CAP = 6 };  // utils/fail_code.py
 
 // ---------------------------------------------------------------------------
 // per-board LDS image
@@ -77,17 +74,6 @@ struct alignas(16) Smem {
   TdDevCfg cfg;           // constant block, staged once per board: per-lane table lookups hit LDS
 };
 
-// The tower on a cell lives in the LDS copy of its cell word, bits 10-13 (unused by the
-// layout format, td_layout.h): bit 3 of the nibble = a tower, bit 2 its level, bits 0-1
-// its type.  (A byte map of its own cost NC bytes of LDS per board: 900 at 30x30, where the
-// board image bounds residency.)  HBM cell words never carry it (store_cells masks it).
-constexpr uint32_t kTwBits = 0xFu << 10;
-__device__ __forceinline__ uint32_t tw_nib(int lv, int type) { return (0x8u | ((uint32_t)lv << 2) | (uint32_t)type) << 10; }
-// the tower byte of a cell word: 0 none, else 0x80 | lv << 2 | type
-__device__ __forceinline__ uint32_t twr_of(uint32_t w) {
-  const uint32_t n = (w >> 10) & 0xFu;
-  return (n & 8u) ? (0x80u | (n & 7u)) : 0u;
-}
 template <int NC>
 __device__ __forceinline__ void set_tower(Smem<NC>& S, int cell, uint32_t nib) {
   S.cell[cell] = (S.cell[cell] & ~kTwBits) | nib;
@@ -624,27 +610,6 @@ __device__ __forceinline__ int summon_cluster(Smem<NC>& S, U& u, const Ctx& x, u
 // ---------------------------------------------------------------------------
 // TDBoard.step (TDBoard.py:295-368) + enemy_LP statistics
 // ---------------------------------------------------------------------------
-// packed cell words (pack_obs_cells): the march direction and the distance to the end
-__device__ __forceinline__ int pk_dir(uint32_t w) { return (int)((w >> 21) & 3u); }
-__device__ __forceinline__ int pk_dist(uint32_t w) { return (int)(w >> 24); }
-
-__device__ __forceinline__ int cheb(int a, int b, int L) {
-  int dr = a / L - b / L, dc = a % L - b % L;
-  dr = dr < 0 ? -dr : dr;
-  dc = dc < 0 ? -dc : dc;
-  return dr > dc ? dr : dc;
-}
-
-// Enemy.damage, TDElements.py:19-28
-__device__ __forceinline__ double damage(double LP, double atk, double def, bool magic) {
-  double dmg = magic ? atk : (dsub(atk, def) < 0.0 ? 0.0 : dsub(atk, def));
-  double lo = dmul(atk, 0.05);
-  if (dmg < lo) dmg = lo;
-  LP = dsub(LP, dmg);
-  if (LP <= 0.0) LP = 0.0;
-  return LP;
-}
-
 // Enemy.defense as the enemy captured it (TDElements.py:33-43)
 __device__ __forceinline__ double e_def(const Ctx& x, uint32_t inf) {
   const int t = en_type(inf), lv = en_lv(inf);
@@ -980,31 +945,6 @@ __device__ __forceinline__ void channel_scalars(Smem<NC>& S, const U& u, const C
 }
 
 
-// Binary observation channels as bits of one word per cell (bit c = channel c):
-// 0-3 roads, 4 end, 6-8 starts, 14 buildable (map[6] == 0), 15-16 tower level,
-// 17-20 tower type (TDBoard.py:113-133).
-constexpr uint32_t kBinaryChannels = 0x1FC1DFu;
-
-__device__ __forceinline__ uint32_t cell_bits(uint32_t w, uint32_t tw) {
-  uint32_t m = (w & 0x1Fu) | (((w >> 5) & 7u) << 6) | ((w >> 24) == 0u ? (1u << 14) : 0u);
-  if (tw & 0x80u) m |= (1u << (15u + ((tw >> 2) & 1u))) | (1u << (17u + (tw & 3u)));
-  return m;
-}
-
-__device__ __forceinline__ float bitf(uint32_t m, int ch) { return (float)((m >> ch) & 1u); }
-
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-
-// Channel kinds of the observation (TDBoard.get_states, :112-143).
-enum ObsKind : int { OK_BIN, OK_CONST, OK_D9, OK_ENEMY };
-__host__ __device__ constexpr int obs_kind(int ch) {
-  return ch == 9 ? OK_D9
-       : (ch < 32 && ((kBinaryChannels >> ch) & 1u)) ? OK_BIN
-       : (ch >= 25 && ch < 41) ? OK_ENEMY
-       : OK_CONST;
-}
-
 // Once the step's actions are done (the towers and map[6] are final), the cell words
 // are replaced in LDS by what the rest of the step reads of a cell: the binary
 // observation bits (cell_bits, bits 0-20), the march direction map[5] (bits 21-22)
@@ -1106,15 +1046,6 @@ __device__ __forceinline__ void write_obs(const Smem<NC>& S, const Ctx& x, float
     }
   }
 }
-
-// Channel classes of the observation as 64-bit channel masks (TDBoard.get_states,
-// :112-143): bits of the packed cell word, the enemy_LP planes, channel 9 (distance
-// by table), and the broadcast channels.
-constexpr uint64_t kChBin = kBinaryChannels;
-constexpr uint64_t kChD9 = 1ull << 9;
-constexpr uint64_t kChEnemy = 0xFFFFull << 25;
-constexpr uint64_t kChAll = (1ull << NCH) - 1;
-constexpr uint64_t kChConst = kChAll & ~(kChBin | kChD9 | kChEnemy);
 
 // The class of every observation window, by the board's misalignment `mis` (units of
 // the 128-B line before the board) and window k, as a compile-time table read with one
@@ -1660,8 +1591,6 @@ __device__ __forceinline__ void attacker_actions(Smem<NC>& S, U& u, const Ctx& x
 // the observation lines are stored write-through (write_obs_lines).  (Storing the
 // layout and tower planes at the start of the step, before the step logic, was
 // measured slower at 4,096 and 8,192 boards: 36.3 / 53.1 vs 25.7 / 38.3 us.)
-// A board whose ring of staged layouts is empty at its episode end (td_step.hip below).
-__device__ __forceinline__ bool take_dry_ring(const StepArgs& a, int b, uint32_t head, int* flags);
 
 // Observation windows written by the stepping wave of a two-wave board (the first half).
 template <int LT>
@@ -1930,19 +1859,6 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
   STAMP_RT(10);
 }
 
-// The kernel's StepArgs, read through the kernarg segment where each field is used
-// (scalar loads that hit the constant cache) instead of being held in SGPRs for the
-// whole kernel: with 80 SGPRs (8 waves per SIMD) the small kernels otherwise spilled ~50
-// SGPRs into VGPR lanes and read them back with ~150 v_readlane (static counts, L = 10):
-// +1.4 % at 4,096 / 8,192 boards (profiles/r03/s10).  The large kernel keeps its
-// by-value arguments (106 SGPRs at 7 waves per SIMD; read through the segment it fell
-// to 83 SGPRs, ran 8 waves per SIMD and lost 4.6 % at 65,536 boards).  The StepArgs must
-// be the kernel's first argument (kernarg offset 0).
-__device__ __forceinline__ const StepArgs& kargs(const StepArgs& a) {
-  (void)a;
-  return *(const StepArgs*)__builtin_amdgcn_kernarg_segment_ptr();  // (C cast: leaves the constant address space)
-}
-
 // One workgroup (one wave) per board.  (A persistent variant that prefetched the
 // next board while stepping the current one measured slower: its static board
 // assignment leaves a one-board tail, and the step is bound by HBM writes.)
@@ -2186,28 +2102,6 @@ __device__ int wave_layout(LayoutSmem<NC>& G, const StepArgs& a, int b, int retr
   return st;
 }
 
-// The step wave of board b found layout `head` unpublished at the episode end.  If a
-// refill wave holds the board's claim it is drawing exactly this layout (an empty ring
-// is urgent: its draw runs to the end): wait for the tag, bounded (1 s; a wait that gives
-// up sets FLAG_CLAIM_TIMEOUT in *flags).  Otherwise the ring ran dry with no refill beside
-// the step: the board is flagged no_layout by the caller.  (The step wave drawing the
-// layout itself measured 4.5x slower steps: the called draw spills 0.5-1 KB of scratch
-// per lane in every step kernel, profiles/r03/s4.)  True when layout `head` is ready.
-__device__ __forceinline__ bool take_dry_ring(const StepArgs& a, int b, uint32_t head, int* flags) {
-  uint32_t* const slot = a.nxt + ((size_t)b * NSLOT + head % NSLOT) * a.slot_words;
-  const uint32_t want = slot_tag(head);
-  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  for (;;) {
-    if (ld_relaxed(a.lay_claim + b) == 0u) return ld_relaxed(slot) == want;
-    if (ld_relaxed(slot) == want) return true;
-    if (__builtin_amdgcn_s_memrealtime() - t0 >= kTakeSpinTicks) {
-      *flags |= FLAG_CLAIM_TIMEOUT;
-      return false;
-    }
-    __builtin_amdgcn_s_sleep(64);
-  }
-}
-
 // TDGymBasic.reset of board b, by one wave (the device is idle for this board: no refill
 // holds it).  The layout is the caller's record (td_reset_layouts), else the board's
 // next staged layout, else a draw from its numpy stream now -- skipping up to `retries`
@@ -2416,6 +2310,8 @@ static hipError_t launch2(const StepArgs& a, hipStream_t s, bool reset, hipEvent
   const bool aligned = (reinterpret_cast<uintptr_t>(a.obs) & 15u) == 0;
   if (reset) {
     hipLaunchKernelGGL(td_reset_kernel<LT>, dim3(a.B), dim3(64), 0, s, a);
+  } else if (a.small == 3 && aligned && half_supported(a)) {
+    return launch_step_half(a, s, ev0, ev1);
   } else if constexpr (LT != 0) {
     if (a.small == 2 && aligned) TD_STEP_DISPATCH(td_step_kernel_small2, LT, a, TD_LAUNCH2);
     else if (a.small && aligned) TD_STEP_DISPATCH(td_step_kernel_small, LT, a, TD_LAUNCH);

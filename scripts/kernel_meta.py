@@ -16,14 +16,22 @@ LIB = os.path.join(HERE, "gym-td_amd", "lib", "libtdstep.so")
 
 
 def kernels(lib=LIB):
-    """{kernel symbol: {"sgpr", "vgpr", "scratch", "lds"}} from the library's gfx950 code object."""
+    """{kernel symbol: {"sgpr", "vgpr", "scratch", "lds"}} from the library's gfx950 code
+    objects (one offload bundle per translation unit in .hip_fatbin)."""
+    magic = b"__CLANG_OFFLOAD_BUNDLE__"
+    notes = ""
     with tempfile.TemporaryDirectory() as d:
-        fat, co = os.path.join(d, "fat.bin"), os.path.join(d, "gfx950.co")
+        fat = os.path.join(d, "fat.bin")
         subprocess.check_call([os.path.join(LLVM, "llvm-objcopy"), "--dump-section=.hip_fatbin=" + fat, lib,
                                os.path.join(d, "copy.so")])
-        subprocess.check_call([os.path.join(LLVM, "clang-offload-bundler"), "--type=o", "--input=" + fat,
-                               "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", "--output=" + co, "--unbundle"])
-        notes = subprocess.check_output([os.path.join(LLVM, "llvm-readelf"), "--notes", co]).decode()
+        blob = open(fat, "rb").read()
+        starts = [i for i in range(len(blob)) if blob.startswith(magic, i)]
+        for k, a in enumerate(starts):
+            part, co = os.path.join(d, "b%d.bin" % k), os.path.join(d, "b%d.co" % k)
+            open(part, "wb").write(blob[a:starts[k + 1] if k + 1 < len(starts) else len(blob)])
+            subprocess.check_call([os.path.join(LLVM, "clang-offload-bundler"), "--type=o", "--input=" + part,
+                                   "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", "--output=" + co, "--unbundle"])
+            notes += subprocess.check_output([os.path.join(LLVM, "llvm-readelf"), "--notes", co]).decode() + "\n"
     out, cur = {}, None
     keys = {".sgpr_count": "sgpr", ".vgpr_count": "vgpr", ".private_segment_fixed_size": "scratch",
             ".group_segment_fixed_size": "lds"}

@@ -12,7 +12,9 @@ line() { grep -h '^{' "$O/$1.log" | python3 -c "import json,sys
 for l in sys.stdin: d=json.loads(l); r=d['roofline']; print('   %-18s' % '$1', round(d['value']/1e6,1), 'M/s  step', round(d['ms_per_step']*1e3,2), 'us  kernel', r['avg_kernel_us'] and round(r['avg_kernel_us'],2), 'frac', r['frac'] and round(r['frac'],3), r['kernel'], 'n', r['kernel_samples'], 'B/gpu', d['config']['boards_per_gpu'], 'flags', d.get('board_flags'), 'eps', d['episodes']['finished'])"; }
 gpusuite() { run pytest_gpu ${1:-900} python -u -m pytest tests -m gpu -q --timeout 400 --timeout-method thread -p no:cacheprovider; local rc=$?; grep -E "^(FAILED|E  )" $O/pytest_gpu.log | head -30; tail -1 $O/pytest_gpu.log; return $rc; }
 case $S in
-s1)  # the stripped build: GPU suite, smoke, the driver's command, every share, timing-event probe
+s1)  # the stripped build + the half-wave kernel: its parity first, the GPU suite, smoke, the driver's command, every share, timing-event probe
+  run pytest_half 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -q -x -k "half and batched" --timeout 300 --timeout-method thread -p no:cacheprovider
+  rc=$?; grep -E "^(FAILED|E  )" $O/pytest_half.log | head -30; tail -1 $O/pytest_half.log; [ $rc -le 1 ] || exit $rc
   gpusuite 900; rc=$?; [ $rc -le 1 ] || exit $rc
   run smoke 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" || exit 1
   run bench_driver 300 python bench.py --gpus 1 --steps 20 --warmup 5 || exit 1
@@ -20,6 +22,9 @@ s1)  # the stripped build: GPU suite, smoke, the driver's command, every share, 
   run b65536 200 python bench.py --no-cpu-baseline --steps 300 --timing none || exit 1; line b65536
   for bb in 8192 4096; do
     run b$bb 200 python bench.py --global-batch $bb --no-cpu-baseline --steps 2000 --timing none || exit 1; line b$bb
+  done
+  for bb in 8192 4096 16384; do
+    run h$bb 200 python bench.py --global-batch $bb --no-cpu-baseline --steps 2000 --timing none --step-kernel half || exit 1; line h$bb
   done
   run p2 300 python bench.py --workload 2p-middle-multi --no-cpu-baseline --steps 200 --timing none || exit 1; line p2
   run l30 300 python bench.py --workload def-large --global-batch 16384 --no-cpu-baseline --steps 200 --timing none || exit 1; line l30
