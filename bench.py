@@ -77,6 +77,14 @@ FLAG_BITS = (("enemy_overflow", 1), ("tower_overflow", 2), ("bad_action", 4), ("
 
 
 KERNEL_SAMPLES_MIN = 8  # sampled launches behind a kernel mean
+# A timed region too short for KERNEL_SAMPLES_MIN samples (the driver's 20 steps) runs without
+# timing events; behind it AFTER_WARM untimed steps bring the GPU back to its steady state
+# after the host-side gap, then a pass of AFTER_STEPS steps is sampled every AFTER_EVERY-th
+# launch.  (A 64-step pass sampled every 8th launch right after the gap measured 213-215 us
+# against 209.9-210.2 us per step in the timed region at 65,536 boards, BENCH_r04 and
+# r05/s1; back-to-back 256-step passes: 203.5 us sampled every 32nd, wall 205.4-205.6 with
+# or without the events, scripts/probe_timing.py in r05/s1.)
+AFTER_WARM, AFTER_STEPS, AFTER_EVERY = 16, 256, 32
 
 
 def event_every(steps, override=None):
@@ -89,25 +97,27 @@ def event_every(steps, override=None):
 
 
 def timing_plan(steps, every):
-    """Where the step-kernel durations are sampled: ("timed", n) -- every ``every``-th
-    launch of the timed region, n launches -- when the timed region holds at least
-    KERNEL_SAMPLES_MIN of them; else ("after", n_steps): the timed region runs without
-    timing events and an untimed pass of n_steps (>= KERNEL_SAMPLES_MIN samples at the same
-    cadence) follows it.  A 20-step line (the driver's) thus averages 8 launches, not 3."""
+    """Where the step-kernel durations are sampled: ("timed", n, every) -- every
+    ``every``-th launch of the timed region, n launches -- when the timed region holds at
+    least KERNEL_SAMPLES_MIN of them; else ("after", AFTER_STEPS, AFTER_EVERY): the timed
+    region runs without timing events, and behind it AFTER_WARM untimed steps and then a
+    pass of AFTER_STEPS steps sampled every AFTER_EVERY-th launch.  A 20-step line (the
+    driver's) thus averages 8 launches of a steady-state pass."""
     n = (steps + every - 1) // every
     if n >= KERNEL_SAMPLES_MIN:
-        return "timed", n
-    return "after", max(steps, KERNEL_SAMPLES_MIN * every)
+        return "timed", n, every
+    return "after", AFTER_STEPS, AFTER_EVERY
 
 
 def kernel_vs_step(avg_kernel_us, step_us):
-    """A step kernel cannot take longer than the wall time per step of the steps it was
-    sampled in: when the mean says so, the kernel figure is not trusted and the roofline
-    fraction is withheld (None) with the reason."""
+    """A step kernel cannot take longer than a step: the sampled mean is held against the
+    TIMED region's wall time per step (ms_per_step), whichever pass the samples came from.
+    When the mean exceeds it the kernel figure is not trusted and the roofline fraction is
+    withheld (None) with the reason."""
     if not (avg_kernel_us == avg_kernel_us) or not (step_us > 0):  # nan: not timed
         return False, None
-    return avg_kernel_us > step_us, ("mean sampled kernel %.2f us exceeds the %.2f us wall time per step it was "
-                                     "sampled in" % (avg_kernel_us, step_us)) if avg_kernel_us > step_us else None
+    return avg_kernel_us > step_us, ("mean sampled kernel %.2f us exceeds the timed region's %.2f us wall time per "
+                                     "step" % (avg_kernel_us, step_us)) if avg_kernel_us > step_us else None
 
 
 def algorithmic_bytes(L, mode="def", multi=False):
@@ -436,7 +446,7 @@ def main():
     # duration is sampled live over the timed region without a timing event pair
     # (and its cache flush) behind every launch
     every = event_every(K, args.event_every)
-    plan, n_plan = timing_plan(K, every) if args.timing == "dispatch" else ("timed", 0)
+    plan, n_plan, every = timing_plan(K, every) if args.timing == "dispatch" else ("timed", 0, every)
     sampled = set(range(0, K, every)) if args.timing == "marker" else set()
     ev = {k: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for k in sampled}
     eng.episode_stats(clear=True)  # the device accumulates finished episodes of the timed steps
@@ -473,12 +483,13 @@ def main():
     sample_wall = elapsed  # wall time of the steps the kernel samples come from
     n_sample_steps = K
     if plan == "after":
-        # short timed region: it ran without timing events; the kernel mean comes from an
-        # untimed pass of the same kernel right behind it, KERNEL_SAMPLES_MIN samples or more
+        # short timed region: it ran without timing events; the kernel mean comes from a
+        # steady-state pass of the same kernel behind it (AFTER_WARM untimed steps first)
+        run_steps(AFTER_WARM, K)
         eng.kernel_timing((n_plan + every - 1) // every, every)
         torch.cuda.synchronize(dev)
         t1 = time.perf_counter()
-        run_steps(n_plan, K)
+        run_steps(n_plan, K + AFTER_WARM)
         torch.cuda.synchronize(dev)
         sample_wall, n_sample_steps = time.perf_counter() - t1, n_plan
     if args.timing == "dispatch":
@@ -500,7 +511,7 @@ def main():
         value = total_steps / elapsed
         bpe = algorithmic_bytes(L, mode, multi)
         achieved = B * bpe / avg_kernel_s / 1e9
-        exceeds, why = kernel_vs_step(avg_kernel_s * 1e6, sample_step_s * 1e6)
+        exceeds, why = kernel_vs_step(avg_kernel_s * 1e6, elapsed / K * 1e6)
         traffic, traffic_src = measured_traffic(args.workload, B, eng.step_kernel_name, eng.obs_alloc)
         out = {
             "metric": metric,
@@ -525,8 +536,9 @@ def main():
                          "kernel_timing": {"dispatch": "dispatch-packet timestamps of every %dth launch (td_kernel_timing) "
                                                        "%s, %.2f us wall per step there" % (
                                                            every, "of the timed region" if plan == "timed" else
-                                                           "of an untimed %d-step pass right after the timed region "
-                                                           "(the timed steps ran without timing events)" % n_plan,
+                                                           "of an untimed %d-step pass behind the timed region and %d warm "
+                                                           "steps (the timed steps ran without timing events)" % (
+                                                               n_plan, AFTER_WARM),
                                                            sample_step_s * 1e6),
                                            "marker": "torch event pairs around every %dth launch" % every,
                                            "none": "not timed"}[args.timing],

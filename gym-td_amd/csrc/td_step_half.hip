@@ -36,6 +36,14 @@
 
 namespace td {
 
+#ifdef TD_STAMPS  // diagnostic builds: per-phase s_memtime stamps of each board (td_step.hip STAMP slots)
+#define HSTAMP(i) do { if (a.stamps && x.hl == 0) a.stamps[(size_t)b * 16 + (i)] = __builtin_amdgcn_s_memtime(); } while (0)
+#define HSTAMP_AT(bb, i, clk) do { if (a.stamps) a.stamps[(size_t)(bb) * 16 + (i)] = (clk); } while (0)
+#else
+#define HSTAMP(i) do { } while (0)
+#define HSTAMP_AT(bb, i, clk) do { } while (0)
+#endif
+
 // ---------------------------------------------------------------------------
 // the pair's LDS image
 // ---------------------------------------------------------------------------
@@ -440,7 +448,7 @@ constexpr int HS = ECAP / 32;   // enemy slots per lane
 constexpr int kHalfFew = 16;    // enemies up to which the towers target in parallel (td_step.hip kFewEnemies)
 
 template <int NC>
-__device__ __forceinline__ double h_board_step(HalfBoard<NC>& S, HU& u, const HCtx& x) {
+__device__ __forceinline__ double h_board_step(HalfBoard<NC>& S, HU& u, const HCtx& x, const StepArgs& a, int b) {
   const TdDevCfg& C = x.C;
   const int L = x.L, hl = x.hl, h = x.h;
   double reward = dadd(0.0, C.reward_time);                 // :298-299
@@ -498,6 +506,7 @@ __device__ __forceinline__ double h_board_step(HalfBoard<NC>& S, HU& u, const HC
     }
   }
 
+  HSTAMP(3);
   // --- towers fire in list order (:306-313); dead enemies stay targetable.  Tower k
   // lives in lane k of the half (cool-down in a register).
   double tcd = hl < u.nt ? S.tCd[hl] : 0.0;
@@ -617,6 +626,7 @@ __device__ __forceinline__ double h_board_step(HalfBoard<NC>& S, HU& u, const HC
     }
   }
   if (hl < u.nt) S.tCd[hl] = tcd;
+  HSTAMP(4);
 
   // --- kills (:313-317): every enemy at LP 0 was hit this step
   bool alive[HS];
@@ -909,6 +919,7 @@ __device__ __forceinline__ bool h_step_board(HalfBoard<NC>& S, const HCtx& x, co
   const int hl = x.hl;
   uint32_t* const hot = a.opp_hot + (size_t)b * HOT_WORDS;
   HU u;
+  HSTAMP(0);
   h_load_board(S, u, x, a, b, P);
   const int64_t act_in = (int64_t)(((uint64_t)S.stg[STG_ACT + 1] << 32) | S.stg[STG_ACT]);
   // the opponent stream: position, lazy-twist boundary and the pre-drawn outputs (used
@@ -918,6 +929,7 @@ __device__ __forceinline__ bool h_step_board(HalfBoard<NC>& S, const HCtx& x, co
   R.cbase = R.pos;
   R.cache = hl < HOT_CACHE ? S.stg[STG_HOT + 4 + hl] : 0u;
   R.early_issue();
+  HSTAMP(1);
   if (u.num_roads < 1 || u.num_roads > 3) {
     // never reset (its road generation failed): nothing to step.  Every output defined
     // (done, no reward, no action taken); the image is cleared so that the pair's writer
@@ -956,14 +968,17 @@ __device__ __forceinline__ bool h_step_board(HalfBoard<NC>& S, const HCtx& x, co
       if (fail_def == FC_OK) { u.def_cd = C.def_interval; real_def = act; }
     }
   }
+  HSTAMP(11);
   // ---- attacker: the built-in opponent
   h_with_opp_rng(a, b, x, R, [&](auto& G) { h_opponent_enemy(S, u, x, G, a.difficulty); });
+  HSTAMP(12);
   // the towers and map[6] are final: cell words back to HBM if they changed, then packed
   h_store_cells(S, u, x, a, b);
   u.cells_dirty = false;
   h_pack_obs_cells(S, x);
   // ---- TDBoard.step
-  double reward = h_board_step(S, u, x);
+  HSTAMP(2);
+  double reward = h_board_step(S, u, x, a, b);
   R.early_finish();  // the next step's pre-drawn opponent outputs
   const bool done = (u.base_LP <= 0) || (u.steps >= C.max_episode_steps);  // :384-385
   u.ep_ret = dadd(u.ep_ret, reward);
@@ -1006,8 +1021,11 @@ __device__ __forceinline__ bool h_step_board(HalfBoard<NC>& S, const HCtx& x, co
     sst(&hot[3], R.cbase);
   }
   if (hl < HOT_CACHE) sst(&hot[4 + hl], R.cache);
+  HSTAMP(5);
   h_enemy_stats(S, u, x);
+  HSTAMP(13);
   h_channel_scalars(S, u, x);
+  HSTAMP(14);
   if (was_reset) {  // the new episode's layout
     h_store_cells(S, u, x, a, b);
     h_pack_obs_cells(S, x);
@@ -1203,6 +1221,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
   const int p = a.xcd_map ? xcd_board((int)blockIdx.x, npair) : (int)blockIdx.x;
   const int lane = (int)threadIdx.x & 63, h = lane >> 5, hl = lane & 31;
   const int b = 2 * p + h;
+#ifdef TD_STAMPS
+  const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
+#endif
   static_assert(sizeof(TdDevCfg) % 16 == 0 && sizeof(TdDevCfg) <= 64 * 16, "cfg staging");
   if (lane < (int)(sizeof(TdDevCfg) / 16))
     reinterpret_cast<uint4*>(&SP.cfg)[lane] = reinterpret_cast<const uint4*>(a.cfg)[lane];
@@ -1218,8 +1239,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
   const uint64_t am = __ballot(anyE);
   const bool two = 2 * p + 1 < a.B;
   constexpr int N4 = NCH * LT * LT / 4;
+#ifdef TD_STAMPS
+  if (hl == 0 && b < a.B) { HSTAMP_AT(b, 6, __builtin_amdgcn_s_memtime()); HSTAMP_AT(b, 9, rt0); }
+#endif
   write_obs_pair<NC, LT>(SP, lane, a.obs + (size_t)2 * p * NCH * NC, two ? 2 * N4 : N4, (am & 1ull) != 0,
                          ((am >> 32) & 1ull) != 0, a.obs_wt != 0, a.edge_wt);
+#ifdef TD_STAMPS
+  if (hl == 0 && b < a.B) {
+    const uint64_t t = __builtin_amdgcn_s_memtime();
+    HSTAMP_AT(b, 7, t); HSTAMP_AT(b, 8, t); HSTAMP_AT(b, 10, __builtin_amdgcn_s_memrealtime());
+  }
+#endif
 }
 
 bool half_supported(const StepArgs& a) { return a.L == 10 && a.mode == MODE_DEF && !a.multi; }

@@ -14,6 +14,9 @@ mode = sys.argv[4] if len(sys.argv) > 4 else "def"
 multi = len(sys.argv) > 5 and sys.argv[5] == "1"
 seeds = np.arange(B) + 11
 eng = TDEngine(L, B, mode, multi, 1, np_seeds=seeds, py_seeds=seeds, autoreset=True, info=not multi)
+if os.environ.get("TD_PROBE_KERNEL"):  # force a step kernel (td_set_step_kernel)
+    eng.set_step_kernel(os.environ["TD_PROBE_KERNEL"])
+print("kernel", eng.step_kernel_name)
 eng.reset_all()
 g = torch.Generator(device="cuda").manual_seed(0)
 if multi:  # a few pre-drawn flag batches, cycled (bench.py's 2p-middle-multi shape)

@@ -31,5 +31,13 @@ s1)  # the stripped build + the half-wave kernel: its parity first, the GPU suit
   run probe_timing_65536 300 python scripts/probe_timing.py 65536 || exit 1; cat $O/probe_timing_65536.log | tail -1 | cut -c1-3000
   run probe_timing_8192 300 python scripts/probe_timing.py 8192 || exit 1; cat $O/probe_timing_8192.log | tail -1 | cut -c1-3000
   ;;
+s2)  # phase stamps of the half-wave kernel vs the one-wave kernels; the driver's command with the new kernel timing
+  for k in small half; do for bb in 8192 4096; do
+    TD_PROBE_KERNEL=$k TDSTEP_LIB=$PWD/gym-td_amd/lib/libtdstep_stamps.so run phases_${k}_$bb 300 python scripts/probe_phases.py $bb 10 600 || exit 1
+    cat $O/phases_${k}_$bb.log
+  done; done
+  run bench_driver 300 python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline || exit 1; line bench_driver
+  grep -o '"kernel_timing": "[^"]*"' $O/bench_driver.log
+  ;;
 *) echo "unknown session $S"; exit 2;;
 esac

@@ -88,18 +88,19 @@ def test_gpus_n_starts_n_ranks(monkeypatch):
 
 
 def test_short_runs_sample_enough_launches():
-    # the driver's 20-step line: no events in the timed region, an untimed pass of 64 steps
-    # sampled every 8th launch (8 samples) behind it
-    assert bench.timing_plan(20, 8) == ("after", 64)
-    assert bench.timing_plan(32, 8) == ("after", 64)
-    assert bench.timing_plan(64, 8) == ("timed", 8)
-    assert bench.timing_plan(2000, 8) == ("timed", 250)
-    assert bench.timing_plan(5, 1) == ("after", 8)
+    # the driver's 20-step line: no events in the timed region; 16 warm steps, then a
+    # 256-step pass sampled every 32nd launch (8 samples) behind it
+    assert bench.timing_plan(20, 8) == ("after", 256, 32)
+    assert bench.timing_plan(32, 8) == ("after", 256, 32)
+    assert bench.timing_plan(64, 8) == ("timed", 8, 8)
+    assert bench.timing_plan(2000, 8) == ("timed", 250, 8)
+    assert bench.timing_plan(5, 1) == ("after", 256, 32)
+    assert bench.AFTER_STEPS // bench.AFTER_EVERY >= bench.KERNEL_SAMPLES_MIN
 
 
 def test_kernel_longer_than_the_step_withholds_the_fraction():
     assert bench.kernel_vs_step(225.9, 221.8)[0] is True
-    assert "exceeds" in bench.kernel_vs_step(225.9, 221.8)[1]
+    assert "exceeds the timed region" in bench.kernel_vs_step(225.9, 221.8)[1]
     assert bench.kernel_vs_step(215.0, 221.8) == (False, None)
     assert bench.kernel_vs_step(float("nan"), 221.8) == (False, None)
 
