@@ -908,29 +908,62 @@ __device__ __forceinline__ void h_load_board(HalfBoard<NC>& S, HU& u, const HCtx
 }
 
 // ---------------------------------------------------------------------------
-// one board's step (td_step.hip step_board, MODE_DEF, small-batch schedule)
+// one board's step (td_step.hip step_board, MODE_DEF, small-batch schedule), in two parts
+// around the pair's early observation pass
 // ---------------------------------------------------------------------------
-// Leaves the board's packed image (cells, group statistics, broadcast channels) in LDS
-// for the pair's observation writer; returns whether the board has enemies.
+// What a board's step carries from part A to part B.
+struct HStep {
+  HU u;
+  int fail_def;
+  int64_t real_def;
+  bool live;     // the board has a layout (else: never reset, nothing stepped)
+  bool enemies;  // enemies on the board after the actions (the enemy planes and channel 5 wait for the step)
+};
+
+// The broadcast channels as they will read after the step, computed before it: the step
+// changes the costs only by its closing cost update (TDBoard.py:348-353), which depends on
+// nothing the step decides, and base_LP only when an enemy leaks (channel 5: exact for a
+// board without enemies; written late for the others).
+template <int NC>
+__device__ __forceinline__ void h_early_scalars(HalfBoard<NC>& S, const HU& u, const HCtx& x) {
+  const TdDevCfg& C = x.C;
+  HU v = u;
+  v.steps = u.steps + 1;
+  v.progress = ddiv((double)v.steps, (double)C.max_episode_steps);
+  double rate;
+  if (v.progress >= 0.5) rate = C.atk_final_rate;
+  else rate = dadd(dmul(C.atk_init_rate, dsub(1.0, v.progress)), dmul(C.atk_final_rate, v.progress));
+  v.cost_atk = pymin(dadd(u.cost_atk, rate), u.max_cost);
+  v.cost_def = pymin(dadd(u.cost_def, C.def_rate), u.max_cost);
+  h_channel_scalars(S, v, x);
+}
+
+// Part A: load, cool-downs, the defender's action and the built-in attacker; the cell words
+// packed for the observation and the broadcast channels as they will read after the step.
 template <int NC, int LT>
-__device__ __forceinline__ bool h_step_board(HalfBoard<NC>& S, const HCtx& x, const StepArgs& a, int b,
-                                             const HPrefetch& P) {
+__device__ __forceinline__ void h_step_a(HalfBoard<NC>& S, const HCtx& x, const StepArgs& a, int b, const HPrefetch& P,
+                                         HStep& T, HalfMt& R) {
   const TdDevCfg& C = x.C;
   const int hl = x.hl;
-  uint32_t* const hot = a.opp_hot + (size_t)b * HOT_WORDS;
-  HU u;
+  HU& u = T.u;
   HSTAMP(0);
   h_load_board(S, u, x, a, b, P);
   const int64_t act_in = (int64_t)(((uint64_t)S.stg[STG_ACT + 1] << 32) | S.stg[STG_ACT]);
   // the opponent stream: position, lazy-twist boundary and the pre-drawn outputs (used
   // only when they start at the current position) from the hot record
-  HalfMt R{a.opp_mt + (size_t)b * OPP_WORDS, S.stg[STG_HOT + 0], S.stg[STG_HOT + 1], hl, x.h, x.lane};
+  R.w = a.opp_mt + (size_t)b * OPP_WORDS;
+  R.pos = S.stg[STG_HOT + 0];
+  R.tw = S.stg[STG_HOT + 1];
   R.cn = S.stg[STG_HOT + 3] == R.pos ? S.stg[STG_HOT + 2] : 0u;
   R.cbase = R.pos;
   R.cache = hl < HOT_CACHE ? S.stg[STG_HOT + 4 + hl] : 0u;
   R.early_issue();
   HSTAMP(1);
-  if (u.num_roads < 1 || u.num_roads > 3) {
+  T.live = u.num_roads >= 1 && u.num_roads <= 3;
+  T.enemies = false;
+  T.fail_def = 0;
+  T.real_def = (int64_t)6 * x.NCr;
+  if (!T.live) {
     // never reset (its road generation failed): nothing to step.  Every output defined
     // (done, no reward, no action taken); the image is cleared so that the pair's writer
     // emits an all-zero observation for this board.
@@ -950,13 +983,11 @@ __device__ __forceinline__ bool h_step_board(HalfBoard<NC>& S, const HCtx& x, co
     for (int i = hl; i < 48; i += 32) S.chv[i] = 0.0f;
     if (hl == 0) S.d9[0] = 0.0f;
     wsync();
-    return false;
+    return;
   }
   u.atk_cd = u.atk_cd - 1 > 0 ? u.atk_cd - 1 : 0;
   u.def_cd = u.def_cd - 1 > 0 ? u.def_cd - 1 : 0;
   const int64_t empty_def = (int64_t)6 * x.NCr;
-  int fail_def = 0;
-  int64_t real_def = empty_def;
   // ---- defender (TDDefense.py:40-77): op = act // L^2, row, column
   {
     int64_t act = act_in;
@@ -964,8 +995,8 @@ __device__ __forceinline__ bool h_step_board(HalfBoard<NC>& S, const HCtx& x, co
     if (u.def_cd == 0 && act != empty_def) {
       const int a32 = (int)act;
       const int op = a32 / (LT * LT);
-      fail_def = h_defender_op(S, u, x, op, a32 - op * LT * LT);
-      if (fail_def == FC_OK) { u.def_cd = C.def_interval; real_def = act; }
+      T.fail_def = h_defender_op(S, u, x, op, a32 - op * LT * LT);
+      if (T.fail_def == FC_OK) { u.def_cd = C.def_interval; T.real_def = act; }
     }
   }
   HSTAMP(11);
@@ -976,7 +1007,19 @@ __device__ __forceinline__ bool h_step_board(HalfBoard<NC>& S, const HCtx& x, co
   h_store_cells(S, u, x, a, b);
   u.cells_dirty = false;
   h_pack_obs_cells(S, x);
-  // ---- TDBoard.step
+  T.enemies = u.n > 0;
+  h_early_scalars(S, u, x);
+}
+
+// Part B: TDBoard.step, done, auto-reset, the board's state and outputs, the group
+// statistics and the final broadcast channels.  Returns whether the board was reset.
+template <int NC, int LT>
+__device__ __forceinline__ bool h_step_b(HalfBoard<NC>& S, const HCtx& x, const StepArgs& a, int b, HStep& T,
+                                         HalfMt& R) {
+  const TdDevCfg& C = x.C;
+  const int hl = x.hl;
+  HU& u = T.u;
+  uint32_t* const hot = a.opp_hot + (size_t)b * HOT_WORDS;
   HSTAMP(2);
   double reward = h_board_step(S, u, x, a, b);
   R.early_finish();  // the next step's pre-drawn opponent outputs
@@ -1044,8 +1087,8 @@ __device__ __forceinline__ bool h_step_board(HalfBoard<NC>& S, const HCtx& x, co
     if (a.win) sst(&a.win[b], win);
     if (a.allow_next) sst(&a.allow_next[b], allow);
     if (a.cooldowns) sst(&a.cooldowns[b], cool);
-    if (a.fail_def) sst(&a.fail_def[b], (int32_t)fail_def);
-    if (a.real_def) sst(&a.real_def[b], real_def);
+    if (a.fail_def) sst(&a.fail_def[b], (int32_t)T.fail_def);
+    if (a.real_def) sst(&a.real_def[b], T.real_def);
     if (a.ep_return) sst(&a.ep_return[b], ep_ret);
     if (a.ep_len) sst(&a.ep_len[b], (int32_t)ep_steps);
     if (done && a.last_ep) {  // the board's last finished episode (td_episode_records)
@@ -1060,7 +1103,8 @@ __device__ __forceinline__ bool h_step_board(HalfBoard<NC>& S, const HCtx& x, co
       atomicAdd(&a.ep_stats[1], ep_ret);
     }
   }
-  return u.n > 0;
+  T.u.n = u.n;
+  return was_reset;
 }
 
 // ---------------------------------------------------------------------------
@@ -1094,16 +1138,29 @@ struct PairWinTab {
   static constexpr T tab = make();
 };
 
+// Channels the step itself decides for a board with enemies: base_LP (5) and the enemy_LP
+// planes (25-40).  Everything else of the observation is final once the actions are.
+__device__ __forceinline__ bool late_channel(int ch) { return ch == 5 || (unsigned)(ch - 25) < 16u; }
+
+// What the pair writer knows of each board: any[] enemies after the step (the group
+// statistics are in LDS), en[] enemies after the actions (late channels), rs[] reset.
+struct PairFlags {
+  bool any0, any1, en0, en1, rs0, rs1;
+};
+
 // The pair's (2, 45, L, L) observation in 128-B-aligned 1-KB windows by the whole wave
 // (td_step.hip write_obs_lines over two board images): lane unit i of the stretch is
 // board i / N4's unit i % N4 (channel, quad of 4 cells).  nunits: N4 when the pair has
 // one board (an odd batch's last wave: its units beyond are dropped by the buffer range).
-// wt: every line write-through (the batch's observation fits the Infinity Cache); else
-// whole lines non-temporal and the two lines shared with neighbouring pairs as plain
-// write-back (edge_wt 2) or write-through (1) stores.
-template <int NC, int LT, int G = 4>
-__device__ __forceinline__ void write_obs_pair(const PairSmem<NC>& SP, int lane, float* out, int nunits, bool any0,
-                                               bool any1, bool wt, int edge_wt) {
+// PASS 0: every unit; 1 (early, before the board steps): every unit but the late channels
+// of a board with enemies; 2 (late): those, and every unit of a board that was reset.
+// Windows no lane of which stores in this pass are skipped.  wt: every line write-through
+// (the batch's observation fits the Infinity Cache); else whole lines non-temporal and the
+// two lines shared with neighbouring pairs as plain write-back (edge_wt 2) or
+// write-through (1) stores.
+template <int NC, int LT, int PASS, int G = 4>
+__device__ __forceinline__ void write_obs_pair(const PairSmem<NC>& SP, int lane, float* out, int nunits,
+                                               const PairFlags& f, bool wt, int edge_wt) {
   static_assert(LT >= 8, "a 128-B line spans at most two channel planes");
   using Tab = PairWinTab<LT>;
   constexpr int Q = Tab::Q, N4 = Tab::N4, N2 = Tab::N2, K = Tab::K;
@@ -1123,9 +1180,18 @@ __device__ __forceinline__ void write_obs_pair(const PairSmem<NC>& SP, int lane,
   const int i0 = lane - mis;
   auto wclass = [&](int k) { return (Tab::tab.w[mis][k >> 3] >> (4 * (k & 7))) & 7u; };
   auto unit = [&](int i, uint32_t wc) { return (wc & 4u) ? (i < 0 ? 0 : (i > N2 - 1 ? N2 - 1 : i)) : i; };
+  // this pass's units of a lane (board bd, channel ch)
+  auto wanted = [&](int bd, int ch) {
+    if constexpr (PASS == 0) return true;
+    const bool en = bd ? f.en1 : f.en0;
+    if constexpr (PASS == 1) return !(en && late_channel(ch));
+    const bool r = bd ? f.rs1 : f.rs0;
+    return r || (en && late_channel(ch));
+  };
   for (int k0 = 0; k0 < K; k0 += G) {
     uint4 A[G];
     uint32_t W[G];
+    uint32_t skip = 0;  // wave-uniform: windows of the group with no unit to store in this pass
 #pragma unroll
     for (int j = 0; j < G; ++j) {
       const int k = k0 + j;
@@ -1134,6 +1200,7 @@ __device__ __forceinline__ void write_obs_pair(const PairSmem<NC>& SP, int lane,
         const int i = unit(i0 + 64 * k, wc);
         const int bd = i >= N4 ? 1 : 0, ib = i - bd * N4;
         const int ch = ib / Q, q = ib - ch * Q;
+        if (PASS != 0 && !__ballot(wanted(bd, ch))) { skip |= 1u << j; continue; }
         const int base = bd * BSZ;
         A[j] = *reinterpret_cast<const uint4*>(sb + base + o_cell + 16 * q);
         if ((wc & 3u) == 1) {
@@ -1150,14 +1217,14 @@ __device__ __forceinline__ void write_obs_pair(const PairSmem<NC>& SP, int lane,
 #pragma unroll
     for (int j = 0; j < G; ++j) {
       const int k = k0 + j;
-      if (!(K % G == 0 || k < K)) continue;
+      if (!(K % G == 0 || k < K) || ((skip >> j) & 1u)) continue;
       const uint32_t wc = wclass(k);
       const bool edge = (wc & 4u) != 0;
       const int i = i0 + 64 * k;
       const int iu = unit(i, wc);
       const int bd = iu >= N4 ? 1 : 0, ib = iu - bd * N4, ch = ib / Q;
       const int base = bd * BSZ;
-      const bool anyE = bd ? any1 : any0;
+      const bool anyE = bd ? f.any1 : f.any0;
       const int e = ch - 25;
       const bool isen = (unsigned)e < 16u, isd9 = ch == 9, isbin = ((kChBin >> ch) & 1ull) != 0;
       const uint32_t a4[4] = {A[j].x, A[j].y, A[j].z, A[j].w};
@@ -1179,8 +1246,8 @@ __device__ __forceinline__ void write_obs_pair(const PairSmem<NC>& SP, int lane,
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
           const uint32_t g = (W[j] >> (8 * c)) & 0xffu;
-          const float f = *reinterpret_cast<const float*>(sb + base + o_gst + 16 * (int)(g & 0x7fu) + 4 * ((e >> 2) & 3));
-          v[c] = g != 0xffu ? f : 0.0f;
+          const float fv = *reinterpret_cast<const float*>(sb + base + o_gst + 16 * (int)(g & 0x7fu) + 4 * ((e >> 2) & 3));
+          v[c] = g != 0xffu ? fv : 0.0f;
         }
       } else {
         const float cv = isen ? 0.0f : __uint_as_float(W[j]);
@@ -1188,7 +1255,8 @@ __device__ __forceinline__ void write_obs_pair(const PairSmem<NC>& SP, int lane,
         for (int c = 0; c < 4; ++c) v[c] = cv;
       }
       const f32x4 val = f32x4{v[0], v[1], v[2], v[3]};
-      const uint32_t off = (uint32_t)i * 16u;  // i < 0 or i >= nunits: out of range already
+      // i < 0 or i >= nunits: out of range already; a unit of another pass: dropped
+      const uint32_t off = wanted(bd, ch) ? (uint32_t)i * 16u : OOB;
       if (wt) {
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, val), rs, off, 0, 16 /* sc1 */);
       } else if (!edge) {
@@ -1209,7 +1277,12 @@ __device__ __forceinline__ void write_obs_pair(const PairSmem<NC>& SP, int lane,
 // the kernel: wave w steps boards 2p and 2p + 1 of its XCD-mapped pair p
 // ---------------------------------------------------------------------------
 // 16 waves per CU (LDS: 8.9 KB per pair), so 4,096 waves = 8,192 boards run as one round;
-// up to 128 VGPRs per lane.
+// up to 128 VGPRs per lane.  Where the batch's observation fits the Infinity Cache
+// (write-through stores) the pair writes all it can right after the actions -- the whole
+// observation of a board without enemies -- so the store stream drains while the boards
+// step (a one-round grid otherwise starts storing only once its first boards finish
+// stepping); the channels the step decides follow after it.  Larger batches write each
+// pair once, after the step.
 template <int LT, int MODE, bool SCAN>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void td_step_kernel_half(StepArgs a_) {
   static_assert(LT == 10 && MODE == MODE_DEF && !SCAN, "the half-wave step is built for TD-def discrete at L = 10");
@@ -1228,24 +1301,47 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
   if (lane < (int)(sizeof(TdDevCfg) / 16))
     reinterpret_cast<uint4*>(&SP.cfg)[lane] = reinterpret_cast<const uint4*>(a.cfg)[lane];
   wsync();
-  bool anyE = false;
-  if (b < a.B) {
-    const HCtx x{SP.cfg, LT, NC, lane, hl, h, a.cfgs, a.epoch};
-    HPrefetch P;
-    h_prefetch<NC>(P, a, b, hl);
-    anyE = h_step_board<NC, LT>(SP.hb[h], x, a, b, P);
-  }
-  wsync();
-  const uint64_t am = __ballot(anyE);
+  const bool mine = b < a.B;
   const bool two = 2 * p + 1 < a.B;
   constexpr int N4 = NCH * LT * LT / 4;
+  float* const out = a.obs + (size_t)2 * p * NCH * NC;
+  const int nunits = two ? 2 * N4 : N4;
+  const bool early = a.obs_wt != 0;
+  const HCtx x{SP.cfg, LT, NC, lane, hl, h, a.cfgs, a.epoch};
+  HStep T;
+  HalfMt R{nullptr, 0u, 0u, hl, h, lane};
+  T.live = false;
+  T.enemies = false;
+  if (mine) {
+    HPrefetch P;
+    h_prefetch<NC>(P, a, b, hl);
+    h_step_a<NC, LT>(SP.hb[h], x, a, b, P, T, R);
+  }
+  wsync();
+  PairFlags f{false, false, false, false, false, false};
+  {
+    const uint64_t em = __ballot(T.enemies);
+    f.en0 = (em & 1ull) != 0;
+    f.en1 = ((em >> 32) & 1ull) != 0;
+  }
+  if (early) write_obs_pair<NC, LT, 1>(SP, lane, out, nunits, f, true, a.edge_wt);
+  bool reset = false;
+  if (mine && T.live) reset = h_step_b<NC, LT>(SP.hb[h], x, a, b, T, R);
+  wsync();
+  {
+    const uint64_t am = __ballot(T.live && T.u.n > 0), rm = __ballot(reset);
+    f.any0 = (am & 1ull) != 0;
+    f.any1 = ((am >> 32) & 1ull) != 0;
+    f.rs0 = (rm & 1ull) != 0;
+    f.rs1 = ((rm >> 32) & 1ull) != 0;
+  }
 #ifdef TD_STAMPS
-  if (hl == 0 && b < a.B) { HSTAMP_AT(b, 6, __builtin_amdgcn_s_memtime()); HSTAMP_AT(b, 9, rt0); }
+  if (hl == 0 && mine) { HSTAMP_AT(b, 6, __builtin_amdgcn_s_memtime()); HSTAMP_AT(b, 9, rt0); }
 #endif
-  write_obs_pair<NC, LT>(SP, lane, a.obs + (size_t)2 * p * NCH * NC, two ? 2 * N4 : N4, (am & 1ull) != 0,
-                         ((am >> 32) & 1ull) != 0, a.obs_wt != 0, a.edge_wt);
+  if (early) write_obs_pair<NC, LT, 2>(SP, lane, out, nunits, f, true, a.edge_wt);
+  else write_obs_pair<NC, LT, 0>(SP, lane, out, nunits, f, false, a.edge_wt);
 #ifdef TD_STAMPS
-  if (hl == 0 && b < a.B) {
+  if (hl == 0 && mine) {
     const uint64_t t = __builtin_amdgcn_s_memtime();
     HSTAMP_AT(b, 7, t); HSTAMP_AT(b, 8, t); HSTAMP_AT(b, 10, __builtin_amdgcn_s_memrealtime());
   }

@@ -39,5 +39,16 @@ s2)  # phase stamps of the half-wave kernel vs the one-wave kernels; the driver'
   run bench_driver 300 python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline || exit 1; line bench_driver
   grep -o '"kernel_timing": "[^"]*"' $O/bench_driver.log
   ;;
+s3)  # half-wave kernel with the early observation pass: its parity, phase stamps, lines beside the one-wave kernels
+  run pytest_half 900 python -u -m pytest tests -m gpu -q -k "half" --timeout 400 --timeout-method thread -p no:cacheprovider
+  rc=$?; grep -E "^(FAILED|E  )" $O/pytest_half.log | head -30; tail -1 $O/pytest_half.log; [ $rc -le 1 ] || exit $rc
+  for bb in 8192 4096; do
+    TD_PROBE_KERNEL=half TDSTEP_LIB=$PWD/gym-td_amd/lib/libtdstep_stamps.so run phases_half_$bb 300 python scripts/probe_phases.py $bb 10 600 || exit 1
+    grep -E "obs|rt |attacker|march" $O/phases_half_$bb.log
+  done
+  for r in 1 2; do for bb in 8192 4096 16384 32768; do for k in auto half; do
+    run ${k}_${bb}_$r 200 python bench.py --global-batch $bb --no-cpu-baseline --steps $((bb > 20000 ? 500 : 2000)) --timing none --step-kernel $k || exit 1; line ${k}_${bb}_$r
+  done; done; done
+  ;;
 *) echo "unknown session $S"; exit 2;;
 esac
