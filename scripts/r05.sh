@@ -46,8 +46,8 @@ s3)  # half-wave kernel with the early observation pass: its parity, phase stamp
     TD_PROBE_KERNEL=half TDSTEP_LIB=$PWD/gym-td_amd/lib/libtdstep_stamps.so run phases_half_$bb 300 python scripts/probe_phases.py $bb 10 600 || exit 1
     grep -E "obs|rt |attacker|march" $O/phases_half_$bb.log
   done
-  for r in 1 2; do for bb in 8192 4096 16384 32768; do for k in auto half; do
-    run ${k}_${bb}_$r 200 python bench.py --global-batch $bb --no-cpu-baseline --steps $((bb > 20000 ? 500 : 2000)) --timing none --step-kernel $k || exit 1; line ${k}_${bb}_$r
+  for r in 1 2; do for bb in 8192 4096 16384 32768 65536; do for k in auto half; do
+    run ${k}_${bb}_$r 200 python bench.py --global-batch $bb --no-cpu-baseline --steps $((bb > 40000 ? 300 : bb > 20000 ? 500 : 2000)) --timing none --step-kernel $k || exit 1; line ${k}_${bb}_$r
   done; done; done
   ;;
 *) echo "unknown session $S"; exit 2;;
