@@ -1306,7 +1306,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
   constexpr int N4 = NCH * LT * LT / 4;
   float* const out = a.obs + (size_t)2 * p * NCH * NC;
   const int nunits = two ? 2 * N4 : N4;
-  const bool early = a.obs_wt != 0;
+#ifndef TD_HALF_EARLY  // (temporary A/B macro, round 5: the early observation pass)
+#define TD_HALF_EARLY 1
+#endif
+  const bool early = TD_HALF_EARLY && a.obs_wt != 0;
   const HCtx x{SP.cfg, LT, NC, lane, hl, h, a.cfgs, a.epoch};
   HStep T;
   HalfMt R{nullptr, 0u, 0u, hl, h, lane};

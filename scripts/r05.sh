@@ -50,5 +50,16 @@ s3)  # half-wave kernel with the early observation pass: its parity, phase stamp
     run ${k}_${bb}_$r 200 python bench.py --global-batch $bb --no-cpu-baseline --steps $((bb > 40000 ? 300 : bb > 20000 ? 500 : 2000)) --timing none --step-kernel $k || exit 1; line ${k}_${bb}_$r
   done; done; done
   ;;
+s4)  # why the half-wave kernel is slow: SQ counters of small / half / half without the early pass at 8,192 boards
+  V=$PWD/gym-td_amd/lib/variants
+  for v in small half noearly; do
+    lib=$PWD/gym-td_amd/lib/libtdstep.so; k=$v; [ $v = noearly ] && { lib=$V/libtdstep_noearly.so; k=half; }
+    BENCH="python bench.py --global-batch 8192 --steps 20 --warmup 2 --burnin 300 --no-cpu-baseline --timing none --step-kernel $k"
+    TDSTEP_LIB=$lib run pmc1_$v 120 timeout -s KILL 100 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_SMEM SQ_INSTS_VMEM_WR -d $O/pmc1_$v -o pmc --output-format csv -- $BENCH || exit 1
+    TDSTEP_LIB=$lib run pmc2_$v 120 timeout -s KILL 100 rocprofv3 --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_IFETCH SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE -d $O/pmc2_$v -o pmc --output-format csv -- $BENCH || exit 1
+    TDSTEP_LIB=$lib run kt_$v 120 timeout -s KILL 100 rocprofv3 --kernel-trace --stats -d $O/kt_$v -o kt --output-format csv -- $BENCH || exit 1
+  done
+  TDSTEP_LIB=$V/libtdstep_noearly.so run nb_8192 200 python bench.py --global-batch 8192 --no-cpu-baseline --steps 2000 --timing none --step-kernel half; line nb_8192
+  ;;
 *) echo "unknown session $S"; exit 2;;
 esac
