@@ -61,5 +61,9 @@ s4)  # why the half-wave kernel is slow: SQ counters of small / half / half with
   done
   TDSTEP_LIB=$V/libtdstep_noearly.so run nb_8192 200 python bench.py --global-batch 8192 --no-cpu-baseline --steps 2000 --timing none --step-kernel half; line nb_8192
   ;;
+s5)  # placement of the observation: offsets into one contiguous block, 30x30 / 16,384 and 10x10 / 65,536
+  run off30 400 python scripts/probe_offset.py 30 16384 100 || exit 1; grep -h offset $O/off30.log | tr '\n' ' '; echo
+  run off10 400 python scripts/probe_offset.py 10 65536 200 || exit 1; grep -h offset $O/off10.log | tr '\n' ' '; echo
+  ;;
 *) echo "unknown session $S"; exit 2;;
 esac
