@@ -59,6 +59,10 @@ s4)  # why the half-wave kernel is slow: SQ counters of small / half / half with
     TDSTEP_LIB=$lib run pmc2_$v 120 timeout -s KILL 100 rocprofv3 --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_IFETCH SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE -d $O/pmc2_$v -o pmc --output-format csv -- $BENCH || exit 1
     TDSTEP_LIB=$lib run kt_$v 120 timeout -s KILL 100 rocprofv3 --kernel-trace --stats -d $O/kt_$v -o kt --output-format csv -- $BENCH || exit 1
   done
+  python3 scripts/pmc_compare.py $O small half noearly > $O/pmc_compare.txt 2>&1; cat $O/pmc_compare.txt
+  for v in small half noearly; do for d in pmc1 pmc2 kt; do
+    find $O/${d}_$v -name "*stats.csv" -exec cp {} $O/${d}_${v}_stats.csv \; 2>/dev/null; rm -rf $O/${d}_$v
+  done; done
   TDSTEP_LIB=$V/libtdstep_noearly.so run nb_8192 200 python bench.py --global-batch 8192 --no-cpu-baseline --steps 2000 --timing none --step-kernel half; line nb_8192
   ;;
 s5)  # placement of the observation: offsets into one contiguous block, 30x30 / 16,384 and 10x10 / 65,536
