@@ -375,7 +375,7 @@ def main():
                          "(td_kernel_timing, the dispatch-packet timestamps rocprofv3 reports; k: --event-every); "
                          "'marker' = torch event pairs around every k-th launch (adds the marker packets' "
                          "overhead); 'none' = no kernel timing (diagnostic A/B of the step rate)")
-    ap.add_argument("--step-kernel", default="auto", choices=("auto", "large", "small", "small2", "half"),
+    ap.add_argument("--step-kernel", default="auto", choices=("auto", "large", "small", "small2"),
                     help="diagnostic: force a step kernel (td_set_step_kernel); default td_create's rule")
     ap.add_argument("--event-every", type=int, default=None,
                     help="timed launches per sampled kernel duration (default 8; every launch perturbs the step)")

@@ -1,7 +1,7 @@
-// td_board.h -- the board rules and observation encoding both step-kernel families share
-// (td_step.hip: one wave per board; td_step_half.hip: one half-wave per board): fail codes,
-// the tower nibble of an LDS cell word, Chebyshev distance, Enemy.damage, and the binary /
-// broadcast / distance / enemy channel classes of the (45, L, L) observation.
+// td_board.h -- board rules and observation encoding of the step kernels (td_step.hip):
+// fail codes, the tower nibble of an LDS cell word, Chebyshev distance, Enemy.damage, the
+// binary / broadcast / distance / enemy channel classes of the (45, L, L) observation, the
+// dry-ring wait and the kernarg-segment read of the step arguments.
 #pragma once
 #include <hip/hip_runtime.h>
 

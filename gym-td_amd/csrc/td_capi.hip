@@ -247,10 +247,7 @@ int apply_kernel(td_handle* h, int small) {
   // slower steps at 16,384-65,536 boards, profiles/r03/s21.)
   h->obs_wt = h->small && obs_bytes <= 192.0 * 1024 * 1024 ? 1 : 0;
   const bool has_small = h->L == 10 || h->L == 20 || h->L == 30;
-  const char* k = !has_small || small == 0 ? "td_step_kernel"
-                  : small == 1           ? "td_step_kernel_small"
-                  : small == 2           ? "td_step_kernel_small2"
-                                         : "td_step_kernel_half";
+  const char* k = !has_small || small == 0 ? "td_step_kernel" : small == 1 ? "td_step_kernel_small" : "td_step_kernel_small2";
   char buf[96];
   std::snprintf(buf, sizeof buf, "%s<%d, %d, %s>", k, has_small ? h->L : 0, h->mode, h->multi ? "true" : "false");
   h->kernel_name = buf;
@@ -765,11 +762,9 @@ int td_step(td_handle* h, const td_step_io* io, void* stream) {
 
 int td_set_step_kernel(td_handle* h, int kind) {
   if (!h) return fail("NULL handle");
-  if (kind < TD_KERNEL_AUTO || kind > TD_KERNEL_HALF) return fail("td_set_step_kernel: unknown kernel kind %d", kind);
+  if (kind < TD_KERNEL_AUTO || kind > TD_KERNEL_SMALL2) return fail("td_set_step_kernel: unknown kernel kind %d", kind);
   if (kind >= TD_KERNEL_SMALL && h->L != 10 && h->L != 20 && h->L != 30)
     return fail("td_set_step_kernel: L = %d has no small-batch step kernel (only L = 10 / 20 / 30)", h->L);
-  if (kind == TD_KERNEL_HALF && !half_supported(base_args(h)))
-    return fail("td_set_step_kernel: the half-wave kernel is built for TD-def discrete boards at L = 10");
   HIP_OK(hipDeviceSynchronize());  // launches already queued keep the kernel they were enqueued with
   return apply_kernel(h, kind == TD_KERNEL_AUTO ? h->small_auto : kind - 1);
 }

@@ -17,7 +17,7 @@ constexpr int HOT_WORDS = 4 + HOT_CACHE;
 struct StepArgs {
   int B, L, mode, multi, difficulty, autoreset;
   int opp_np;           // random_agent=False: the built-in opponents draw from np_mt (auto-reset off)
-  int small;            // 0 td_step_kernel, 1 td_step_kernel_small, 2 td_step_kernel_small2, 3 td_step_kernel_half
+  int small;            // 0 td_step_kernel, 1 td_step_kernel_small, 2 td_step_kernel_small2
   int obs_wt;           // small kernel: observation stores write-through (the batch's obs fits the MALL)
   TdHdr* hdr;
   double* en_lp;
@@ -88,11 +88,6 @@ __host__ __device__ inline int xcd_board(int i, int B) {
 
 // ev0 / ev1: optional timing events bound to the step kernel's dispatch (td_kernel_timing).
 hipError_t launch_step(const StepArgs& a, hipStream_t s, bool reset, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
-// The half-wave step kernel (td_step_half.hip: two boards per wave, one per 32-lane half):
-// built for TD-def discrete at L = 10; boards resident at once on `cus` compute units.
-bool half_supported(const StepArgs& a);
-hipError_t launch_step_half(const StepArgs& a, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1);
-int half_resident_boards(const StepArgs& a, int cus);
 // Small-batch step-kernel workgroups (one per board) resident at once on `cus` compute
 // units, for the one-wave (td_step_kernel_small) or two-wave (td_step_kernel_small2) build.
 int step_resident_boards(const StepArgs& a, int cus, int waves);

@@ -2310,8 +2310,6 @@ static hipError_t launch2(const StepArgs& a, hipStream_t s, bool reset, hipEvent
   const bool aligned = (reinterpret_cast<uintptr_t>(a.obs) & 15u) == 0;
   if (reset) {
     hipLaunchKernelGGL(td_reset_kernel<LT>, dim3(a.B), dim3(64), 0, s, a);
-  } else if (a.small == 3 && aligned && half_supported(a)) {
-    return launch_step_half(a, s, ev0, ev1);
   } else if constexpr (LT != 0) {
     if (a.small == 2 && aligned) TD_STEP_DISPATCH(td_step_kernel_small2, LT, a, TD_LAUNCH2);
     else if (a.small && aligned) TD_STEP_DISPATCH(td_step_kernel_small, LT, a, TD_LAUNCH);

@@ -18,7 +18,7 @@ MT_WORDS = 625
 OPP_WORDS = 626
 HDR_BYTES = 96
 ABI_VERSION = 3  # include/tdstep.h TD_ABI_VERSION
-STEP_KERNELS = {"auto": 0, "large": 1, "small": 2, "small2": 3, "half": 4}  # enum td_step_kernel_kind
+STEP_KERNELS = {"auto": 0, "large": 1, "small": 2, "small2": 3}  # enum td_step_kernel_kind
 
 c_u32p = ctypes.POINTER(ctypes.c_uint32)
 c_i32p = ctypes.POINTER(ctypes.c_int32)

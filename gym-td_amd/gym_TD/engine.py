@@ -123,9 +123,8 @@ class TDEngine(object):
     random_agent: TDGymBasic's random_agent (False: the built-in opponent draws from
           each board's layout stream; with auto-reset the next layout is then drawn
           right after the step that ends the episode, in stream order).
-    step_kernel: 'auto' (td_create's rule by batch size), 'large', 'small', 'small2' or
-          'half' (two boards per wave; TD-def discrete at 10x10) -- td_set_step_kernel; they
-          give the same results.
+    step_kernel: 'auto' (td_create's rule by batch size), 'large', 'small' or 'small2'
+          (td_set_step_kernel; the three give the same results).
     """
 
     def __init__(self, map_size, n_boards, mode="def", multi_action=None, difficulty=1, device=None,
@@ -393,14 +392,14 @@ class TDEngine(object):
                                         _lib.ptr(m, _lib.ctypes.c_uint8) if m is not None else None, self._stream()))
 
     def set_step_kernel(self, kind):
-        """Select the step kernel: 'auto', 'large', 'small', 'small2' or 'half' (td_set_step_kernel)."""
+        """Select the step kernel: 'auto', 'large', 'small' or 'small2' (td_set_step_kernel)."""
         if kind not in _lib.STEP_KERNELS:
             raise ValueError("step kernel must be one of %s" % sorted(_lib.STEP_KERNELS))
         _lib.check(_lib.lib.td_set_step_kernel(self._h, _lib.STEP_KERNELS[kind]))
 
     @property
     def step_kernel(self):
-        """The step kernel td_step launches: 'large', 'small', 'small2' or 'half'."""
+        """The step kernel td_step launches: 'large', 'small' or 'small2'."""
         k = _lib.check(_lib.lib.td_step_kernel(self._h))
         return {v: n for n, v in _lib.STEP_KERNELS.items()}[k]
 

@@ -192,17 +192,14 @@ int td_reset_layouts(td_handle* h, const uint32_t* recs, const int32_t* boards, 
  * per-element one (same bytes, slower). */
 int td_step(td_handle* h, const td_step_io* io, void* stream);
 
-/* Which step kernel td_step launches (they differ in occupancy, load schedule and lanes
- * per board, not in results):
+/* Which step kernel td_step launches (one wave per board in all three; they differ in
+ * occupancy and load schedule, not in results):
  *   TD_KERNEL_LARGE  td_step_kernel        several rounds of waves (7 per SIMD), live slots
  *                                          loaded once the header's counts are in;
  *   TD_KERNEL_SMALL  td_step_kernel_small  one round (8 waves per SIMD), 16 enemy + 16 tower
  *                                          slots prefetched with the header;
  *   TD_KERNEL_SMALL2 td_step_kernel_small2 as SMALL, plus a second wave per board that
  *                                          writes half of the observation;
- *   TD_KERNEL_HALF   td_step_kernel_half   two neighbouring boards per wave, one per 32-lane
- *                                          half; the wave writes both observations as one
- *                                          stretch (TD-def discrete at L = 10 only);
  *   TD_KERNEL_AUTO   td_create's rule: SMALL2 up to half a round of boards, SMALL up to one
  *                    round, SMALL2 again up to 3 rounds at L = 10 and 10 rounds at L = 30
  *                    (single-action boards), else LARGE (L = 10 / 20 / 30; other L only
@@ -212,9 +209,7 @@ int td_step(td_handle* h, const td_step_io* io, void* stream);
  * at an L without one.  td_step_kernel returns the resolved kind, td_step_kernel_name the
  * kernel's name as rocprofv3 shows it ("td_step_kernel_small<10, 0, false>": L, mode,
  * multi-action scan). */
-enum td_step_kernel_kind {
-  TD_KERNEL_AUTO = 0, TD_KERNEL_LARGE = 1, TD_KERNEL_SMALL = 2, TD_KERNEL_SMALL2 = 3, TD_KERNEL_HALF = 4
-};
+enum td_step_kernel_kind { TD_KERNEL_AUTO = 0, TD_KERNEL_LARGE = 1, TD_KERNEL_SMALL = 2, TD_KERNEL_SMALL2 = 3 };
 int td_set_step_kernel(td_handle* h, int kind);
 int td_step_kernel(td_handle* h);
 const char* td_step_kernel_name(td_handle* h);

@@ -70,8 +70,7 @@ _MODE_CASES = [
 
 
 @pytest.mark.parametrize("L,B,mode,multi,difficulty,steps,random_agent,kernel", [
-    c + (k,) for c in _MODE_CASES for k in (("large", "small", "small2") if c[0] in (10, 20, 30) else ("large",)) +
-    (("half",) if c[0] == 10 and c[2] == "def" and not c[3] else ())])
+    c + (k,) for c in _MODE_CASES for k in (("large", "small", "small2") if c[0] in (10, 20, 30) else ("large",))])
 def test_batched_modes_vs_oracle(L, B, mode, multi, difficulty, steps, random_agent, kernel):
     """B boards of one mode in one launch vs B oracle envs: reward bits, done,
     state digest, observation bytes and the info tensors of every board, on every step
@@ -399,22 +398,10 @@ def test_step_kernel_selector():
                             ("small2", "td_step_kernel_small2<")):
                 eng.set_step_kernel(k)
                 assert eng.step_kernel == k and eng.step_kernel_name == "%s%d, 0, false>" % (name, L)
-            if L == 10:
-                eng.set_step_kernel("half")
-                assert eng.step_kernel == "half" and eng.step_kernel_name == "td_step_kernel_half<10, 0, false>"
-            else:
-                with pytest.raises(_lib.TDError, match="half-wave kernel"):
-                    eng.set_step_kernel("half")
             eng.set_step_kernel("auto")
             assert eng.step_kernel == "small2"  # 4 boards: half a round of waves or less
         finally:
             eng.close()
-    eng = TDEngine(10, 4, "atk", False, 1, np_seeds=[1, 2, 3, 4], py_seeds=[1, 2, 3, 4])
-    try:
-        with pytest.raises(_lib.TDError, match="half-wave kernel"):
-            eng.set_step_kernel("half")
-    finally:
-        eng.close()
     eng = TDEngine(12, 4, "2p", True, 1, np_seeds=[1, 2, 3, 4], py_seeds=[1, 2, 3, 4])
     try:
         assert eng.step_kernel == "large" and eng.step_kernel_name == "td_step_kernel<0, 2, true>"
@@ -575,7 +562,7 @@ def test_export_import_roundtrip_random_agent_false():
         b_eng.close()
 
 
-@pytest.mark.parametrize("kernel", ("large", "small", "small2", "half"))
+@pytest.mark.parametrize("kernel", ("large", "small", "small2"))
 def test_paramconfig_reaches_live_engines(kernel):
     """paramConfig (TDParam.py:98-100) in the middle of episodes, twice, on a live engine.
     The reference reads most values live from `config`, but an Enemy / Tower keeps the
@@ -679,8 +666,7 @@ def _obs_checksum(obs):
 
 @pytest.mark.parametrize("B,steps,kernel,refill", [
     (16384, 200, "large", 16), (512, 1500, "small2", 16), (8192, 400, "small", 16), (4096, 300, "large", 16),
-    (16384, 200, "large", 0), (8192, 400, "small", 0), (4096, 300, "small2", 0), (8192, 400, "half", 16),
-    (4096, 300, "half", 0), (513, 1500, "half", 16)])
+    (16384, 200, "large", 0), (8192, 400, "small", 0), (4096, 300, "small2", 0)])
 def test_autoreset_under_load_matches_explicit_reset(B, steps, kernel, refill):
     """The staged-layout rings under load: 16,384 boards with 1-LP bases and a weak
     defence finish ~250 episodes per step; 512 boards step so fast that one draw
@@ -736,7 +722,7 @@ def test_autoreset_under_load_matches_explicit_reset(B, steps, kernel, refill):
         eb.close()
 
 
-@pytest.mark.parametrize("kernel", ("large", "small", "small2", "half"))
+@pytest.mark.parametrize("kernel", ("large", "small", "small2"))
 def test_many_towers_vs_oracle(kernel):
     """Boards with more towers than the step prefetches up front (16): tower distance
     1, rich defender.  Same bit-exact comparison as the batched tests."""

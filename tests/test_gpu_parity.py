@@ -22,16 +22,10 @@ from gym_TD.engine import TDEngine  # noqa: E402
 
 from test_oracle_golden import _info_view  # noqa: E402
 
-# The step kernels (td_set_step_kernel): the large-batch kernel of the metric's 65,536
-# boards, the one-round kernel (one wave per board), the two-wave kernel, and the
-# half-wave kernel (two boards per wave) of the N = 8 share (8,192 boards) and configs[1]
-# (4,096).  Every parity test below runs each of them where the kernel exists.
-KERNELS = ("large", "small", "small2", "half")
-
-
-def kernel_applies(kernel, L, mode="def", multi=False):
-    """The half-wave kernel is built for TD-def discrete boards at 10x10 only."""
-    return kernel != "half" or (L == 10 and mode == "def" and not multi)
+# The three step kernels (td_set_step_kernel): the large-batch kernel of the metric's
+# 65,536 boards, the one-round kernel of the N = 8 share (8,192 boards), the two-wave
+# kernel of configs[1] (4,096 boards).  Every parity test below runs each of them.
+KERNELS = ("large", "small", "small2")
 
 
 @contextlib.contextmanager
@@ -62,8 +56,6 @@ def _make_env(tr):
 def test_device_replays_golden(name, kernel):
     tr = G.load_traj(name)
     L = tr["L"]
-    if not kernel_applies(kernel, L, tr["mode"], tr["multi"]):
-        pytest.skip("no %s kernel for this board" % kernel)
     with reference_settings(tr["overrides"], tr["multi"]):
         env = _make_env(tr)
         try:
@@ -121,9 +113,7 @@ def _oracle_envs(L, seeds, mode="def", multi=False, difficulty=1):
 @pytest.mark.parametrize("L,B,steps", [(10, 95, 260), (20, 32, 160), (30, 16, 120)])
 def test_batched_vs_oracle(L, B, steps, kernel):
     """B boards in one launch vs B oracle envs, random + smart defender actions (an odd
-    batch at 10x10: the half-wave kernel's last wave steps one board)."""
-    if not kernel_applies(kernel, L):
-        pytest.skip("no %s kernel at L = %d" % (kernel, L))
+    batch at 10x10)."""
     seeds = [s for s in range(1000, 1000 + 3 * B) if L > 10 or s not in (1045,)]
     orc, ok = [], []
     for s in seeds:
@@ -227,8 +217,7 @@ def test_autoreset_matches_explicit_reset():
 # least once, on the staged-layout rings the refill kernel fills).
 @pytest.mark.parametrize("L,B,mode,multi,steps,kernel", [
     (10, 4096, "def", False, 1300, "auto"), (10, 8192, "def", False, 1300, "auto"),
-    (10, 8192, "def", False, 1300, "large"), (10, 8192, "def", False, 1300, "half"),
-    (10, 4096, "def", False, 1300, "half"), (10, 16384, "def", False, 1300, "auto"),
+    (10, 8192, "def", False, 1300, "large"), (10, 16384, "def", False, 1300, "auto"),
     (10, 65536, "def", False, 1300, "auto"),
     (20, 16384, "2p", True, 300, "auto"), (30, 16384, "def", False, 300, "auto"),
     (30, 16384, "def", False, 300, "large")])

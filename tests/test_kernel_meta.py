@@ -27,7 +27,7 @@ def meta():
 def test_every_kernel_is_present(meta):
     for k in ("td_step_kernelILi10ELi0ELb0", "td_step_kernel_smallILi10ELi0ELb0", "td_step_kernel_small2ILi10ELi0ELb0",
               "td_step_kernelILi20ELi2ELb1", "td_step_kernel_small2ILi30ELi0ELb0", "td_refill_kernelILi10",
-              "td_reset_kernelILi10", "td_autoreset_kernelILi10", "td_step_kernel_halfILi10ELi0ELb0"):
+              "td_reset_kernelILi10", "td_autoreset_kernelILi10"):
         assert any(k in n for n in meta), k
 
 
@@ -41,10 +41,3 @@ def test_small_kernels_keep_eight_waves_at_10x10(meta):
         if ("td_step_kernel_smallILi10" in n or "td_step_kernel_small2ILi10" in n):
             assert r["sgpr"] <= 80 and r["vgpr"] <= 64, (n, r)
             assert r["lds"] * 32 <= 160 * 1024 * (2 if "small2" in n else 1), (n, r)  # 8 waves per SIMD fit LDS
-
-
-def test_half_kernel_runs_one_round_of_8192_boards(meta):
-    """td_step_kernel_half: 16 waves (32 boards) per CU -- LDS for 16 pairs, <= 128 VGPRs --
-    so the N = 8 share's 8,192 boards are one round on 256 CUs."""
-    (n, r), = [(n, r) for n, r in meta.items() if "td_step_kernel_half" in n]
-    assert r["lds"] * 16 <= 160 * 1024 and r["vgpr"] <= 128 and r["scratch"] == 0, (n, r)
