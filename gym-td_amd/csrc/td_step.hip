@@ -1859,6 +1859,17 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
   STAMP_RT(10);
 }
 
+// (temporary A/B, round 5) issue priority by dispatch order in one-round grids: the waves
+// dispatched first finish first and start the observation store stream early.
+__device__ __forceinline__ void prio_by_order() {
+#if defined(TD_PRIO_GRAD)
+  const unsigned lvl = blockIdx.x * (unsigned)TD_PRIO_GRAD / gridDim.x;  // 0 .. TD_PRIO_GRAD - 1
+  if (lvl == 0) __builtin_amdgcn_s_setprio(3);
+  else if (lvl == 1 && TD_PRIO_GRAD > 2) __builtin_amdgcn_s_setprio(2);
+  else if (lvl == 2 && TD_PRIO_GRAD > 3) __builtin_amdgcn_s_setprio(1);
+#endif
+}
+
 // One workgroup (one wave) per board.  (A persistent variant that prefetched the
 // next board while stepping the current one measured slower: its static board
 // assignment leaves a one-board tail, and the step is bound by HBM writes.)
@@ -1869,6 +1880,7 @@ __device__ __forceinline__ void step_kernel_body(const StepArgs& a) {
   const int i = (int)blockIdx.x;
   if (i >= a.B) return;
   const int b = a.xcd_map ? xcd_board(i, a.B) : i;
+  if constexpr (SMALL) prio_by_order();
   stage_cfg(S, a.cfg);
   const int L = LT ? LT : a.L;
   const Ctx x{S.cfg, L, L * L, (int)(threadIdx.x & 63), a.cfgs, a.epoch};
@@ -1914,6 +1926,7 @@ __global__ __launch_bounds__(128) TD_SMALL2_ATTR void td_step_kernel_small2(Step
   __shared__ StepOut SO;
   if ((int)blockIdx.x >= a.B) return;
   const int b = a.xcd_map ? xcd_board((int)blockIdx.x, a.B) : (int)blockIdx.x;
+  prio_by_order();
   const int lane = (int)threadIdx.x & 63;
   if (threadIdx.x < 64) {
     stage_cfg(S, a.cfg);

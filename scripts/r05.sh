@@ -69,5 +69,16 @@ s5)  # placement of the observation: offsets into one contiguous block, 30x30 / 
   run off30 400 python scripts/probe_offset.py 30 16384 100 || exit 1; grep -h offset $O/off30.log | tr '\n' ' '; echo
   run off10 400 python scripts/probe_offset.py 10 65536 200 || exit 1; grep -h offset $O/off10.log | tr '\n' ' '; echo
   ;;
+s6)  # issue priority by dispatch order in one-round grids (variants p4: 4 levels, p2: first half high)
+  V=$PWD/gym-td_amd/lib/variants
+  for r in 1 2; do for v in prod p4 p2; do for bb in 8192 4096; do
+    lib=$PWD/gym-td_amd/lib/libtdstep.so; [ $v != prod ] && lib=$V/libtdstep_$v.so
+    TDSTEP_LIB=$lib run ${v}_${bb}_$r 200 python bench.py --global-batch $bb --no-cpu-baseline --steps 2000 --timing none || exit 1; line ${v}_${bb}_$r
+  done; done; done
+  for v in p4 p2; do
+    TDSTEP_LIB=$V/libtdstep_$v.so run pytest_$v 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -q -x -k "small and not full_size" --timeout 300 --timeout-method thread -p no:cacheprovider
+    rc=$?; tail -1 $O/pytest_$v.log; [ $rc -le 1 ] || exit $rc
+  done
+  ;;
 *) echo "unknown session $S"; exit 2;;
 esac
