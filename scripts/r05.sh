@@ -80,5 +80,14 @@ s6)  # issue priority by dispatch order in one-round grids (variants p4: 4 level
     rc=$?; tail -1 $O/pytest_$v.log; [ $rc -le 1 ] || exit $rc
   done
   ;;
+s7)  # compact group map (NC > 256): GPU suite, 30x30 / 2p lines, the driver's command
+  gpusuite 900; rc=$?; [ $rc -le 1 ] || exit $rc
+  for r in 1 2; do
+    run l30_$r 300 python bench.py --workload def-large --global-batch 16384 --no-cpu-baseline --steps 200 --timing none || exit 1; line l30_$r
+    run p2_$r 300 python bench.py --workload 2p-middle-multi --no-cpu-baseline --steps 200 --timing none || exit 1; line p2_$r
+  done
+  run l30_large 300 python bench.py --workload def-large --global-batch 16384 --no-cpu-baseline --steps 200 --timing none --step-kernel large || exit 1; line l30_large
+  run bench_driver 300 python bench.py --gpus 1 --steps 20 --warmup 5 || exit 1; line bench_driver
+  ;;
 *) echo "unknown session $S"; exit 2;;
 esac
