@@ -631,8 +631,9 @@ __device__ __forceinline__ double e_def(const Ctx& x, uint32_t inf) {
 }
 
 // Enemies up to which the towers target in parallel (board_step; FEW = false: never --
-// the large kernel, where it measured slower, and the two-wave 20x20 single-action
-// kernel, which has no registers to spare for it).
+// the large kernel, where it measured slower, and the two-wave 20x20 / 30x30 single-action
+// kernels, which have no registers to spare for it: at 30x30 it spilled 12 B per lane
+// once the compact group map let 8 waves per SIMD fit LDS).
 constexpr int kFewEnemies = 16;
 
 template <int NC, bool FEW = true>
@@ -1779,7 +1780,7 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
 
   // ---- TDBoard.step
   // (parallel targeting: +1.1-1.4 % at 8,192 / 4,096 boards, -0.7 % in the large kernel at 65,536, profiles/r03/s29)
-  double reward = board_step<NC, SMALL && !(SPLIT && LT == 20 && MODE == MODE_DEF && !SCAN)>(S, u, x, a, b);
+  double reward = board_step<NC, SMALL && !(SPLIT && (LT == 20 || LT == 30) && MODE == MODE_DEF && !SCAN)>(S, u, x, a, b);
   // The next step's opponent words, loaded since the attacker phase, are consumed here,
   // before this step's state stores: gfx950 counts loads and stores in one vmcnt, so
   // after the stores the wait for these loads became a wait for every store's
