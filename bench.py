@@ -78,13 +78,15 @@ FLAG_BITS = (("enemy_overflow", 1), ("tower_overflow", 2), ("bad_action", 4), ("
 
 KERNEL_SAMPLES_MIN = 8  # sampled launches behind a kernel mean
 # A timed region too short for KERNEL_SAMPLES_MIN samples (the driver's 20 steps) runs without
-# timing events; behind it AFTER_WARM untimed steps bring the GPU back to its steady state
-# after the host-side gap, then a pass of AFTER_STEPS steps is sampled every AFTER_EVERY-th
-# launch.  (A 64-step pass sampled every 8th launch right after the gap measured 213-215 us
-# against 209.9-210.2 us per step in the timed region at 65,536 boards, BENCH_r04 and
-# r05/s1; back-to-back 256-step passes: 203.5 us sampled every 32nd, wall 205.4-205.6 with
-# or without the events, scripts/probe_timing.py in r05/s1.)
-AFTER_WARM, AFTER_STEPS, AFTER_EVERY = 16, 256, 32
+# timing events; the kernel is sampled in a pass of PRE_STEPS steps right before it (behind
+# the burn-in, before the warm-up steps), every PRE_EVERY-th launch.  Passes sampled after
+# the timed region, behind a host-side gap, ran slower than the steps timed before them
+# (65,536 boards: 64 steps sampled every 8th 213-215 us against 209.9-210.2 us per timed
+# step, BENCH_r04 and r05/s1; 256 steps every 32nd behind 16 warm steps 209.6 vs 208.0,
+# r05/s7), while back-to-back 256-step passes measured 203.5 us sampled every 32nd at a
+# wall time of 205.4-205.6 us per step with or without the events (scripts/probe_timing.py,
+# r05/s1).
+PRE_STEPS, PRE_EVERY = 256, 32
 
 
 def event_every(steps, override=None):
@@ -99,14 +101,14 @@ def event_every(steps, override=None):
 def timing_plan(steps, every):
     """Where the step-kernel durations are sampled: ("timed", n, every) -- every
     ``every``-th launch of the timed region, n launches -- when the timed region holds at
-    least KERNEL_SAMPLES_MIN of them; else ("after", AFTER_STEPS, AFTER_EVERY): the timed
-    region runs without timing events, and behind it AFTER_WARM untimed steps and then a
-    pass of AFTER_STEPS steps sampled every AFTER_EVERY-th launch.  A 20-step line (the
-    driver's) thus averages 8 launches of a steady-state pass."""
+    least KERNEL_SAMPLES_MIN of them; else ("pre", PRE_STEPS, PRE_EVERY): the timed region
+    runs without timing events, and a pass of PRE_STEPS steps right before it (behind the
+    burn-in, before the warm-up) is sampled every PRE_EVERY-th launch.  A 20-step line (the
+    driver's) thus averages 8 launches of the steady state it is timed in."""
     n = (steps + every - 1) // every
     if n >= KERNEL_SAMPLES_MIN:
         return "timed", n, every
-    return "after", AFTER_STEPS, AFTER_EVERY
+    return "pre", PRE_STEPS, PRE_EVERY
 
 
 def kernel_vs_step(avg_kernel_us, step_us):
@@ -433,8 +435,8 @@ def main():
     pool = draw(N_ACTION_BUFS) if multi else None
     period = P.hyper_parameters.max_episode_steps
     gidx = np.arange(B) + rank * B
-    for k in range(args.burnin + W):
-        if args.stagger and k < args.burnin and k < period and k > 0:
+    for k in range(args.burnin):
+        if args.stagger and k < period and k > 0:
             m = (gidx % period) == k
             if m.any():
                 eng.reset(m)  # a failing draw leaves the board in its first episode (the reference raises)
@@ -449,11 +451,8 @@ def main():
     plan, n_plan, every = timing_plan(K, every) if args.timing == "dispatch" else ("timed", 0, every)
     sampled = set(range(0, K, every)) if args.timing == "marker" else set()
     ev = {k: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for k in sampled}
-    eng.episode_stats(clear=True)  # the device accumulates finished episodes of the timed steps
     if args.refill_interval is not None:
         eng.set_refill_interval(args.refill_interval)
-    if plan == "timed" and args.timing == "dispatch":
-        eng.kernel_timing(n_plan, every)  # timestamped by their own dispatch
 
     def run_steps(n, first):
         for k in range(n):
@@ -463,6 +462,23 @@ def main():
             eng.step(def_act=d, atk_act=a)
             if first + k in sampled:
                 ev[first + k][1].record(stream)
+
+    sample_wall, n_sample_steps, kern_pre = None, K, None
+    if plan == "pre":
+        # a timed region too short to sample: the kernel durations come from a steady-state
+        # pass right before it; the timed steps run without timing events
+        eng.kernel_timing((n_plan + every - 1) // every, every)
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        run_steps(n_plan, 0)
+        torch.cuda.synchronize(dev)
+        sample_wall, n_sample_steps = time.perf_counter() - t1, n_plan
+        kern_pre = (eng.kernel_times().astype(np.float64) / 1e3).tolist()
+        eng.kernel_timing(0)
+    run_steps(W, 0)  # warm-up
+    eng.episode_stats(clear=True)  # the device accumulates finished episodes of the timed steps
+    if plan == "timed" and args.timing == "dispatch":
+        eng.kernel_timing(n_plan, every)  # timestamped by their own dispatch
 
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -480,19 +496,11 @@ def main():
     flags = eng.flags()
     ep_stats = eng.episode_stats(clear=True)
     ep_recs = eng.episode_records()
-    sample_wall = elapsed  # wall time of the steps the kernel samples come from
-    n_sample_steps = K
-    if plan == "after":
-        # short timed region: it ran without timing events; the kernel mean comes from a
-        # steady-state pass of the same kernel behind it (AFTER_WARM untimed steps first)
-        run_steps(AFTER_WARM, K)
-        eng.kernel_timing((n_plan + every - 1) // every, every)
-        torch.cuda.synchronize(dev)
-        t1 = time.perf_counter()
-        run_steps(n_plan, K + AFTER_WARM)
-        torch.cuda.synchronize(dev)
-        sample_wall, n_sample_steps = time.perf_counter() - t1, n_plan
-    if args.timing == "dispatch":
+    if sample_wall is None:
+        sample_wall = elapsed  # wall time of the steps the kernel samples come from
+    if kern_pre is not None:
+        kern_ms = kern_pre
+    elif args.timing == "dispatch":
         kern_ms = (eng.kernel_times().astype(np.float64) / 1e3).tolist()
         eng.kernel_timing(0)
     elif args.timing == "marker":
@@ -536,9 +544,8 @@ def main():
                          "kernel_timing": {"dispatch": "dispatch-packet timestamps of every %dth launch (td_kernel_timing) "
                                                        "%s, %.2f us wall per step there" % (
                                                            every, "of the timed region" if plan == "timed" else
-                                                           "of an untimed %d-step pass behind the timed region and %d warm "
-                                                           "steps (the timed steps ran without timing events)" % (
-                                                               n_plan, AFTER_WARM),
+                                                           "of an untimed %d-step pass right before the warm-up and the timed "
+                                                           "region (the timed steps ran without timing events)" % n_plan,
                                                            sample_step_s * 1e6),
                                            "marker": "torch event pairs around every %dth launch" % every,
                                            "none": "not timed"}[args.timing],

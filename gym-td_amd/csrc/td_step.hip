@@ -52,7 +52,10 @@ namespace td {
 // The multi-action scan borrows the area for 2 NC bytes of flags and real actions.
 template <int NC>
 struct GrpMap {
-  static constexpr bool compact = NC > 256;
+#ifndef TD_GRP_COMPACT_MIN  // (temporary A/B, round 5)
+#define TD_GRP_COMPACT_MIN 256
+#endif
+  static constexpr bool compact = NC > TD_GRP_COMPACT_MIN;
   static constexpr int need = compact ? (2 * NC > NC + 4 * ECAP ? 2 * NC : NC + 4 * ECAP) : 4 * NC;
   static constexpr int bytes = (need + 15) & ~15;
 };

@@ -89,5 +89,22 @@ s7)  # compact group map (NC > 256): GPU suite, 30x30 / 2p lines, the driver's c
   run l30_large 300 python bench.py --workload def-large --global-batch 16384 --no-cpu-baseline --steps 200 --timing none --step-kernel large || exit 1; line l30_large
   run bench_driver 300 python bench.py --gpus 1 --steps 20 --warmup 5 || exit 1; line bench_driver
   ;;
+s8)  # compact group map vs none at 30x30 (same box), 2p; the driver's command with the pre-pass kernel timing
+  V=$PWD/gym-td_amd/lib/variants
+  for r in 1 2 3; do for v in prod nocompact; do
+    lib=$PWD/gym-td_amd/lib/libtdstep.so; [ $v != prod ] && lib=$V/libtdstep_$v.so
+    TDSTEP_LIB=$lib run l30_${v}_$r 300 python bench.py --workload def-large --global-batch 16384 --no-cpu-baseline --steps 200 --timing none || exit 1; line l30_${v}_$r
+  done; done
+  for v in prod nocompact; do
+    lib=$PWD/gym-td_amd/lib/libtdstep.so; [ $v != prod ] && lib=$V/libtdstep_$v.so
+    TDSTEP_LIB=$lib run p2_${v} 300 python bench.py --workload 2p-middle-multi --no-cpu-baseline --steps 200 --timing none || exit 1; line p2_${v}
+  done
+  for r in 1 2; do
+    run bench_driver_$r 300 python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline || exit 1; line bench_driver_$r
+    grep -o '"frac_withheld[^}]*' $O/bench_driver_$r.log || true
+  done
+  run pytest_30 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_deep.py tests/test_gpu_envs.py -m gpu -q -x -k "30 or 20" --timeout 300 --timeout-method thread -p no:cacheprovider
+  rc=$?; tail -1 $O/pytest_30.log; [ $rc -le 1 ] || exit $rc
+  ;;
 *) echo "unknown session $S"; exit 2;;
 esac

@@ -88,14 +88,14 @@ def test_gpus_n_starts_n_ranks(monkeypatch):
 
 
 def test_short_runs_sample_enough_launches():
-    # the driver's 20-step line: no events in the timed region; 16 warm steps, then a
-    # 256-step pass sampled every 32nd launch (8 samples) behind it
-    assert bench.timing_plan(20, 8) == ("after", 256, 32)
-    assert bench.timing_plan(32, 8) == ("after", 256, 32)
+    # the driver's 20-step line: no events in the timed region; a 256-step pass right before
+    # it (behind the burn-in) sampled every 32nd launch (8 samples)
+    assert bench.timing_plan(20, 8) == ("pre", 256, 32)
+    assert bench.timing_plan(32, 8) == ("pre", 256, 32)
     assert bench.timing_plan(64, 8) == ("timed", 8, 8)
     assert bench.timing_plan(2000, 8) == ("timed", 250, 8)
-    assert bench.timing_plan(5, 1) == ("after", 256, 32)
-    assert bench.AFTER_STEPS // bench.AFTER_EVERY >= bench.KERNEL_SAMPLES_MIN
+    assert bench.timing_plan(5, 1) == ("pre", 256, 32)
+    assert bench.PRE_STEPS // bench.PRE_EVERY >= bench.KERNEL_SAMPLES_MIN
 
 
 def test_kernel_longer_than_the_step_withholds_the_fraction():
