@@ -44,27 +44,11 @@ namespace td {
 // ---------------------------------------------------------------------------
 // per-board LDS image
 // ---------------------------------------------------------------------------
-// The enemy group map: the head enemy index of each (type, cell) group, 0xFF none.
-// Small boards (NC <= 256) keep a byte per (type, cell): grp[type * NC + cell].  Larger
-// ones a byte per cell -- the first enemy on it (any type), 0xFF none -- and, indexed by
-// that enemy, four bytes of heads by type: grp[cell] -> c, grp[NC + 4 c + type] (NC + 512
-// bytes instead of 4 NC: at 30x30 the board image bounds residency, 14 -> 16 boards per CU).
-// The multi-action scan borrows the area for 2 NC bytes of flags and real actions.
-template <int NC>
-struct GrpMap {
-#ifndef TD_GRP_COMPACT_MIN  // (temporary A/B, round 5)
-#define TD_GRP_COMPACT_MIN 256
-#endif
-  static constexpr bool compact = NC > TD_GRP_COMPACT_MIN;
-  static constexpr int need = compact ? (2 * NC > NC + 4 * ECAP ? 2 * NC : NC + 4 * ECAP) : 4 * NC;
-  static constexpr int bytes = (need + 15) & ~15;
-};
-
 template <int NC>
 struct alignas(16) Smem {
   static_assert(NC % 4 == 0, "cell and tower maps are moved in 16-B / 4-B units");
   uint32_t cell[NC];      // cell words (td_layout.h), + the tower on the cell in bits 10-13 (tw_nib)
-  uint8_t grp[GrpMap<NC>::bytes];  // enemy group map (GrpMap); the multi-action scan's flags
+  uint8_t grp[4][NC];     // enemy group (head enemy index) per (type, cell), 0xFF none
   union {
     struct {              // load .. march: the enemy list (written back right after the march)
       double eLP[ECAP];
@@ -456,14 +440,13 @@ __device__ __forceinline__ int defender_op(Smem<NC>& S, U& u, const Ctx& x, int 
 // (In the two-wave kernel the second wave folds the flags while the first loads the
 // board, and writes the real actions out after the step's actions: scan_fold /
 // scan_write_real below, handed over at barriers.)
-// The flags folded into grp[0, NC) (grp[NC, 2 NC) cleared); true when a flag is not 0 / 1 / 2.
+// The flags folded into grp[0] (grp[1] cleared); true when a flag is not 0 / 1 / 2.
 template <int NC>
 __device__ __forceinline__ bool scan_fold(Smem<NC>& S, int lane, int ncr, const int64_t* A) {
-  static_assert(GrpMap<NC>::bytes >= 2 * NC, "flags and real actions in the group map");
   const int n = 6 * ncr;
-  uint8_t* flag = &S.grp[0];
+  uint8_t* flag = &S.grp[0][0];
   uint32_t* fw = reinterpret_cast<uint32_t*>(flag);
-  for (int i = lane; i < (2 * NC) / 4; i += 64) fw[i] = 0u;  // flags and real actions
+  for (int i = lane; i < (2 * NC) / 4; i += 64) fw[i] = 0u;  // grp[0] and grp[1]
   wsync();
   bool bad = false;
   if ((ncr & 1) == 0 && (reinterpret_cast<uintptr_t>(A) & 15u) == 0) {  // 16-B units of two cells of one plane
@@ -507,7 +490,7 @@ __device__ __forceinline__ bool scan_fold(Smem<NC>& S, int lane, int ncr, const 
 template <int NC>
 __device__ __forceinline__ void scan_write_real(const Smem<NC>& S, int lane, int ncr, int64_t* R) {
   const int n = 6 * ncr;
-  const uint8_t* real = &S.grp[NC];
+  const uint8_t* real = &S.grp[1][0];
   if ((ncr & 1) == 0 && (reinterpret_cast<uintptr_t>(R) & 15u) == 0) {
     typedef long long i64x2 __attribute__((ext_vector_type(2)));
     i64x2* R2 = reinterpret_cast<i64x2*>(R);
@@ -533,8 +516,8 @@ __device__ __forceinline__ void defender_scan(Smem<NC>& S, U& u, const Ctx& x, c
                                               bool bad = false) {
   const TdDevCfg& C = x.C;
   const int ncr = x.NCr;
-  uint8_t* flag = &S.grp[0];
-  uint8_t* real = &S.grp[NC];
+  uint8_t* flag = &S.grp[0][0];
+  uint8_t* real = &S.grp[1][0];
   if constexpr (FOLD) bad = scan_fold(S, x.lane, ncr, A);
   if (bad) u.flags |= FLAG_BAD_ACTION;
   for (int base = 0; base < ncr && active; base += 64) {
@@ -634,9 +617,8 @@ __device__ __forceinline__ double e_def(const Ctx& x, uint32_t inf) {
 }
 
 // Enemies up to which the towers target in parallel (board_step; FEW = false: never --
-// the large kernel, where it measured slower, and the two-wave 20x20 / 30x30 single-action
-// kernels, which have no registers to spare for it: at 30x30 it spilled 12 B per lane
-// once the compact group map let 8 waves per SIMD fit LDS).
+// the large kernel, where it measured slower, and the two-wave 20x20 single-action
+// kernel, which has no registers to spare for it).
 constexpr int kFewEnemies = 16;
 
 template <int NC, bool FEW = true>
@@ -881,10 +863,9 @@ __device__ __forceinline__ void enemy_stats(Smem<NC>& S, const U& u, const Ctx& 
   const TdDevCfg& C = x.C;
   const int n = u.n;
   if (n == 0) return;  // write_obs emits zero planes without reading grp
-  using GM = GrpMap<NC>;
-  static_assert(GM::bytes % 16 == 0 && offsetof(Smem<NC>, grp) % 16 == 0, "grp cleared in 16-B units");
-  for (int i = x.lane; i < GM::bytes / 16; i += 64)
-    reinterpret_cast<uint4*>(&S.grp[0])[i] = uint4{0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+  static_assert((4 * NC) % 16 == 0 && offsetof(Smem<NC>, grp) % 16 == 0, "grp cleared in 16-B units");
+  for (int i = x.lane; i < 4 * NC / 16; i += 64)
+    reinterpret_cast<uint4*>(&S.grp[0][0])[i] = uint4{0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
   uint32_t key[2];
   float r[2] = {0.0f, 0.0f};
   bool val[2];
@@ -903,15 +884,12 @@ __device__ __forceinline__ void enemy_stats(Smem<NC>& S, const U& u, const Ctx& 
   float mn[2] = {1.0f, 1.0f}, mx[2] = {0.0f, 0.0f}, sm[2] = {0.0f, 0.0f};
   int cnt[2] = {0, 0};
   bool head[2] = {val[0], val[1]};
-  bool chead[2] = {val[0], val[1]};  // compact map: the first enemy on its cell (any type)
   for (int j = 0; j < n; ++j) {  // enemy j's group key and ratio from the lane that holds it
     const uint32_t kj = j < 64 ? rdl(key[0], j) : rdl(key[1], j - 64);
     const float rj = j < 64 ? rdl(r[0], j) : rdl(r[1], j - 64);
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       int i = x.lane + 64 * s;
-      if constexpr (GM::compact)
-        if (val[s] && j < i && ((kj ^ key[s]) & 0xfffu) == 0u) chead[s] = false;
       if (val[s] && kj == key[s]) {
         if (j < i) head[s] = false;
         else {
@@ -924,12 +902,6 @@ __device__ __forceinline__ void enemy_stats(Smem<NC>& S, const U& u, const Ctx& 
     }
   }
   const float mcl = (float)C.max_cluster_length;
-  if constexpr (GM::compact) {
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-      if (chead[s]) S.grp[key[s] & 0xfffu] = (uint8_t)(x.lane + 64 * s);
-    wsync();
-  }
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
     int i = x.lane + 64 * s;
@@ -938,22 +910,10 @@ __device__ __forceinline__ void enemy_stats(Smem<NC>& S, const U& u, const Ctx& 
       S.gst[i][1] = mx[s];
       S.gst[i][2] = __fdiv_rn(sm[s], (float)cnt[s]);
       S.gst[i][3] = __fdiv_rn((float)cnt[s], mcl);
-      if constexpr (GM::compact) S.grp[NC + 4 * (int)S.grp[key[s] & 0xfffu] + (int)(key[s] >> 12)] = (uint8_t)i;
-      else S.grp[(key[s] >> 12) * NC + (key[s] & 0xfffu)] = (uint8_t)i;
+      S.grp[key[s] >> 12][key[s] & 0xfffu] = (uint8_t)i;
     }
   }
   wsync();
-}
-
-// The head enemy of the (type t, cell) group, 0xFF none (GrpMap).
-template <int NC>
-__device__ __forceinline__ uint32_t grp_head(const Smem<NC>& S, int t, int cell) {
-  if constexpr (GrpMap<NC>::compact) {
-    const uint32_t c = S.grp[cell];
-    return c == 0xFFu ? 0xFFu : S.grp[NC + 4 * (int)(c & 0x7fu) + t];
-  } else {
-    return S.grp[t * NC + cell];
-  }
 }
 
 // Channel 9 by distance (per episode): s[9] = map[4] / (max(map[4]) + 1), an
@@ -1008,8 +968,8 @@ __device__ __forceinline__ float obs_value(const Smem<NC>& S, int ch, int cell, 
     case OK_ENEMY: {
       if (!any_enemy) return 0.0f;
       const int e = ch - 25;
-      const uint32_t g = grp_head(S, e & 3, cell);
-      return g == 0xFFu ? 0.0f : S.gst[g & 0x7fu][e >> 2];
+      const uint32_t g = S.grp[e & 3][cell];
+      return g == 0xFFu ? 0.0f : S.gst[g][e >> 2];
     }
     default: return S.chv[ch];
   }
@@ -1066,8 +1026,8 @@ __device__ __forceinline__ void write_obs(const Smem<NC>& S, const Ctx& x, float
         v = f32x4{S.d9[w.x >> 24], S.d9[w.y >> 24], S.d9[w.z >> 24], S.d9[w.w >> 24]};
       } else if (any_enemy) {  // wave-uniform
         const int e = ch - 25, st = e >> 2, t = e & 3;
-        const uint32_t g0 = grp_head(S, t, 4 * q), g1 = grp_head(S, t, 4 * q + 1);
-        const uint32_t g2 = grp_head(S, t, 4 * q + 2), g3 = grp_head(S, t, 4 * q + 3);
+        const uint32_t g4 = *reinterpret_cast<const uint32_t*>(&S.grp[t][4 * q]);
+        const uint32_t g0 = g4 & 0xffu, g1 = (g4 >> 8) & 0xffu, g2 = (g4 >> 16) & 0xffu, g3 = g4 >> 24;
         // branch-free: read a clamped slot, keep it only where the cell has a group
         const float f0 = S.gst[g0 & (ECAP - 1)][st], f1 = S.gst[g1 & (ECAP - 1)][st];
         const float f2 = S.gst[g2 & (ECAP - 1)][st], f3 = S.gst[g3 & (ECAP - 1)][st];
@@ -1149,7 +1109,7 @@ __device__ __forceinline__ void write_obs_lines(const Smem<NC>& S, int lane, flo
   constexpr uint32_t OOB = 0x80000000u;  // beyond the buffer's num_records: store dropped
   const char* const sb = reinterpret_cast<const char*>(&S);
   const int o_cell = (int)(reinterpret_cast<const char*>(S.cell) - sb);  // packed cell words (pack_obs_cells)
-  const int o_grp = (int)(reinterpret_cast<const char*>(&S.grp[0]) - sb);
+  const int o_grp = (int)(reinterpret_cast<const char*>(&S.grp[0][0]) - sb);
   const int o_chv = (int)(reinterpret_cast<const char*>(S.chv) - sb);
   const int o_d9 = (int)(reinterpret_cast<const char*>(S.d9) - sb);
   const int o_gst = (int)(reinterpret_cast<const char*>(&S.gst[0][0]) - sb);
@@ -1180,8 +1140,7 @@ __device__ __forceinline__ void write_obs_lines(const Smem<NC>& S, int lane, flo
           // enemy plane: the cell quad's group bytes; else the channel's broadcast value
           // (bit select: a ternary here compiled to a divergent branch)
           const int e = ch - 25;
-          const int wa = o_grp + (GrpMap<NC>::compact ? 0 : (e & 3) * NC) + 4 * q, wb = o_chv + 4 * ch;
-          const int m = -(int)((unsigned)e < 16u);
+          const int wa = o_grp + (e & 3) * NC + 4 * q, wb = o_chv + 4 * ch, m = -(int)((unsigned)e < 16u);
           const int wo = wb ^ ((wa ^ wb) & m);
           W[j] = *reinterpret_cast<const uint32_t*>(sb + wo);
         } else {
@@ -1224,9 +1183,7 @@ __device__ __forceinline__ void write_obs_lines(const Smem<NC>& S, int lane, flo
         } else if (isen && any_enemy) {  // enemy stats by the cell's group head
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
-            uint32_t g = (W[j] >> (8 * c)) & 0xffu;
-            if constexpr (GrpMap<NC>::compact)  // the cell's first enemy -> the head of type e & 3
-              g = g == 0xffu ? g : (uint32_t)*reinterpret_cast<const uint8_t*>(sb + o_grp + NC + 4 * (int)(g & 0x7fu) + (e & 3));
+            const uint32_t g = (W[j] >> (8 * c)) & 0xffu;
             const float f = *reinterpret_cast<const float*>(sb + o_gst + 16 * (int)(g & 0x7fu) + 4 * ((e >> 2) & 3));
             v[c] = g != 0xffu ? f : 0.0f;
           }
@@ -1507,9 +1464,9 @@ __device__ __forceinline__ void opponent_tower_lv0(Smem<NC>& S, U& u, const Ctx&
 template <int NC, class Rng>
 __device__ __forceinline__ void build_near_road(Smem<NC>& S, U& u, const Ctx& x, Rng& R, int t, bool draw_type) {
   // road cells in row-major order, then random.shuffle (Fisher-Yates on randbelow)
-  // The list is kept in the group map as u16 cell indices (at most NC of them).
-  static_assert(GrpMap<NC>::bytes >= 2 * NC, "road cells in the group map");
-  uint16_t* cells = reinterpret_cast<uint16_t*>(&S.grp[0]);
+  // The list lives in the sort-key scratch as cell indices (<= L*L <= 4096 > 4*ECAP,
+  // so it is kept in the group map instead: grp has 4*NC bytes -> store u16 cells).
+  uint16_t* cells = reinterpret_cast<uint16_t*>(&S.grp[0][0]);
   int nroad = 0;
   for (int base = 0; base < x.NCr; base += 64) {
     int c = base + x.lane;
@@ -1783,7 +1740,7 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
 
   // ---- TDBoard.step
   // (parallel targeting: +1.1-1.4 % at 8,192 / 4,096 boards, -0.7 % in the large kernel at 65,536, profiles/r03/s29)
-  double reward = board_step<NC, SMALL && !(SPLIT && (LT == 20 || LT == 30) && MODE == MODE_DEF && !SCAN)>(S, u, x, a, b);
+  double reward = board_step<NC, SMALL && !(SPLIT && LT == 20 && MODE == MODE_DEF && !SCAN)>(S, u, x, a, b);
   // The next step's opponent words, loaded since the attacker phase, are consumed here,
   // before this step's state stores: gfx950 counts loads and stores in one vmcnt, so
   // after the stores the wait for these loads became a wait for every store's
@@ -1935,11 +1892,9 @@ __global__ __launch_bounds__(64) void td_step_kernel(StepArgs a) {
 // 65,536 boards the same build is 7 % slower (SGPR spill code), hence two kernels.
 // The two-wave 20x20 kernels of the multi-action scan and of TD-atk do not fit 64 VGPRs:
 // at 8 waves per SIMD they spilled (112-116 / 8 B of scratch per lane; the scan still
-// spilled at 6), so 5 / 6; the 30x30 scan (~180 VGPRs) runs 2.
+// spilled at 6), so 5 / 6.
 template <int LT, int MODE, bool SCAN>
-constexpr int small2_cap() {
-  return LT == 20 && SCAN ? 5 : LT == 30 && SCAN ? 2 : LT == 20 && MODE == MODE_ATK ? 6 : 8;
-}
+constexpr int small2_cap() { return LT == 20 && SCAN ? 5 : LT == 20 && MODE == MODE_ATK ? 6 : 8; }
 #define TD_SMALL_ATTR __attribute__((amdgpu_waves_per_eu(8, 8)))
 #define TD_SMALL2_ATTR __attribute__((amdgpu_waves_per_eu(small2_cap<LT, MODE, SCAN>(), small2_cap<LT, MODE, SCAN>())))
 template <int LT, int MODE, bool SCAN>
