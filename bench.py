@@ -381,6 +381,9 @@ def main():
                     help="diagnostic: force a step kernel (td_set_step_kernel); default td_create's rule")
     ap.add_argument("--event-every", type=int, default=None,
                     help="timed launches per sampled kernel duration (default 8; every launch perturbs the step)")
+    ap.add_argument("--kernel-sampling", default="pre", choices=("pre", "post"),
+                    help="a timed region too short to sample (< 64 steps): the sampled pass runs right before "
+                         "the warm-up ('pre') or behind the timed region after 16 warm steps ('post')")
     ap.add_argument("--refill-interval", type=int, default=None,
                     help="diagnostic: steps between layout-refill launches in the timed region (0 = none)")
     args = ap.parse_args()
@@ -463,6 +466,8 @@ def main():
             if first + k in sampled:
                 ev[first + k][1].record(stream)
 
+    if plan == "pre" and args.kernel_sampling == "post":
+        plan = "post"
     sample_wall, n_sample_steps, kern_pre = None, K, None
     if plan == "pre":
         # a timed region too short to sample: the kernel durations come from a steady-state
@@ -496,6 +501,14 @@ def main():
     flags = eng.flags()
     ep_stats = eng.episode_stats(clear=True)
     ep_recs = eng.episode_records()
+    if plan == "post":
+        run_steps(16, K)
+        eng.kernel_timing((n_plan + every - 1) // every, every)
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        run_steps(n_plan, K + 16)
+        torch.cuda.synchronize(dev)
+        sample_wall, n_sample_steps = time.perf_counter() - t1, n_plan
     if sample_wall is None:
         sample_wall = elapsed  # wall time of the steps the kernel samples come from
     if kern_pre is not None:
@@ -544,8 +557,10 @@ def main():
                          "kernel_timing": {"dispatch": "dispatch-packet timestamps of every %dth launch (td_kernel_timing) "
                                                        "%s, %.2f us wall per step there" % (
                                                            every, "of the timed region" if plan == "timed" else
-                                                           "of an untimed %d-step pass right before the warm-up and the timed "
-                                                           "region (the timed steps ran without timing events)" % n_plan,
+                                                           "of an untimed %d-step pass %s (the timed steps ran without "
+                                                           "timing events)" % (n_plan, "right before the warm-up and the "
+                                                                               "timed region" if plan == "pre" else
+                                                                               "behind the timed region"),
                                                            sample_step_s * 1e6),
                                            "marker": "torch event pairs around every %dth launch" % every,
                                            "none": "not timed"}[args.timing],

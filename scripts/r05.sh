@@ -106,5 +106,14 @@ s8)  # compact group map vs none at 30x30 (same box), 2p; the driver's command w
   run pytest_30 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_deep.py tests/test_gpu_envs.py -m gpu -q -x -k "30 or 20" --timeout 300 --timeout-method thread -p no:cacheprovider
   rc=$?; tail -1 $O/pytest_30.log; [ $rc -le 1 ] || exit $rc
   ;;
+s9)  # the driver's command: where the kernel is sampled (pre / post pass), and the timed region alone
+  for r in 1 2; do
+    for m in pre post; do
+      run drv_${m}_$r 300 python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --kernel-sampling $m || exit 1; line drv_${m}_$r
+    done
+    run drv_none_$r 300 python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --timing none || exit 1; line drv_none_$r
+    run drv_256_$r 300 python bench.py --gpus 1 --steps 256 --warmup 5 --no-cpu-baseline --event-every 32 || exit 1; line drv_256_$r
+  done
+  ;;
 *) echo "unknown session $S"; exit 2;;
 esac
