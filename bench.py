@@ -31,9 +31,10 @@ MAX and the episode-stat gather after the timed region (RCCL on GPUs).
 
 One JSON line on rank 0: metric/value/unit (the metric string, ``global_batch``,
 ``boards_per_gpu`` and ``scaling`` follow what actually ran), ``roofline`` for
-the step kernel (its average duration from HIP timing events bound to every timed
-launch's own dispatch on the launch stream -- the timestamps rocprofv3's kernel
-trace reports -- and the algorithmic bytes per launch;
+the step kernel (its average duration from HIP timing events bound to the own
+dispatch of every k-th launch of the timed region on the launch stream -- the
+timestamps rocprofv3's kernel trace reports; k from the warm-up's step time,
+``event_every`` -- and the algorithmic bytes per launch;
 ``traffic`` is the PMC-measured HBM bytes per launch of the same kernel build at
 the same boards per GPU, with its source, or null) and ``cpu_baseline`` (the C
 restatement oracle/td_cpu.c on this host's cores, rank 0, N=1;
@@ -41,6 +42,7 @@ restatement oracle/td_cpu.c on this host's cores, rank 0, N=1;
 """
 import argparse
 import json
+import math
 import multiprocessing as mp
 import os
 import sys
@@ -71,49 +73,40 @@ DATA = {("def", False): "synthetic: uniform random defender actions, built-in lv
         ("2p", True): "synthetic: defender flags uniform in {0,1,2} (6,L,L), attacker clusters uniform in {0..4} (3,8), "
                       "seeded boards"}
 N_ACTION_BUFS = 8  # distinct pre-drawn action batches cycled through the timed steps (multi-action shapes)
-EVENT_EVERY = 8  # timed steps per sampled kernel duration (an event pair per launch costs ~10 % of the step rate at 8,192 boards)
+EVENT_EVERY = 8  # timed steps per sampled kernel duration when the warm-up gives no step time (--warmup 0)
 
 FLAG_BITS = (("enemy_overflow", 1), ("tower_overflow", 2), ("bad_action", 4), ("no_layout", 8), ("bad_move", 16))
 
+# The step kernel is sampled inside the timed region itself, on every k-th launch.  A
+# launch bound to a timing-event pair (td_kernel_timing) delays the next dispatch by about
+# EVENT_COST_US (~3 us at 65,536 and at 8,192 boards with events on every launch,
+# scripts/probe_timing.py in r05/s1; 4,096 boards with every 2nd: +1 us per step, r05/s10),
+# so k is chosen from the warm-up's wall time per step to keep that cost below
+# EVENT_PERTURB of the step, and at most half the timed steps apart (two samples at least).
+# Passes sampled outside the timed region measured another window of the rollout: 20-step
+# windows of the same run differ by up to 10 % (65,536 boards: 208.5 us per step after
+# 1,200 burn-in steps, 228.0 after 1,456, 231.9 after 1,520, r05/s10).
+EVENT_COST_US = 3.0
+EVENT_PERTURB = 0.01
 
-KERNEL_SAMPLES_MIN = 8  # sampled launches behind a kernel mean
-# A timed region too short for KERNEL_SAMPLES_MIN samples (the driver's 20 steps) runs without
-# timing events; the kernel is sampled in a pass of PRE_STEPS steps right before it (behind
-# the burn-in, before the warm-up steps), every PRE_EVERY-th launch.  Passes sampled after
-# the timed region, behind a host-side gap, ran slower than the steps timed before them
-# (65,536 boards: 64 steps sampled every 8th 213-215 us against 209.9-210.2 us per timed
-# step, BENCH_r04 and r05/s1; 256 steps every 32nd behind 16 warm steps 209.6 vs 208.0,
-# r05/s7), while back-to-back 256-step passes measured 203.5 us sampled every 32nd at a
-# wall time of 205.4-205.6 us per step with or without the events (scripts/probe_timing.py,
-# r05/s1).
-PRE_STEPS, PRE_EVERY = 256, 32
 
-
-def event_every(steps, override=None):
-    """Timed launches per sampled kernel duration: every 8th.  Sampling every launch
-    perturbs what it measures: 42.5 vs 37.6 us per step at 8,192 boards, 219.8 vs 214.4 us
-    at 65,536 (profiles/r03/s6, --timing none beside it)."""
+def event_every(steps, warm_step_us=None, override=None):
+    """Timed launches per sampled kernel duration: the smallest k with EVENT_COST_US / k
+    below EVENT_PERTURB of the warm-up's step time, at least 2, at most ceil(steps / 2).
+    The driver's 20 steps at 65,536 boards (~210 us): every 2nd launch, 10 samples
+    (kernel 205.7-207.4 us in steps of 209.0-209.9, against 209.8-210.4 without events,
+    r05/s10).  Without a warm-up step time: every EVENT_EVERY-th."""
     if override:
         return max(1, int(override))
-    return EVENT_EVERY
-
-
-def timing_plan(steps, every):
-    """Where the step-kernel durations are sampled: ("timed", n, every) -- every
-    ``every``-th launch of the timed region, n launches -- when the timed region holds at
-    least KERNEL_SAMPLES_MIN of them; else ("pre", PRE_STEPS, PRE_EVERY): the timed region
-    runs without timing events, and a pass of PRE_STEPS steps right before it (behind the
-    burn-in, before the warm-up) is sampled every PRE_EVERY-th launch.  A 20-step line (the
-    driver's) thus averages 8 launches of the steady state it is timed in."""
-    n = (steps + every - 1) // every
-    if n >= KERNEL_SAMPLES_MIN:
-        return "timed", n, every
-    return "pre", PRE_STEPS, PRE_EVERY
+    if not (warm_step_us and warm_step_us > 0):
+        return EVENT_EVERY
+    k = math.ceil(EVENT_COST_US / (EVENT_PERTURB * warm_step_us))
+    return int(max(2, min(k, (steps + 1) // 2)))
 
 
 def kernel_vs_step(avg_kernel_us, step_us):
     """A step kernel cannot take longer than a step: the sampled mean is held against the
-    TIMED region's wall time per step (ms_per_step), whichever pass the samples came from.
+    timed region's wall time per step (ms_per_step), the steps it was sampled in.
     When the mean exceeds it the kernel figure is not trusted and the roofline fraction is
     withheld (None) with the reason."""
     if not (avg_kernel_us == avg_kernel_us) or not (step_us > 0):  # nan: not timed
@@ -341,14 +334,14 @@ def init_dist(gpu, backend="nccl"):
     return torch.device("cpu")
 
 
-def collect(elapsed, avg_kernel_s, sample_step_s, ep_stats, ep_recs, coll):
+def collect(elapsed, avg_kernel_s, warm_step_s, ep_stats, ep_recs, coll):
     """After the timed region: the MAX of the clocks over ranks (one all_reduce) and the
     timed steps' episode statistics (per-rank count / return sum, f64 [2]) and per-board
     last-episode records (16 B per board) gathered to rank 0 -- the only exchange of a run,
-    over RCCL on GPUs.  Returns ((elapsed, avg_kernel_s, sample_step_s), per_rank [W, 2],
+    over RCCL on GPUs.  Returns ((elapsed, avg_kernel_s, warm_step_s), per_rank [W, 2],
     (ret, length, win)); the last two are None off rank 0."""
     from gym_TD import shard
-    t = shard.max_over_ranks(torch.tensor([elapsed, avg_kernel_s, sample_step_s], dtype=torch.float64, device=coll))
+    t = shard.max_over_ranks(torch.tensor([elapsed, avg_kernel_s, warm_step_s], dtype=torch.float64, device=coll))
     per_rank = shard.gather_stats(ep_stats.to(coll))
     recs = shard.gather_episode_records(*[x.to(coll) for x in ep_recs])
     return tuple(float(v) for v in t.cpu()), per_rank, recs
@@ -380,10 +373,8 @@ def main():
     ap.add_argument("--step-kernel", default="auto", choices=("auto", "large", "small", "small2"),
                     help="diagnostic: force a step kernel (td_set_step_kernel); default td_create's rule")
     ap.add_argument("--event-every", type=int, default=None,
-                    help="timed launches per sampled kernel duration (default 8; every launch perturbs the step)")
-    ap.add_argument("--kernel-sampling", default="pre", choices=("pre", "post"),
-                    help="a timed region too short to sample (< 64 steps): the sampled pass runs right before "
-                         "the warm-up ('pre') or behind the timed region after 16 warm steps ('post')")
+                    help="timed launches per sampled kernel duration (default: event_every, from the warm-up's "
+                         "step time; every launch perturbs the step)")
     ap.add_argument("--refill-interval", type=int, default=None,
                     help="diagnostic: steps between layout-refill launches in the timed region (0 = none)")
     args = ap.parse_args()
@@ -447,15 +438,9 @@ def main():
         eng.step(def_act=d, atk_act=a)
     acts = pool if multi else draw(K)
     stream = torch.cuda.current_stream(dev)
-    # HIP events bracket every `every`-th step kernel on its stream: the kernel's
-    # duration is sampled live over the timed region without a timing event pair
-    # (and its cache flush) behind every launch
-    every = event_every(K, args.event_every)
-    plan, n_plan, every = timing_plan(K, every) if args.timing == "dispatch" else ("timed", 0, every)
-    sampled = set(range(0, K, every)) if args.timing == "marker" else set()
-    ev = {k: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for k in sampled}
     if args.refill_interval is not None:
         eng.set_refill_interval(args.refill_interval)
+    sampled, ev = set(), {}  # --timing marker: torch event pairs around the sampled steps
 
     def run_steps(n, first):
         for k in range(n):
@@ -466,24 +451,21 @@ def main():
             if first + k in sampled:
                 ev[first + k][1].record(stream)
 
-    if plan == "pre" and args.kernel_sampling == "post":
-        plan = "post"
-    sample_wall, n_sample_steps, kern_pre = None, K, None
-    if plan == "pre":
-        # a timed region too short to sample: the kernel durations come from a steady-state
-        # pass right before it; the timed steps run without timing events
-        eng.kernel_timing((n_plan + every - 1) // every, every)
-        torch.cuda.synchronize(dev)
-        t1 = time.perf_counter()
-        run_steps(n_plan, 0)
-        torch.cuda.synchronize(dev)
-        sample_wall, n_sample_steps = time.perf_counter() - t1, n_plan
-        kern_pre = (eng.kernel_times().astype(np.float64) / 1e3).tolist()
-        eng.kernel_timing(0)
-    run_steps(W, 0)  # warm-up
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    run_steps(W, 0)  # warm-up: its wall time per step sets the sampling stride
+    torch.cuda.synchronize(dev)
+    warm_step_s = (time.perf_counter() - t1) / W if W > 0 else float("nan")
+    # HIP events bound to every `every`-th step kernel of the timed region (their own
+    # dispatch's timestamps): the kernel's duration is sampled live in the steps timed
+    every = event_every(K, warm_step_s * 1e6 if W > 0 else None, args.event_every)
+    n_samples = (K + every - 1) // every
+    if args.timing == "dispatch":
+        eng.kernel_timing(n_samples, every)
+    elif args.timing == "marker":
+        sampled = set(range(0, K, every))
+        ev = {k: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for k in sampled}
     eng.episode_stats(clear=True)  # the device accumulates finished episodes of the timed steps
-    if plan == "timed" and args.timing == "dispatch":
-        eng.kernel_timing(n_plan, every)  # timestamped by their own dispatch
 
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -501,30 +483,18 @@ def main():
     flags = eng.flags()
     ep_stats = eng.episode_stats(clear=True)
     ep_recs = eng.episode_records()
-    if plan == "post":
-        run_steps(16, K)
-        eng.kernel_timing((n_plan + every - 1) // every, every)
-        torch.cuda.synchronize(dev)
-        t1 = time.perf_counter()
-        run_steps(n_plan, K + 16)
-        torch.cuda.synchronize(dev)
-        sample_wall, n_sample_steps = time.perf_counter() - t1, n_plan
-    if sample_wall is None:
-        sample_wall = elapsed  # wall time of the steps the kernel samples come from
-    if kern_pre is not None:
-        kern_ms = kern_pre
-    elif args.timing == "dispatch":
+    if args.timing == "dispatch":
         kern_ms = (eng.kernel_times().astype(np.float64) / 1e3).tolist()
         eng.kernel_timing(0)
     elif args.timing == "marker":
         kern_ms = [s.elapsed_time(e) for s, e in ev.values()]
     else:
         kern_ms = [float("nan")]
-    avg_kernel_s = float(np.mean(kern_ms)) / 1e3
+    avg_kernel_s = float(np.mean(kern_ms)) / 1e3 if kern_ms else float("nan")
     # after timing: MAX of the clocks over ranks, and the episode statistics of the
     # timed steps gathered to rank 0 (the only exchange; RCCL on GPUs)
-    (elapsed, avg_kernel_s, sample_step_s), per_rank, recs = collect(
-        elapsed, avg_kernel_s, sample_wall / n_sample_steps, ep_stats, ep_recs, coll)
+    (elapsed, avg_kernel_s, warm_step_s), per_rank, recs = collect(
+        elapsed, avg_kernel_s, warm_step_s, ep_stats, ep_recs, coll)
     reported_world = dist.get_world_size() if world > 1 else 1  # what the process group (RCCL) reports
 
     if rank == 0:
@@ -554,15 +524,10 @@ def main():
                          "avg_kernel_us": avg_kernel_s * 1e6,
                          "kernel_samples": len(kern_ms) * world,
                          "kernel_exceeds_step": exceeds,
-                         "kernel_timing": {"dispatch": "dispatch-packet timestamps of every %dth launch (td_kernel_timing) "
-                                                       "%s, %.2f us wall per step there" % (
-                                                           every, "of the timed region" if plan == "timed" else
-                                                           "of an untimed %d-step pass %s (the timed steps ran without "
-                                                           "timing events)" % (n_plan, "right before the warm-up and the "
-                                                                               "timed region" if plan == "pre" else
-                                                                               "behind the timed region"),
-                                                           sample_step_s * 1e6),
-                                           "marker": "torch event pairs around every %dth launch" % every,
+                         "kernel_timing": {"dispatch": "dispatch-packet timestamps (td_kernel_timing) of every %dth launch "
+                                                       "of the timed region (%d samples; warm-up %.2f us per step)" % (
+                                                           every, len(kern_ms), warm_step_s * 1e6),
+                                           "marker": "torch event pairs around every %dth launch of the timed region" % every,
                                            "none": "not timed"}[args.timing],
                          "algorithmic_bytes_per_launch": B * bpe},
             "board_flags_nonzero": int((flags != 0).sum()),

@@ -115,5 +115,31 @@ s9)  # the driver's command: where the kernel is sampled (pre / post pass), and 
     run drv_256_$r 300 python bench.py --gpus 1 --steps 256 --warmup 5 --no-cpu-baseline --event-every 32 || exit 1; line drv_256_$r
   done
   ;;
+s10)  # is the slow 20-step window after the pre-pass the pass or the step range?  timed-region sampling every 2nd/4th launch at K=20
+  for bi in 1200 1456 1461 1520; do
+    run none_b$bi 300 python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --timing none --burnin $bi || exit 1; line none_b$bi
+  done
+  for r in 1 2; do
+    for bb in 65536 8192 4096; do
+      run none_${bb}_$r 300 python bench.py --global-batch $bb --steps 20 --warmup 5 --no-cpu-baseline --timing none || exit 1; line none_${bb}_$r
+      for e in 2 4; do
+        run e${e}_${bb}_$r 300 python bench.py --global-batch $bb --steps 20 --warmup 5 --no-cpu-baseline --event-every $e || exit 1; line e${e}_${bb}_$r
+      done
+    done
+  done
+  ;;
+s11)  # kernel sampled inside the timed region (stride from the warm-up): the driver's command, its kernel trace, the other lines
+  for r in 1 2 3; do
+    run drv_$r 300 python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline || exit 1; line drv_$r
+  done
+  run kt_drv 300 timeout -s KILL 280 rocprofv3 --kernel-trace --stats -d $O/kt_drv -o kt --output-format csv -- python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline || exit 1
+  line kt_drv; grep -h "td_step_kernel" $(find $O/kt_drv -name "*kernel_stats.csv") | cut -c1-200
+  for bb in 8192 4096; do
+    run k20_$bb 300 python bench.py --global-batch $bb --steps 20 --warmup 5 --no-cpu-baseline || exit 1; line k20_$bb
+    run k2000_$bb 300 python bench.py --global-batch $bb --steps 2000 --no-cpu-baseline || exit 1; line k2000_$bb
+  done
+  run p2 300 python bench.py --workload 2p-middle-multi --no-cpu-baseline --steps 200 || exit 1; line p2
+  run l30 300 python bench.py --workload def-large --global-batch 16384 --no-cpu-baseline --steps 200 || exit 1; line l30
+  ;;
 *) echo "unknown session $S"; exit 2;;
 esac

@@ -87,15 +87,19 @@ def test_gpus_n_starts_n_ranks(monkeypatch):
     assert cmd[-4:] == [bench.os.path.abspath(bench.__file__), "--gpus", "4", "--steps", "5"][-4:]
 
 
-def test_short_runs_sample_enough_launches():
-    # the driver's 20-step line: no events in the timed region; a 256-step pass right before
-    # it (behind the burn-in) sampled every 32nd launch (8 samples)
-    assert bench.timing_plan(20, 8) == ("pre", 256, 32)
-    assert bench.timing_plan(32, 8) == ("pre", 256, 32)
-    assert bench.timing_plan(64, 8) == ("timed", 8, 8)
-    assert bench.timing_plan(2000, 8) == ("timed", 250, 8)
-    assert bench.timing_plan(5, 1) == ("pre", 256, 32)
-    assert bench.PRE_STEPS // bench.PRE_EVERY >= bench.KERNEL_SAMPLES_MIN
+def test_sampling_stride_follows_the_step_time():
+    # the kernel is sampled inside the timed region; the stride keeps the events' cost
+    # (EVENT_COST_US per sampled launch) under EVENT_PERTURB of the step, with >= 2 samples
+    assert bench.event_every(20, 210.0) == 2  # the driver's line: 10 samples
+    assert bench.event_every(20, 33.0) == 10  # 8,192 boards: capped at half the timed steps
+    assert bench.event_every(2000, 33.0) == 10
+    assert bench.event_every(2000, 21.0) == 15
+    assert bench.event_every(1, 210.0) == 2  # one timed step: one sample
+    assert bench.event_every(20, None) == bench.EVENT_EVERY  # --warmup 0
+    assert bench.event_every(20, 210.0, override=1) == 1
+    for steps, us in ((20, 210.0), (300, 497.0), (2000, 21.0), (200, 300.0)):
+        k = bench.event_every(steps, us)
+        assert bench.EVENT_COST_US / (k * us) <= bench.EVENT_PERTURB or k == (steps + 1) // 2
 
 
 def test_kernel_longer_than_the_step_withholds_the_fraction():
