@@ -141,5 +141,17 @@ s11)  # kernel sampled inside the timed region (stride from the warm-up): the dr
   run p2 300 python bench.py --workload 2p-middle-multi --no-cpu-baseline --steps 200 || exit 1; line p2
   run l30 300 python bench.py --workload def-large --global-batch 16384 --no-cpu-baseline --steps 200 || exit 1; line l30
   ;;
+s12)  # 16-bit cell words at L = 10: the GPU suite, the driver's command, the L = 10 lines, the bytes at 65,536
+  gpusuite 900; rc=$?; [ $rc -le 1 ] || exit $rc
+  for r in 1 2; do
+    run drv_$r 300 python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline || exit 1; line drv_$r
+    run b65536_$r 300 python bench.py --steps 300 --no-cpu-baseline || exit 1; line b65536_$r
+  done
+  for bb in 8192 4096 32768; do
+    run b${bb} 300 python bench.py --global-batch $bb --steps 2000 --no-cpu-baseline || exit 1; line b$bb
+  done
+  OUT=$O NAME=c16_65536 B=65536 timeout -k 10 700 bash scripts/pmc_ab.sh || exit 1
+  rm -rf $O/c16_65536/FETCH_SIZE $O/c16_65536/WRITE_SIZE
+  ;;
 *) echo "unknown session $S"; exit 2;;
 esac
