@@ -454,6 +454,10 @@ __device__ __forceinline__ bool scan_fold(Smem<NC>& S, int lane, int ncr, const 
     const i64x2* A2 = reinterpret_cast<const i64x2*>(A);
     const int n2 = n / 2;
     constexpr int K = 8;  // 16-B loads in flight per lane
+    // (not unrolled: with the trip count known (NC) the compiler unrolled this loop and
+    // hoisted the next rounds' loads, 85-91 VGPRs at 20x20 and 182-188 at 30x30 in every
+    // multi-action kernel; rolled, 62-63)
+#pragma unroll 1
     for (int base = 0; base < n2; base += 64 * K) {
       i64x2 v[K];
 #pragma unroll
@@ -1911,11 +1915,11 @@ __global__ __launch_bounds__(64) void td_step_kernel(StepArgs a) {
 // limit for 8 resident waves (MI355X_MICROARCH.md, residency), so 8,192 boards -- 8
 // GPUs' share of BASELINE's 65,536 -- run as ONE round instead of 6,144 + 2,048.  At
 // 65,536 boards the same build is 7 % slower (SGPR spill code), hence two kernels.
-// The two-wave 20x20 kernels of the multi-action scan and of TD-atk do not fit 64 VGPRs:
-// at 8 waves per SIMD they spilled (112-116 / 8 B of scratch per lane; the scan still
-// spilled at 6), so 5 / 6.
+// The two-wave 20x20 TD-atk kernel does not fit 64 VGPRs: at 8 waves per SIMD it spilled
+// (8 B of scratch per lane), so 6.  (The multi-action scan kernels ran at 5 until the
+// flag fold's loop was kept rolled, scan_fold.)
 template <int LT, int MODE, bool SCAN>
-constexpr int small2_cap() { return LT == 20 && SCAN ? 5 : LT == 20 && MODE == MODE_ATK ? 6 : 8; }
+constexpr int small2_cap() { return LT == 20 && MODE == MODE_ATK && !SCAN ? 6 : 8; }
 #define TD_SMALL_ATTR __attribute__((amdgpu_waves_per_eu(8, 8)))
 #define TD_SMALL2_ATTR __attribute__((amdgpu_waves_per_eu(small2_cap<LT, MODE, SCAN>(), small2_cap<LT, MODE, SCAN>())))
 template <int LT, int MODE, bool SCAN>

@@ -153,5 +153,24 @@ s12)  # 16-bit cell words at L = 10: the GPU suite, the driver's command, the L 
   OUT=$O NAME=c16_65536 B=65536 timeout -k 10 700 bash scripts/pmc_ab.sh || exit 1
   rm -rf $O/c16_65536/FETCH_SIZE $O/c16_65536/WRITE_SIZE
   ;;
+s13)  # A/B on one box: this build (16-bit cell words, rolled flag fold + 8 waves/SIMD for the multi-action scan) vs libtdstep_prev.so
+  for r in 1 2; do
+    for v in prev new; do
+      lib=$PWD/gym-td_amd/lib/libtdstep.so; [ $v = prev ] && lib=$PWD/gym-td_amd/lib/libtdstep_prev.so
+      TDSTEP_LIB=$lib run ${v}_p2_$r 300 python bench.py --workload 2p-middle-multi --steps 200 --no-cpu-baseline --timing none || exit 1; line ${v}_p2_$r
+    done
+    for bb in 4096 8192 16384 65536; do
+      st=2000; [ $bb -ge 65536 ] && st=300
+      for v in prev new; do
+        lib=$PWD/gym-td_amd/lib/libtdstep.so; [ $v = prev ] && lib=$PWD/gym-td_amd/lib/libtdstep_prev.so
+        TDSTEP_LIB=$lib run ${v}_${bb}_$r 300 python bench.py --global-batch $bb --steps $st --no-cpu-baseline --timing none || exit 1; line ${v}_${bb}_$r
+      done
+    done
+  done
+  for v in prev new; do
+    lib=$PWD/gym-td_amd/lib/libtdstep.so; [ $v = prev ] && lib=$PWD/gym-td_amd/lib/libtdstep_prev.so
+    TDSTEP_LIB=$lib run ${v}_p2_32768 300 python bench.py --workload 2p-middle-multi --global-batch 32768 --steps 100 --no-cpu-baseline --timing none || exit 1; line ${v}_p2_32768
+  done
+  ;;
 *) echo "unknown session $S"; exit 2;;
 esac
