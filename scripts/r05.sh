@@ -172,5 +172,16 @@ s13)  # A/B on one box: this build (16-bit cell words, rolled flag fold + 8 wave
     TDSTEP_LIB=$lib run ${v}_p2_32768 300 python bench.py --workload 2p-middle-multi --global-batch 32768 --steps 100 --no-cpu-baseline --timing none || exit 1; line ${v}_p2_32768
   done
   ;;
+s14)  # probes: c16 without the end / start compares (v1: wrong observation, timing only); the u32 build with vmcnt(0) after the opponent prefetch (v2)
+  for r in 1 2; do
+    for bb in 4096 16384 8192 65536; do
+      st=2000; [ $bb -ge 65536 ] && st=300
+      for v in prev new v1 v2; do
+        lib=$PWD/gym-td_amd/lib/libtdstep_$v.so; [ $v = new ] && lib=$PWD/gym-td_amd/lib/libtdstep.so
+        TDSTEP_LIB=$lib run ${v}_${bb}_$r 300 python bench.py --global-batch $bb --steps $st --no-cpu-baseline --timing none || exit 1; line ${v}_${bb}_$r
+      done
+    done
+  done
+  ;;
 *) echo "unknown session $S"; exit 2;;
 esac
