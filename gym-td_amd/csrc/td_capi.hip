@@ -78,7 +78,6 @@ constexpr int kSideStreams = 2;  // refill streams: one stuck on a long draw doe
 struct td_handle {
   int L = 0, NC = 0, B = 0, mode = 0, multi = 0, difficulty = 1, device = 0, autoreset = 1;
   int opp_np = 0;  // random_agent=False
-  int cell16 = 0;  // 16-bit HBM cell words (td_common.h kCell16: the L = 10 kernels)
   int small = 0, obs_wt = 0;  // the step kernel (0 large, 1 small, 2 small2), write-through observation stores
   int small_auto = 0;         // td_create's choice (TD_KERNEL_AUTO)
   std::string kernel_name;    // td_step_kernel_name
@@ -415,10 +414,6 @@ td_handle* td_create(const td_config* cfg, int map_size, int n_boards, int mode,
   }
   td_handle* h = new td_handle();
   h->L = map_size; h->NC = map_size * map_size; h->B = n_boards; h->mode = mode; h->multi = multi_action ? 1 : 0;
-  // the kernels launched for L = 10 are the <10> builds (NC = 100: 16-bit cell words);
-  // every other L runs a build with NC > 121 (<20>, <30> or the generic <0>)
-  static_assert(kCell16<100> && !kCell16<400> && !kCell16<32 * 32>, "cell word width by build (generic: L <= 32)");
-  h->cell16 = map_size == 10 ? 1 : 0;
   h->difficulty = difficulty; h->device = device; h->lw = layout_words(map_size);
   h->scratch_stride = (sizeof(RoadResume) + road_scratch_bytes(map_size) + 15) & ~(size_t)15;
   h->stage_cap = std::min(n_boards, 4096);
@@ -432,7 +427,7 @@ td_handle* td_create(const td_config* cfg, int map_size, int n_boards, int mode,
   rc |= dalloc(&h->d_en_inf, B * ECAP);
   rc |= dalloc(&h->d_tw_cd, B * TCAP);
   rc |= dalloc(&h->d_tw_inf, B * TCAP);
-  rc |= dalloc(&h->d_cells, B * h->NC / (h->cell16 ? 2 : 1));
+  rc |= dalloc(&h->d_cells, B * h->NC);
   rc |= dalloc(&h->d_opp, B * OPP_WORDS);
   rc |= dalloc(&h->d_hot, B * HOT_WORDS);
   rc |= dalloc(&h->d_np, B * OPP_WORDS);
@@ -897,29 +892,6 @@ static int state_copy(td_handle* h, int b0, int count, void* host, bool to_host)
     p = q;
     opp = (uint32_t*)(p + (size_t)count * (sizeof(TdHdr) + ECAP * 20 + TCAP * 12 + (size_t)h->NC * 4));
   }
-  const TdHdr* const rec_hdr = reinterpret_cast<const TdHdr*>(p);  // the buffer's header section
-  // the cell words: 32-bit in the buffer, 16-bit on the device at L = 10 (cell_pack16)
-  auto cp_cells = [&]() -> int {
-    if (!h->cell16) return cp(h->d_cells, (size_t)h->NC * 4);
-    const size_t n = (size_t)count * h->NC;
-    uint32_t* cw = reinterpret_cast<uint32_t*>(p);
-    uint16_t* d = reinterpret_cast<uint16_t*>(h->d_cells) + (size_t)b0 * h->NC;
-    std::vector<uint16_t> c16(n);
-    if (to_host) {
-      HIP_OK(hipMemcpy(c16.data(), d, n * 2, hipMemcpyDeviceToHost));
-      for (int i = 0; i < count; ++i) {
-        const TdHdr& x = rec_hdr[i];
-        for (int c = 0; c < h->NC; ++c)
-          cw[(size_t)i * h->NC + c] = cell_unpack16(c16[(size_t)i * h->NC + c], c, x.num_roads, x.end_cell,
-                                                    x.start_cell[0], x.start_cell[1], x.start_cell[2]);
-      }
-    } else {
-      for (size_t k = 0; k < n; ++k) c16[k] = (uint16_t)cell_pack16(cw[k]);
-      HIP_OK(hipMemcpy(d, c16.data(), n * 2, hipMemcpyHostToDevice));
-    }
-    p += n * 4;
-    return 0;
-  };
   std::vector<uint32_t> hot((size_t)count * HOT_WORDS);
   if (!to_host) {  // the hot record follows the imported words (no pre-drawn outputs)
     for (int i = 0; i < count; ++i) {
@@ -930,7 +902,7 @@ static int state_copy(td_handle* h, int b0, int count, void* host, bool to_host)
   }
   if (cp(h->d_hdr, sizeof(TdHdr)) || cp(h->d_en_lp, ECAP * 8) || cp(h->d_en_mg, ECAP * 8) ||
       cp(h->d_en_inf, ECAP * 4) || cp(h->d_tw_cd, TCAP * 8) || cp(h->d_tw_inf, TCAP * 4) ||
-      cp_cells() || cp(h->d_opp, OPP_WORDS * 4))
+      cp(h->d_cells, (size_t)h->NC * 4) || cp(h->d_opp, OPP_WORDS * 4))
     return -1;
   if (to_host) {  // position and lazy boundary live in the hot record
     HIP_OK(hipMemcpy(hot.data(), h->d_hot + (size_t)b0 * HOT_WORDS, hot.size() * 4, hipMemcpyDeviceToHost));
@@ -962,19 +934,6 @@ int td_import_state(td_handle* h, int b0, int count, const void* host_src) {
                   x.max_base_LP);
     if (x.n_en < 0 || x.n_en > ECAP || x.n_tw < 0 || x.n_tw > TCAP)
       return fail("td_import_state: board %d: %d enemies / %d towers exceed the capacity", b0 + i, x.n_en, x.n_tw);
-    if (h->cell16) {  // the words must survive the 16-bit device format (td_common.h cell_pack16)
-      const uint32_t* cw = reinterpret_cast<const uint32_t*>(static_cast<const uint8_t*>(host_src) +
-                                                             (size_t)count * (sizeof(TdHdr) + ECAP * 20 + TCAP * 12)) +
-                           (size_t)i * h->NC;
-      for (int c = 0; c < h->NC; ++c) {
-        const uint32_t w = cw[c] & ~(0x3Fu << 10);  // (bits 10-15: not part of the format)
-        if (!cell_fits16(w) || cell_unpack16(cell_pack16(w), c, x.num_roads, x.end_cell, x.start_cell[0],
-                                             x.start_cell[1], x.start_cell[2]) != w)
-          return fail("td_import_state: board %d cell %d: word 0x%x does not fit the L = 10 cell format (map[6] > 15, "
-                      "distance > 127, map[0] != any road, or end / start bits other than the header's)",
-                      b0 + i, c, (unsigned)cw[c]);
-      }
-    }
   }
   return state_copy(h, b0, count, const_cast<void*>(host_src), false);
 }

@@ -8,8 +8,7 @@
 //   en_inf  u32              [B][ECAP]   cell | type<<12 | lv<<14 | slowdown<<16 | cfg epoch<<24
 //   tw_cd   f64              [B][TCAP]   tower cool-down     (Tower.cd, :54)
 //   tw_inf  u32              [B][TCAP]   cell | type<<12 | lv<<14 | build epoch<<16 | stats epoch<<24
-//   cells   u32              [B][L*L]    cell words (td_layout.h bit layout); u16 at L = 10
-//                                        (cell_pack16: the step re-reads them every step)
+//   cells   u32              [B][L*L]    cell words (td_layout.h bit layout)
 //   opp_mt  u32              [B][626]    CPython-random MT19937 of the built-in opponent (lazy twist)
 //   nxt     u32              [B][8+L*L]  staged layout for the board's next episode
 // Enemy / tower lists keep the reference's list order (index order).
@@ -75,36 +74,6 @@ struct alignas(16) TdDevCfg {
 __host__ __device__ inline int cw_dist(uint32_t w) { return (int)((w >> 16) & 0xffu); }
 __host__ __device__ inline int cw_dir(uint32_t w) { return (int)((w >> 8) & 3u); }
 __host__ __device__ inline int cw_block(uint32_t w) { return (int)(w >> 24); }
-
-// HBM cell words of the L = 10 kernels (every build with NC <= 121): 16 bits; the LDS
-// image and the layout records keep td_layout.h's 32-bit word.  Per cell:
-//   bits 0-2   road planes map[1..3]; map[0] is their OR (TDBoard.py:38-42 sets both)
-//   bits 3-4   next direction map[5]
-//   bits 5-11  distance to the end map[4] (< L*L <= 121)
-//   bits 12-15 build-block counter map[6]: at most 5 -- a road cell's mark plus one tower
-//              per quadrant of the cell's tower_distance diamond (a tower is built only
-//              where no tower is within tower_distance, TDBoard.py:232-245, so two in one
-//              quadrant, whose L1 diameter is tower_distance, cannot both exist)
-// The end / start bits (4, 5-7) are the header's end_cell / start_cell[0, num_roads).
-// (-200 B read per board and step at 10x10: the cell words are re-read every step.)
-template <int NC>
-constexpr bool kCell16 = NC <= 121;
-__host__ __device__ inline uint32_t cell_pack16(uint32_t w) {
-  return ((w >> 1) & 7u) | (((w >> 8) & 3u) << 3) | (((w >> 16) & 0x7fu) << 5) | (((w >> 24) & 0xfu) << 12);
-}
-// Whether cell_pack16 keeps a 32-bit word (bits 10-15, the step's tower nibble, excluded).
-__host__ __device__ inline bool cell_fits16(uint32_t w) {
-  return ((w & 1u) != 0u) == (((w >> 1) & 7u) != 0u) && ((w >> 16) & 0xffu) < 128u && (w >> 24) < 16u;
-}
-__host__ __device__ inline uint32_t cell_unpack16(uint32_t h, int c, int nr, int end_cell, int s0, int s1, int s2) {
-  const uint32_t roads = h & 7u;
-  uint32_t w = (roads ? 1u : 0u) | (roads << 1) | (((h >> 3) & 3u) << 8) | (((h >> 5) & 0x7fu) << 16) | ((h >> 12) << 24);
-  if (nr >= 1) {
-    w |= (c == end_cell ? 16u : 0u) | (c == s0 ? 32u : 0u);
-    w |= (nr > 1 && c == s1 ? 64u : 0u) | (nr > 2 && c == s2 ? 128u : 0u);
-  }
-  return w;
-}
 
 __host__ __device__ inline uint32_t en_pack(int cell, int type, int lv, int slow, int ep) {
   return (uint32_t)cell | ((uint32_t)type << 12) | ((uint32_t)lv << 14) | ((uint32_t)slow << 16) | ((uint32_t)ep << 24);

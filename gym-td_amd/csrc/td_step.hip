@@ -1236,7 +1236,7 @@ static_assert(offsetof(TdHdr, steps) == 24 && offsetof(TdHdr, start_cell) == 56 
                   offsetof(TdHdr, max_cost) == 80 && offsetof(TdHdr, max_base_LP) == 88,
               "Prefetch header word map");
 
-template <int PFE, int PFT, bool C16 = false>
+template <int PFE, int PFT>
 __device__ __forceinline__ void prefetch_issue(Prefetch& P, const StepArgs& a, int b, int lane, int ncr,
                                                bool want_act) {
   const size_t eb = (size_t)b * ECAP, tb = (size_t)b * TCAP, cb = (size_t)b * ncr;
@@ -1249,11 +1249,7 @@ __device__ __forceinline__ void prefetch_issue(Prefetch& P, const StepArgs& a, i
     P.tcd = a.tw_cd[tb + lane];
     P.tinf = a.tw_inf[tb + lane];
   }
-  if constexpr (C16) {  // 16-bit words (kCell16): four cells in 8 B, expanded in load_board
-    const uint2* g2 = reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(a.cells) + cb);
-    const uint2 h = lane < (ncr >> 2) ? g2[lane] : uint2{0u, 0u};
-    P.c4 = uint4{h.x, h.y, 0u, 0u};
-  } else if ((ncr & 3) == 0) {
+  if ((ncr & 3) == 0) {
     P.c4 = lane < (ncr >> 2) ? reinterpret_cast<const uint4*>(a.cells + cb)[lane] : uint4{0u, 0u, 0u, 0u};
   } else {  // (assigned whole: member-wise stores kept P.c4 in scratch in the generic-L build)
     P.c4 = uint4{lane < ncr ? a.cells[cb + lane] : 0u, lane + 64 < ncr ? a.cells[cb + lane + 64] : 0u, 0u, 0u};
@@ -1276,17 +1272,7 @@ __device__ __forceinline__ double lane_f64(uint32_t v, int l) {
 template <int NC, int PFE, int PFT>
 __device__ __forceinline__ void load_board(Smem<NC>& S, U& u, const Ctx& x, const StepArgs& a, int b, const Prefetch& P) {
   const size_t eb = (size_t)b * ECAP, cb = (size_t)b * x.NCr;
-  if constexpr (kCell16<NC>) {
-    // 16-bit words: the end / start bits from the header (cell_unpack16)
-    static_assert(NC % 4 == 0 && NC / 4 <= 64, "four cells per lane");
-    const int nr = (int)lane_word(P.w, 12), ec = (int)lane_word(P.w, 13);
-    const int s0 = (int)lane_word(P.w, 14), s1 = (int)lane_word(P.w, 15), s2 = (int)lane_word(P.w, 16);
-    const int c = 4 * x.lane;
-    if (x.lane < NC / 4)
-      reinterpret_cast<uint4*>(S.cell)[x.lane] =
-          uint4{cell_unpack16(P.c4.x & 0xffffu, c, nr, ec, s0, s1, s2), cell_unpack16(P.c4.x >> 16, c + 1, nr, ec, s0, s1, s2),
-                cell_unpack16(P.c4.y & 0xffffu, c + 2, nr, ec, s0, s1, s2), cell_unpack16(P.c4.y >> 16, c + 3, nr, ec, s0, s1, s2)};
-  } else if ((x.NCr & 3) == 0) {
+  if ((x.NCr & 3) == 0) {
     // 16-B cell loads: the first 256 cells came with the prefetch, the rest (L > 16)
     // are all issued before any is stored to LDS
     const int n4 = x.NCr >> 2;
@@ -1367,15 +1353,8 @@ __device__ __forceinline__ void reset_board(Smem<NC>& S, U& u, const Ctx& x, con
 template <int NC>
 __device__ __forceinline__ void store_cells(const Smem<NC>& S, const U& u, const Ctx& x, const StepArgs& a, int b) {
   const size_t cb = (size_t)b * x.NCr;
-  if constexpr (kCell16<NC>) {  // four cells per lane in 8 B (the tower nibble is not packed)
-    if (u.cells_dirty && x.lane < NC / 4) {
-      const uint4 w = reinterpret_cast<const uint4*>(S.cell)[x.lane];
-      uint2* g2 = reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(a.cells) + cb);
-      sst(&g2[x.lane], uint2{cell_pack16(w.x) | (cell_pack16(w.y) << 16), cell_pack16(w.z) | (cell_pack16(w.w) << 16)});
-    }
-  } else if (u.cells_dirty) {
+  if (u.cells_dirty)
     for (int i = x.lane; i < x.NCr; i += 64) sst(&a.cells[cb + i], S.cell[i] & ~kTwBits);
-  }
 }
 
 __device__ __forceinline__ TdHdr hdr_of(const U& u) {
@@ -1899,7 +1878,7 @@ __device__ __forceinline__ void step_kernel_body(const StepArgs& a) {
   const Ctx x{S.cfg, L, L * L, (int)(threadIdx.x & 63), a.cfgs, a.epoch};
   Prefetch P;
   constexpr int PF = SMALL ? PF_SMALL : PF_LARGE;
-  prefetch_issue<PF, PF, kCell16<NC>>(P, a, b, x.lane, x.NCr, MODE != MODE_ATK && !a.multi);
+  prefetch_issue<PF, PF>(P, a, b, x.lane, x.NCr, MODE != MODE_ATK && !a.multi);
   step_board<NC, LT, MODE, SCAN, SMALL>(S, x, a, b, P);
 }
 
@@ -1944,7 +1923,7 @@ __global__ __launch_bounds__(128) TD_SMALL2_ATTR void td_step_kernel_small2(Step
     stage_cfg(S, a.cfg);
     const Ctx x{S.cfg, LT, NC, lane, a.cfgs, a.epoch};
     Prefetch P;
-    prefetch_issue<PF_SMALL, PF_SMALL, kCell16<NC>>(P, a, b, lane, NC, MODE != MODE_ATK && !a.multi);
+    prefetch_issue<PF_SMALL, PF_SMALL>(P, a, b, lane, NC, MODE != MODE_ATK && !a.multi);
     step_board<NC, LT, MODE, SCAN, true, true>(S, x, a, b, P, &SO);
   } else {
     float* const obs = a.obs + (size_t)b * NCH * NC;
@@ -1994,7 +1973,7 @@ __global__ __launch_bounds__(64) void td_opponent_kernel(StepArgs a, int side, i
   const int L = LT ? LT : a.L;
   const Ctx x{S.cfg, L, L * L, (int)threadIdx.x, a.cfgs, a.epoch};
   Prefetch P;
-  prefetch_issue<PF_SMALL, PF_SMALL, kCell16<NC>>(P, a, b, x.lane, x.NCr, false);
+  prefetch_issue<PF_SMALL, PF_SMALL>(P, a, b, x.lane, x.NCr, false);
   U u;
   load_board<NC, PF_SMALL, PF_SMALL>(S, u, x, a, b, P);
   if (u.num_roads < 1 || u.num_roads > 3) return;  // never reset: nothing to act on

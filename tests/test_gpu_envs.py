@@ -442,39 +442,6 @@ def test_import_refuses_records_without_captured_fields():
         eng.close()
 
 
-def test_import_checks_the_16bit_cell_words():
-    """At L = 10 the device keeps 16-bit cell words (td_common.h cell_pack16): map[6] up to
-    15 and any distance < 128 round-trip through import / export; a word the format cannot
-    hold (map[6] 16, distance 128, an end bit off the header's end cell, map[0] without a
-    road plane) is refused and changes nothing."""
-    from gym_TD import _lib
-    L, B = 10, 4
-    seeds, _ = _first_ok_seeds(L, B, 6200, "def", False, 1)
-    eng = TDEngine(L, B, "def", False, 1, np_seeds=seeds, py_seeds=seeds, autoreset=False)
-    try:
-        eng.reset()
-        good = eng.export_state()
-        before = [canon.state_digest(eng.board_state(b)) for b in range(B)]
-        hd = good["hdr"][2]
-        off = [c for c in range(L * L) if c != int(hd["end_cell"]) and c not in [int(v) for v in hd["start_cell"]]][0]
-        st = {k: np.array(v, copy=True) for k, v in good.items()}
-        st["cells"][2][off] = (st["cells"][2][off] & 0x00FFFFFF) | (15 << 24)
-        st["cells"][2][off + 1] = (st["cells"][2][off + 1] & 0xFF00FFFF) | (127 << 16)
-        eng.import_state(st)
-        back = eng.export_state()
-        assert np.array_equal(back["cells"], st["cells"])
-        for bad in ((off, lambda w: (w & 0x00FFFFFF) | (16 << 24)), (off, lambda w: (w & 0xFF00FFFF) | (128 << 16)),
-                    (off, lambda w: w | 16), (off, lambda w: (w & ~0xF) | 1)):
-            st = {k: np.array(v, copy=True) for k, v in good.items()}
-            st["cells"][2][bad[0]] = bad[1](int(st["cells"][2][bad[0]]))
-            with pytest.raises(_lib.TDError, match="board 2 cell"):
-                eng.import_state(st)
-        eng.import_state(good)
-        assert [canon.state_digest(eng.board_state(b)) for b in range(B)] == before
-    finally:
-        eng.close()
-
-
 def test_config_epochs_recycled_past_256():
     """paramConfig every step for 300 steps (a curriculum): the device has 256 constant
     blocks, so after 255 changes td_set_config recycles blocks no live enemy or tower

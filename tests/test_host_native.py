@@ -235,36 +235,3 @@ def test_board_map_is_an_xcd_contiguous_permutation(B):
         ident = np.zeros(B, np.int32)
         assert lib.td_board_map(B, kind, 0, _lib.ptr(ident, _lib.ctypes.c_int32)) == 0
         assert np.array_equal(ident, np.arange(B))
-
-
-def _unpack16(h, c, nr, end, starts):
-    """td_common.h cell_unpack16 (the 16-bit HBM cell word of the L = 10 kernels)."""
-    roads = h & 7
-    w = (1 if roads else 0) | roads << 1 | ((h >> 3) & 3) << 8 | ((h >> 5) & 0x7F) << 16 | (h >> 12) << 24
-    if nr >= 1:
-        w |= (16 if c == end else 0) | (32 if c == starts[0] else 0)
-        w |= (64 if nr > 1 and c == starts[1] else 0) | (128 if nr > 2 and c == starts[2] else 0)
-    return w
-
-
-def _pack16(w):
-    return ((w >> 1) & 7) | ((w >> 8) & 3) << 3 | ((w >> 16) & 0x7F) << 5 | ((w >> 24) & 0xF) << 12
-
-
-def test_layout_records_fit_the_16bit_cell_words():
-    """Every L = 10 layout the generator draws survives the device's 16-bit cell words:
-    map[0] is the OR of the road planes, distances < 128, map[6] < 16, and the end / start
-    bits sit exactly on the record's end / start cells (td_common.h cell_pack16)."""
-    n = 0
-    for s in range(600):
-        w = np.zeros(625, np.uint32)
-        lib.td_np_seed(_p(w), s)
-        st, rec = generate_layout(w, 10)
-        if st != 0:
-            continue
-        nr, end, starts = int(rec[1]), int(rec[2]), [int(v) for v in rec[4:7]]
-        for c in range(100):
-            cw = int(rec[8 + c])
-            assert _unpack16(_pack16(cw), c, nr, end, starts) == cw, (s, c, hex(cw))
-        n += 1
-    assert n > 500
