@@ -183,5 +183,30 @@ s14)  # probes: c16 without the end / start compares (v1: wrong observation, tim
     done
   done
   ;;
+s15)  # per-phase instruction attribution at 8,192 boards: builds without the observation (x1), channel_scalars (x2), enemy_stats (x3)
+  BENCH="python bench.py --global-batch 8192 --steps 20 --warmup 2 --burnin 300 --no-cpu-baseline --timing none"
+  for v in base x1 x2 x3; do
+    lib=$PWD/gym-td_amd/lib/libtdstep_$v.so; [ $v = base ] && lib=$PWD/gym-td_amd/lib/libtdstep.so
+    TDSTEP_LIB=$lib run pmc1_$v 120 timeout -s KILL 100 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_SMEM SQ_INSTS_VMEM_WR -d $O/pmc1_$v -o pmc --output-format csv -- $BENCH || exit 1
+    TDSTEP_LIB=$lib run kt_$v 120 timeout -s KILL 100 rocprofv3 --kernel-trace --stats -d $O/kt_$v -o kt --output-format csv -- $BENCH || exit 1
+    TDSTEP_LIB=$lib run t_$v 300 python bench.py --global-batch 8192 --steps 2000 --no-cpu-baseline --timing none || exit 1; line t_$v
+  done
+  python3 scripts/pmc_compare.py $O base x1 x2 x3 > $O/pmc_compare.txt; cat $O/pmc_compare.txt
+  rm -rf $O/pmc1_* $O/kt_*
+  ;;
+s16)  # probes of the small kernel's shape: 4 waves per SIMD over 2 rounds (y1), two boards per wave in sequence (y3)
+  for r in 1 2; do
+    for v in base y1 y3; do
+      lib=$PWD/gym-td_amd/lib/libtdstep_$v.so; [ $v = base ] && lib=$PWD/gym-td_amd/lib/libtdstep.so
+      TDSTEP_LIB=$lib run ${v}_8192_$r 300 python bench.py --global-batch 8192 --steps 2000 --no-cpu-baseline --timing none || exit 1; line ${v}_8192_$r
+    done
+  done
+  for bb in 4096 16384; do
+    for v in base y3; do
+      lib=$PWD/gym-td_amd/lib/libtdstep_$v.so; [ $v = base ] && lib=$PWD/gym-td_amd/lib/libtdstep.so
+      TDSTEP_LIB=$lib run ${v}_small_$bb 300 python bench.py --global-batch $bb --steps 2000 --no-cpu-baseline --timing none --step-kernel small || exit 1; line ${v}_small_$bb
+    done
+  done
+  ;;
 *) echo "unknown session $S"; exit 2;;
 esac
