@@ -30,8 +30,34 @@ __device__ __forceinline__ uint32_t twr_of(uint32_t w) {
 __device__ __forceinline__ int pk_dir(uint32_t w) { return (int)((w >> 21) & 3u); }
 __device__ __forceinline__ int pk_dist(uint32_t w) { return (int)(w >> 24); }
 
-__device__ __forceinline__ int cheb(int a, int b, int L) {
-  int dr = a / L - b / L, dc = a % L - b % L;
+// Division by the board side L of a cell index (0 <= v < 1024, L <= 32) with one 24-bit
+// multiply, v_mul_u32_u24 (full rate): v / L = (v * Lm) >> 16, Lm = ceil(2^16 / L), exact
+// since (1024 - 1) * (Lm * L - 2^16) < 32 * 1024 < 2^16.  (Division by a constant takes
+// v_mul_hi_u32, and the remainder a v_mul_lo_u32: quarter-rate instructions.)
+__host__ __device__ constexpr uint32_t side_magic(int L) { return (65536u + (uint32_t)L - 1u) / (uint32_t)L; }
+__device__ __forceinline__ int div_side(int v, uint32_t Lm) { return (int)(__umul24((uint32_t)v, Lm) >> 16); }
+
+// x / D for 0 <= x < LIM, the same way at a compile-time divisor (the observation's unit
+// -> channel): the smallest shift S with (LIM - 1) * e < 2^S, e = M * D - 2^S
+// (Granlund-Montgomery), and a product below 2^32.
+template <int D, int LIM>
+struct Div24 {
+  static constexpr int pick() {
+    for (int s = 8; s <= 24; ++s) {
+      const long long m = ((1ll << s) + D - 1) / D, e = m * D - (1ll << s);
+      if ((long long)(LIM - 1) * e < (1ll << s) && (long long)(LIM - 1) * m < (1ll << 32) && m < (1ll << 24)) return s;
+    }
+    return -1;
+  }
+  static constexpr int S = pick();
+  static_assert(S > 0, "no exact 24-bit reciprocal");
+  static constexpr uint32_t M = (uint32_t)(((1ll << S) + D - 1) / D);
+  __device__ static int div(int x) { return (int)(__umul24((uint32_t)x, M) >> S); }
+};
+
+__device__ __forceinline__ int cheb(int a, int b, int L, uint32_t Lm) {
+  const int ra = div_side(a, Lm), rb = div_side(b, Lm);
+  int dr = ra - rb, dc = (a - ra * L) - (b - rb * L);
   dr = dr < 0 ? -dr : dr;
   dc = dc < 0 ? -dc : dc;
   return dr > dc ? dr : dc;

@@ -107,6 +107,7 @@ struct Ctx {
   int L, NCr, lane;
   const TdDevCfg* tab;  // every epoch's block (HBM)
   int ep;
+  uint32_t Lm = side_magic(L);  // div_side's multiplier
 };
 
 // A value an enemy or tower captured when it was created or upgraded (TDElements.py:
@@ -115,10 +116,14 @@ struct Ctx {
 // (The compiler merges the two loads into one FLAT load of a selected pointer, which
 // counts in vmcnt; keeping them apart -- an empty asm on the HBM value -- measured
 // +-0.6 % across 65,536 / 8,192 / 4,096 boards, profiles/r03/s17: not kept.)
+// (The older block's address with a 24-bit multiply: ep * sizeof(TdDevCfg) < 2^24; as
+// x.tab[ep] it took a 64-bit v_mad_u64_u32, a quarter-rate instruction, at every call.)
 template <class F>
 __device__ __forceinline__ double captured(const Ctx& x, int ep, F f) {
   double v = f(x.C);
-  if (ep != x.ep) v = f(x.tab[ep]);
+  if (ep != x.ep)
+    v = f(*reinterpret_cast<const TdDevCfg*>(reinterpret_cast<const char*>(x.tab) +
+                                             __umul24((uint32_t)ep, (uint32_t)sizeof(TdDevCfg))));
   return v;
 }
 
@@ -331,7 +336,7 @@ __device__ __forceinline__ void with_opp_rng(const StepArgs& a, int b, int lane,
 template <int NC>
 __device__ __forceinline__ void diamond(Smem<NC>& S, const Ctx& x, int cell, int delta) {
   const int k = x.C.tower_distance, W = 2 * k + 1, L = x.L;
-  const int r0 = cell / L, c0 = cell % L;
+  const int r0 = div_side(cell, x.Lm), c0 = cell - r0 * L;
   for (int idx = x.lane; idx < W * W; idx += 64) {
     int i = idx / W - k, j = idx % W - k;
     int ai = i < 0 ? -i : i, aj = j < 0 ? -j : j;
@@ -713,7 +718,7 @@ __device__ __forceinline__ double board_step(Smem<NC>& S, U& u, const Ctx& x, co
       int tgt = -1;
       for (int j = 0; j < n; ++j) {  // first enemy within range (list order)
         const int ec = en_cell(rdl(inf[0], j));
-        if (tgt < 0 && (double)cheb(ec, tc, L) <= rge) tgt = j;
+        if (tgt < 0 && (double)cheb(ec, tc, L, x.Lm) <= rge) tgt = j;
       }
       const int tgc = en_cell((uint32_t)__shfl((int)inf[0], tgt < 0 ? 0 : tgt));  // every lane shuffles
       const double dr = tt >= 2 && tgt >= 0 ? tp[4 * lane + 3] : -1.0;
@@ -721,7 +726,7 @@ __device__ __forceinline__ double board_step(Smem<NC>& S, U& u, const Ctx& x, co
       if (tt == 3)
         for (int j = 0; j < n; ++j) {
           const int ec = en_cell(rdl(inf[0], j));
-          if (frz < 0 && (double)cheb(tgc, ec, L) <= dr) frz = j;
+          if (frz < 0 && (double)cheb(tgc, ec, L, x.Lm) <= dr) frz = j;
         }
       if (tgt >= 0) cd = dadd(cd, tp[4 * lane + 1]);         // cd += intv
       if (tries && cd < 0.0) cd = 0.0;                       // :311-312
@@ -735,7 +740,7 @@ __device__ __forceinline__ double board_step(Smem<NC>& S, U& u, const Ctx& x, co
           if (lane == (int)rdl((uint32_t)tgt, k)) lp[0] = damage(lp[0], atk, e_def(x, inf[0]), kt == 1);
         } else if (kt == 2) {  // TowerBomb splash (:95-110)
           const int kc = (int)rdl((uint32_t)tgc, k);
-          if (val[0] && (double)cheb(kc, en_cell(inf[0]), L) <= tp[4 * k + 3])
+          if (val[0] && (double)cheb(kc, en_cell(inf[0]), L, x.Lm) <= tp[4 * k + 3])
             lp[0] = damage(lp[0], atk, e_def(x, inf[0]), false);
         } else if (lane == (int)rdl((uint32_t)frz, k)) {
           lp[0] = damage(lp[0], atk, 0.0, true);
@@ -749,8 +754,8 @@ __device__ __forceinline__ double board_step(Smem<NC>& S, U& u, const Ctx& x, co
         const uint32_t ti = rdl(tinf_l, k);
         const int tt = (ti >> 12) & 3, tc = ti & 0xfff;
         const double rge = tp[4 * k];
-        bool in0 = val[0] && (double)cheb(en_cell(inf[0]), tc, L) <= rge;
-        bool in1 = val[1] && (double)cheb(en_cell(inf[1]), tc, L) <= rge;
+        bool in0 = val[0] && (double)cheb(en_cell(inf[0]), tc, L, x.Lm) <= rge;
+        bool in1 = val[1] && (double)cheb(en_cell(inf[1]), tc, L, x.Lm) <= rge;
         uint64_t m0 = ballot(in0), m1 = ballot(in1);
         if (m0 | m1) {
           const int tgt = m0 ? ctz64(m0) : 64 + ctz64(m1);
@@ -768,11 +773,11 @@ __device__ __forceinline__ double board_step(Smem<NC>& S, U& u, const Ctx& x, co
             if (tt == 2) {  // TowerBomb splash (:95-110)
 #pragma unroll
               for (int s = 0; s < 2; ++s)
-                if (val[s] && (double)cheb(tgc, en_cell(inf[s]), L) <= dr)
+                if (val[s] && (double)cheb(tgc, en_cell(inf[s]), L, x.Lm) <= dr)
                   lp[s] = damage(lp[s], atk, e_def(x, inf[s]), false);
             } else {  // TowerFrozen: first enemy within splash of the target (:112-132)
-              bool h0 = val[0] && (double)cheb(tgc, en_cell(inf[0]), L) <= dr;
-              bool h1 = val[1] && (double)cheb(tgc, en_cell(inf[1]), L) <= dr;
+              bool h0 = val[0] && (double)cheb(tgc, en_cell(inf[0]), L, x.Lm) <= dr;
+              bool h1 = val[1] && (double)cheb(tgc, en_cell(inf[1]), L, x.Lm) <= dr;
               uint64_t q0 = ballot(h0), q1 = ballot(h1);
               if (q0 | q1) {
                 const int f = q0 ? ctz64(q0) : 64 + ctz64(q1);
@@ -814,7 +819,8 @@ __device__ __forceinline__ double board_step(Smem<NC>& S, U& u, const Ctx& x, co
       mg[s] = dsub(mg[s], 1.0);
       const int d = pk_dir(S.cell[cell]);
       // map[5] codes (TDBoard.py:319): 0:+c 1:-c 2:+r 3:-r
-      int r = cell / L + (d == 2) - (d == 3), c = cell % L + (d == 0) - (d == 1);
+      const int r1 = div_side(cell, x.Lm);
+      int r = r1 + (d == 2) - (d == 3), c = cell - r1 * L + (d == 0) - (d == 1);
       if (r < 0 || r >= L || c < 0 || c >= L) { u.flags |= FLAG_BAD_MOVE; break; }
       cell = r * L + c;
       if (cell == u.end_cell) { leak[s] = true; break; }
@@ -1121,6 +1127,7 @@ __device__ __forceinline__ void write_obs_lines(const Smem<NC>& S, int lane, flo
   const int head = mis ? 8 - mis : 0, tail = ((N4 + mis) & ~7) - mis;   // [0, head), [tail, N4): shared lines
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(out, 0, N4 * 16, 0x00020000);
   const int i0 = lane - mis;
+  typedef Div24<Q, N4 + 64> DivQ;  // unit -> channel (every unit read is in [0, N4))
   // the window's channel class and edge bit (wave-uniform, ObsWinTab)
   auto wclass = [&](int k) { return (ObsWinTab<LT>::tab.w[mis][k >> 3] >> (4 * (k & 7))) & 7u; };
   // only a window at either end of the board holds lanes outside it (i < 0, i >= N4):
@@ -1136,7 +1143,7 @@ __device__ __forceinline__ void write_obs_lines(const Smem<NC>& S, int lane, flo
         const uint32_t wc = wclass(k);
         if (PASS != 0 && (((wc & 3u) == 0) != (PASS == 1))) continue;  // wave-uniform
         const int i = unit(i0 + 64 * k, wc);
-        const int ch = i / Q, q = i - ch * Q;
+        const int ch = DivQ::div(i), q = i - ch * Q;
         A[j] = *reinterpret_cast<const uint4*>(sb + o_cell + 16 * q);
         if ((wc & 3u) == 1) {  // broadcast channels only: the channel's value
           W[j] = *reinterpret_cast<const uint32_t*>(sb + o_chv + 4 * ch);
@@ -1160,7 +1167,7 @@ __device__ __forceinline__ void write_obs_lines(const Smem<NC>& S, int lane, flo
       if (PASS != 0 && (((wc & 3u) == 0) != (PASS == 1))) continue;
       const bool edge = (wc & 4u) != 0;  // the window holds a line shared with a neighbour
       const int i = i0 + 64 * k;
-      const int ch = unit(i, wc) / Q;
+      const int ch = DivQ::div(unit(i, wc));
       const int e = ch - 25;
       const bool isen = (unsigned)e < 16u, isd9 = ch == 9, isbin = ((kChBin >> ch) & 1ull) != 0;
       const uint32_t a4[4] = {A[j].x, A[j].y, A[j].z, A[j].w};
@@ -1491,7 +1498,8 @@ __device__ __forceinline__ void build_near_road(Smem<NC>& S, U& u, const Ctx& x,
     int k = (int)R.ri(0, 24);
     int dr = k / 5 - 2, dc = k % 5 - 2;
     int cc = cells[i];
-    int r = cc / x.L + dr, c = cc % x.L + dc;
+    const int rc = div_side(cc, x.Lm);
+    int r = rc + dr, c = cc - rc * x.L + dc;
     if (r < 0 || r >= x.L || c < 0 || c >= x.L) continue;
     int fc = tower_build(S, u, x, t, r * x.L + c);
     if (fc == FC_OK) { u.def_cd = x.C.def_interval; return; }

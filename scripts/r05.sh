@@ -208,5 +208,22 @@ s16)  # probes of the small kernel's shape: 4 waves per SIMD over 2 rounds (y1),
     done
   done
   ;;
+s17)  # 24-bit multiplies for the divisions by L and by L^2/4 (v_mul_hi_u32 / v_mul_lo_u32 are quarter rate): the GPU suite, then A/B vs libtdstep_base.so
+  gpusuite 900; rc=$?; [ $rc -le 1 ] || exit $rc
+  for r in 1 2; do
+    for bb in 4096 8192 16384 65536; do
+      st=2000; [ $bb -ge 65536 ] && st=300
+      for v in base new; do
+        lib=$PWD/gym-td_amd/lib/libtdstep_$v.so; [ $v = new ] && lib=$PWD/gym-td_amd/lib/libtdstep.so
+        TDSTEP_LIB=$lib run ${v}_${bb}_$r 300 python bench.py --global-batch $bb --steps $st --no-cpu-baseline --timing none || exit 1; line ${v}_${bb}_$r
+      done
+    done
+    for v in base new; do
+      lib=$PWD/gym-td_amd/lib/libtdstep_$v.so; [ $v = new ] && lib=$PWD/gym-td_amd/lib/libtdstep.so
+      TDSTEP_LIB=$lib run ${v}_p2_$r 300 python bench.py --workload 2p-middle-multi --steps 200 --no-cpu-baseline --timing none || exit 1; line ${v}_p2_$r
+      TDSTEP_LIB=$lib run ${v}_l30_$r 300 python bench.py --workload def-large --global-batch 16384 --steps 200 --no-cpu-baseline --timing none || exit 1; line ${v}_l30_$r
+    done
+  done
+  ;;
 *) echo "unknown session $S"; exit 2;;
 esac
