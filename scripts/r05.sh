@@ -250,5 +250,16 @@ s18)  # final-build validation and profiles: GPU suite, smoke, the driver's comm
     rm -rf $O/pmc/${wl}_$bb/FETCH_SIZE $O/pmc/${wl}_$bb/WRITE_SIZE
   done
   ;;
+s19)  # one-wave kernels: binary-plane windows early (z1); observation windows per batch 2 (z2) / 8 (z3) instead of 4
+  for r in 1 2; do
+    for spec in 8192:2000 65536:300 32768:600; do
+      bb=${spec%%:*}; st=${spec##*:}
+      for v in base z1 z2 z3; do
+        lib=$PWD/gym-td_amd/lib/libtdstep_$v.so; [ $v = base ] && lib=$PWD/gym-td_amd/lib/libtdstep.so
+        TDSTEP_LIB=$lib run ${v}_${bb}_$r 300 python bench.py --global-batch $bb --steps $st --no-cpu-baseline --timing none || exit 1; line ${v}_${bb}_$r
+      done
+    done
+  done
+  ;;
 *) echo "unknown session $S"; exit 2;;
 esac
