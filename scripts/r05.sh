@@ -261,5 +261,9 @@ s19)  # one-wave kernels: binary-plane windows early (z1); observation windows p
     done
   done
   ;;
+s20)  # every board of the BASELINE-sized batches against the C restatement (new parity test)
+  run pytest_every 1000 python -u -m pytest tests/test_gpu_parity.py -m gpu -v -k every_board --timeout 900 --timeout-method thread -p no:cacheprovider --durations=0
+  rc=$?; grep -E "PASSED|FAILED|^E  |passed|failed|s call" $O/pytest_every.log | head -40; exit $rc
+  ;;
 *) echo "unknown session $S"; exit 2;;
 esac

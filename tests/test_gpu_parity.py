@@ -295,6 +295,62 @@ def test_full_size_properties(L, B, mode, multi, steps, kernel):
             o.close()
 
 
+# Every board of the BASELINE-sized batches against the C restatement for the first
+# steps (test_full_size_properties follows 12 boards per batch for 1,300 steps): the
+# metric's 65,536 x 10x10 on the large kernel, the N = 8 share (8,192, small kernel),
+# configs[1] (4,096, two-wave kernel), configs[2] (16,384 x TD-2p 20x20 multi-action) and
+# configs[4] per GPU (16,384 x 30x30).
+@pytest.mark.parametrize("L,B,mode,multi,steps", [
+    (10, 65536, "def", False, 8), (10, 8192, "def", False, 24), (10, 4096, "def", False, 24),
+    (20, 16384, "2p", True, 3), (30, 16384, "def", False, 3)])
+def test_every_board_of_full_size_batches(L, B, mode, multi, steps):
+    """Reward bits, done and every observation byte of every board at every step (the
+    boards whose first layout draw fails, where the reference raises, are flagged and
+    stay unstepped on the device; the oracle skips them)."""
+    from oracle import td_cpu as C
+    from test_gpu_deep import _reset_skipping, ROAD_ATTEMPTS
+    seeds = np.arange(B, dtype=np.int64) + 31000
+    eng = TDEngine(L, B, mode, multi, 1, np_seeds=seeds, py_seeds=seeds, autoreset=True, info=not multi)
+    orc = {}
+    try:
+        obs, failed = eng.reset()
+        bad = set(int(b) for b in failed)
+        for b in range(B):
+            if b in bad:
+                continue
+            try:
+                orc[b] = C.Env(L, mode, 1, int(seeds[b]), int(seeds[b]), multi=multi, road_attempts=ROAD_ATTEMPTS)
+            except C.RoadGenError:  # the device flagged the same boards
+                raise AssertionError("board %d: the oracle's draw failed, the device's did not" % b)
+        assert len(orc) + len(bad) == B and len(bad) < B // 10
+        ob = obs.cpu().numpy()
+        for b, o in orc.items():
+            assert np.array_equal(ob[b], o.obs()), b
+        g = torch.Generator(device="cuda").manual_seed(11)
+        for k in range(steps):
+            if multi:
+                d = torch.randint(0, 3, (B, 6, L, L), device="cuda", generator=g, dtype=torch.int64)
+            else:
+                d = torch.randint(0, 6 * L * L + 1, (B,), device="cuda", generator=g, dtype=torch.int64)
+            a = torch.randint(0, 5, (B, 3, 8), device="cuda", generator=g, dtype=torch.int64) if mode == "2p" else None
+            eng.step(def_act=d, atk_act=a)
+            dh, ah = d.cpu().numpy(), (a.cpu().numpy() if a is not None else None)
+            ob, rw, dn = eng.obs.cpu().numpy(), eng.reward.cpu().numpy(), eng.done.cpu().numpy()
+            for b, o in orc.items():
+                wo, wr, wd = o.step(dh[b] if multi else int(dh[b]), ah[b] if ah is not None else None)
+                assert canon.fhex(rw[b]) == canon.fhex(wr), (k, b)
+                assert bool(dn[b]) == wd, (k, b)
+                if wd:
+                    wo = _reset_skipping(o)
+                assert np.array_equal(ob[b], wo), (k, b, np.argwhere(ob[b] != wo)[:5].tolist())
+            del ob
+        assert (eng.flags()[sorted(orc)] == 0).all()
+    finally:
+        eng.close()
+        for o in orc.values():
+            o.close()
+
+
 def test_reference_kat_on_device():
     """The reference's own known-answer test (TDBoard.py:674-751) through the C-ABI:
     the seed-1024 two-road 10x10 layout (roads drawn by the restatement of
