@@ -265,5 +265,12 @@ s20)  # every board of the BASELINE-sized batches against the C restatement (new
   run pytest_every 1000 python -u -m pytest tests/test_gpu_parity.py -m gpu -v -k every_board --timeout 900 --timeout-method thread -p no:cacheprovider --durations=0
   rc=$?; grep -E "PASSED|FAILED|^E  |passed|failed|s call" $O/pytest_every.log | head -40; exit $rc
   ;;
+s21)  # s19 then s20 in one call
+  bash scripts/r05.sh s19 || exit 1
+  bash scripts/r05.sh s20
+  ;;
+s22)  # the observation stream alone (scripts/obs_ceiling.hip): the practical write ceiling of the step's store shape
+  run obs_ceiling 200 ./scripts/bin/obs_ceiling || exit 1; cat $O/obs_ceiling.log
+  ;;
 *) echo "unknown session $S"; exit 2;;
 esac
