@@ -272,5 +272,9 @@ s21)  # s19 then s20 in one call
 s22)  # the observation stream alone (scripts/obs_ceiling.hip): the practical write ceiling of the step's store shape
   run obs_ceiling 200 ./scripts/bin/obs_ceiling || exit 1; cat $O/obs_ceiling.log
   ;;
+s23)  # the N > 1 control flow of this round's bench.py (kernel sampled in the timed region, MAX over ranks) with ranks sharing one GPU over gloo
+  TD_BENCH_DIST_BACKEND=gloo TD_BENCH_SAME_DEVICE=1 run n2 300 python bench.py --gpus 2 --steps 20 --warmup 5 || exit 1; line n2; grep -h '^{' $O/n2.log | cut -c1-1500
+  TD_BENCH_DIST_BACKEND=gloo TD_BENCH_SAME_DEVICE=1 run n8 400 python bench.py --gpus 8 --steps 20 --warmup 5 || exit 1; line n8; grep -h '^{' $O/n8.log | cut -c1-1500
+  ;;
 *) echo "unknown session $S"; exit 2;;
 esac
