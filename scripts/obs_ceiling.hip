@@ -71,7 +71,25 @@ static double timed(F launch, double bytes) {
   return bytes / (ms / n * 1e-3) / 1e12;
 }
 
-int main() {
+int main(int argc, char** argv) {
+  // argv[1] = 20 or 30: 16,384 boards of a 20x20 (72,000 B) or 30x30 (162,000 B) observation
+  if (argc > 1) {
+    const int L = std::atoi(argv[1]), nb = 16384, rowb = 45 * L * L * 4;
+    const size_t bytesz = (size_t)nb * rowb + 4096;
+    for (int contig = 0; contig < 2; ++contig) {
+      char* buf = nullptr;
+      if (contig) CK(hipExtMallocWithFlags((void**)&buf, bytesz, hipDeviceMallocContiguous));
+      else CK(hipMalloc(&buf, bytesz));
+      CK(hipMemset(buf, 0, bytesz));
+      const double bytes = (double)nb * rowb;
+      const double px = timed([&] { hipLaunchKernelGGL((obs<2, 0, true>), dim3(nb), dim3(64), 0, 0, buf, nb, rowb); }, bytes);
+      const double ax = timed([&] { hipLaunchKernelGGL((obs<0, 0, true>), dim3(nb), dim3(64), 0, 0, buf, nb, rowb); }, bytes);
+      std::printf("%s %dx%d %5d boards (%7.1f MB) | nt + plain shared (xcd map) %.2f | all plain %.2f TB/s | %.1f us at nt+plain\n",
+                  contig ? "contiguous" : "hipMalloc ", L, L, nb, bytes / 1e6, px, ax, bytes / (px * 1e12) * 1e6);
+      CK(hipFree(buf));
+    }
+    return 0;
+  }
   const int rowb = 18000;
   const size_t maxb = (size_t)65536 * rowb + 4096;
   for (int contig = 0; contig < 2; ++contig) {

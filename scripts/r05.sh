@@ -276,5 +276,9 @@ s23)  # the N > 1 control flow of this round's bench.py (kernel sampled in the t
   TD_BENCH_DIST_BACKEND=gloo TD_BENCH_SAME_DEVICE=1 run n2 300 python bench.py --gpus 2 --steps 20 --warmup 5 || exit 1; line n2; grep -h '^{' $O/n2.log | cut -c1-1500
   TD_BENCH_DIST_BACKEND=gloo TD_BENCH_SAME_DEVICE=1 run n8 400 python bench.py --gpus 8 --steps 20 --warmup 5 || exit 1; line n8; grep -h '^{' $O/n8.log | cut -c1-1500
   ;;
+s24)  # the observation stream alone at 20x20 and 30x30 (16,384 boards)
+  run obs_ceiling_20 200 ./scripts/bin/obs_ceiling 20 || exit 1; cat $O/obs_ceiling_20.log
+  run obs_ceiling_30 200 ./scripts/bin/obs_ceiling 30 || exit 1; cat $O/obs_ceiling_30.log
+  ;;
 *) echo "unknown session $S"; exit 2;;
 esac
