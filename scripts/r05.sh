@@ -280,5 +280,11 @@ s24)  # the observation stream alone at 20x20 and 30x30 (16,384 boards)
   run obs_ceiling_20 200 ./scripts/bin/obs_ceiling 20 || exit 1; cat $O/obs_ceiling_20.log
   run obs_ceiling_30 200 ./scripts/bin/obs_ceiling 30 || exit 1; cat $O/obs_ceiling_30.log
   ;;
+s25)  # phase stamps at 8,192 boards: the product vs the build without the observation writer (x1)
+  for v in stamps x1stamps; do
+    TD_PROBE_KERNEL=small TDSTEP_LIB=$PWD/gym-td_amd/lib/libtdstep_$v.so run phases_${v}_8192 300 python scripts/probe_phases.py 8192 10 600 || exit 1
+    cat $O/phases_${v}_8192.log | grep -v amdgpu
+  done
+  ;;
 *) echo "unknown session $S"; exit 2;;
 esac
