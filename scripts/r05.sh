@@ -286,5 +286,18 @@ s25)  # phase stamps at 8,192 boards: the product vs the build without the obser
     cat $O/phases_${v}_8192.log | grep -v amdgpu
   done
   ;;
+s26)  # captured(): the HBM config load kept apart from the LDS one (no FLAT load, no vmcnt(0) behind the wave's stores) -- w1
+  for r in 1 2; do
+    for spec in 8192:2000 4096:2000 16384:1000 65536:300; do
+      bb=${spec%%:*}; st=${spec##*:}
+      for v in base w1; do
+        lib=$PWD/gym-td_amd/lib/libtdstep_$v.so; [ $v = base ] && lib=$PWD/gym-td_amd/lib/libtdstep.so
+        TDSTEP_LIB=$lib run ${v}_${bb}_$r 300 python bench.py --global-batch $bb --steps $st --no-cpu-baseline --timing none || exit 1; line ${v}_${bb}_$r
+      done
+    done
+  done
+  TD_PROBE_KERNEL=small TDSTEP_LIB=$PWD/gym-td_amd/lib/libtdstep_w1stamps.so run phases_w1_8192 300 python scripts/probe_phases.py 8192 10 600 || exit 1
+  grep -v amdgpu $O/phases_w1_8192.log
+  ;;
 *) echo "unknown session $S"; exit 2;;
 esac
