@@ -312,5 +312,16 @@ s27)  # w2 = w1 + vmcnt(0) before the state stores (no wait on the wave's own st
   TD_PROBE_KERNEL=small TDSTEP_LIB=$PWD/gym-td_amd/lib/libtdstep_w2stamps.so run phases_w2_8192 300 python scripts/probe_phases.py 8192 10 600 || exit 1
   grep -v amdgpu $O/phases_w2_8192.log
   ;;
+s28)  # issue sensitivity: +8 dependent SALU (ps) / VALU (pv) per observation window
+  for r in 1 2; do
+    for spec in 8192:2000 65536:300; do
+      bb=${spec%%:*}; st=${spec##*:}
+      for v in base ps pv; do
+        lib=$PWD/gym-td_amd/lib/libtdstep_$v.so; [ $v = base ] && lib=$PWD/gym-td_amd/lib/libtdstep.so
+        TDSTEP_LIB=$lib run ${v}_${bb}_$r 300 python bench.py --global-batch $bb --steps $st --no-cpu-baseline --timing none || exit 1; line ${v}_${bb}_$r
+      done
+    done
+  done
+  ;;
 *) echo "unknown session $S"; exit 2;;
 esac
