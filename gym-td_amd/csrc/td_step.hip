@@ -113,17 +113,21 @@ struct Ctx {
 // A value an enemy or tower captured when it was created or upgraded (TDElements.py:
 // 4-43, 45-63, 134-170): from the block of its epoch -- the staged current one, or
 // (after a paramConfig) an older block in HBM.
-// (The compiler merges the two loads into one FLAT load of a selected pointer, which
-// counts in vmcnt; keeping them apart -- an empty asm on the HBM value -- measured
-// +-0.6 % across 65,536 / 8,192 / 4,096 boards, profiles/r03/s17: not kept.)
-// (The older block's address with a 24-bit multiply: ep * sizeof(TdDevCfg) < 2^24; as
-// x.tab[ep] it took a 64-bit v_mad_u64_u32, a quarter-rate instruction, at every call.)
+// The two loads are kept apart by an empty asm on the HBM value, waited for inside its
+// branch: otherwise the compiler merges them into one FLAT load of a selected pointer,
+// which waits with vmcnt(0) and lgkmcnt(0) at every call (16 FLAT loads in the small
+// kernel).  Apart: -0.4 to -0.5 % at 32,768-65,536 boards, +-0.5 % below (r05/s26, s27;
+// +-0.6 % in round 3, r03/s17).  The older block's address takes a 24-bit multiply
+// (ep * sizeof(TdDevCfg) < 2^24); as x.tab[ep] it took a quarter-rate v_mad_u64_u32.
 template <class F>
 __device__ __forceinline__ double captured(const Ctx& x, int ep, F f) {
   double v = f(x.C);
-  if (ep != x.ep)
-    v = f(*reinterpret_cast<const TdDevCfg*>(reinterpret_cast<const char*>(x.tab) +
-                                             __umul24((uint32_t)ep, (uint32_t)sizeof(TdDevCfg))));
+  if (ep != x.ep) {
+    double w = f(*reinterpret_cast<const TdDevCfg*>(reinterpret_cast<const char*>(x.tab) +
+                                                    __umul24((uint32_t)ep, (uint32_t)sizeof(TdDevCfg))));
+    __asm__ volatile("" : "+v"(w));
+    v = w;
+  }
   return v;
 }
 
