@@ -323,5 +323,18 @@ s28)  # issue sensitivity: +8 dependent SALU (ps) / VALU (pv) per observation wi
     done
   done
   ;;
+s29)  # the class-by-class observation writer (write_obs_lean, one-wave kernels at 10x10): parity first, then A/B vs libtdstep_base.so
+  run pytest_lean 900 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_store_policy.py tests/test_gpu_envs.py -m gpu -q -x --timeout 600 --timeout-method thread -p no:cacheprovider
+  rc=$?; grep -E "^(FAILED|E  )" $O/pytest_lean.log | head -20; tail -1 $O/pytest_lean.log; [ $rc -eq 0 ] || exit $rc
+  for r in 1 2; do
+    for spec in 8192:2000 65536:300 32768:600; do
+      bb=${spec%%:*}; st=${spec##*:}
+      for v in base new; do
+        lib=$PWD/gym-td_amd/lib/libtdstep_$v.so; [ $v = new ] && lib=$PWD/gym-td_amd/lib/libtdstep.so
+        TDSTEP_LIB=$lib run ${v}_${bb}_$r 300 python bench.py --global-batch $bb --steps $st --no-cpu-baseline --timing none || exit 1; line ${v}_${bb}_$r
+      done
+    done
+  done
+  ;;
 *) echo "unknown session $S"; exit 2;;
 esac
