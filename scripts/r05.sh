@@ -361,5 +361,18 @@ s30)  # final-build validation and profiles (after the captured() change): GPU s
     rm -rf $O/pmc/${wl}_$bb/FETCH_SIZE $O/pmc/${wl}_$bb/WRITE_SIZE
   done
   ;;
+s31)  # l2: class-by-class observation writer, 4 windows at a time (LDS reads first): parity on it, then A/B vs the product
+  TDSTEP_LIB=$PWD/gym-td_amd/lib/libtdstep_l2.so run pytest_l2 900 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_store_policy.py -m gpu -q -x --timeout 600 --timeout-method thread -p no:cacheprovider
+  rc=$?; grep -E "^(FAILED|E  )" $O/pytest_l2.log | head -20; tail -1 $O/pytest_l2.log; [ $rc -eq 0 ] || exit $rc
+  for r in 1 2; do
+    for spec in 8192:2000 65536:300 32768:600; do
+      bb=${spec%%:*}; st=${spec##*:}
+      for v in base l2; do
+        lib=$PWD/gym-td_amd/lib/libtdstep_$v.so; [ $v = base ] && lib=$PWD/gym-td_amd/lib/libtdstep.so
+        TDSTEP_LIB=$lib run ${v}_${bb}_$r 300 python bench.py --global-batch $bb --steps $st --no-cpu-baseline --timing none || exit 1; line ${v}_${bb}_$r
+      done
+    done
+  done
+  ;;
 *) echo "unknown session $S"; exit 2;;
 esac
