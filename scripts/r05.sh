@@ -374,5 +374,13 @@ s31)  # l2: class-by-class observation writer, 4 windows at a time (LDS reads fi
     done
   done
   ;;
+s32)  # the multi-action flag fold: 12 loads in flight at 6 waves per SIMD (f1), 4 at 8 (f2), vs the product (8 at 8)
+  for r in 1 2; do
+    for v in base f1 f2; do
+      lib=$PWD/gym-td_amd/lib/libtdstep_$v.so; [ $v = base ] && lib=$PWD/gym-td_amd/lib/libtdstep.so
+      TDSTEP_LIB=$lib run ${v}_p2_$r 300 python bench.py --workload 2p-middle-multi --steps 200 --no-cpu-baseline --timing none || exit 1; line ${v}_p2_$r
+    done
+  done
+  ;;
 *) echo "unknown session $S"; exit 2;;
 esac
