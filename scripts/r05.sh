@@ -382,5 +382,14 @@ s32)  # the multi-action flag fold: 12 loads in flight at 6 waves per SIMD (f1),
     done
   done
   ;;
+s33)  # kernel choice at the N = 2 / 4 shares: every step kernel at 16,384 and 32,768 boards (and 8,192)
+  for r in 1 2; do
+    for bb in 16384 32768 8192; do
+      for k in auto large small small2; do
+        run ${k}_${bb}_$r 300 python bench.py --global-batch $bb --steps 600 --no-cpu-baseline --timing none --step-kernel $k || exit 1; line ${k}_${bb}_$r
+      done
+    done
+  done
+  ;;
 *) echo "unknown session $S"; exit 2;;
 esac
