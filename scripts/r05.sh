@@ -391,5 +391,15 @@ s33)  # kernel choice at the N = 2 / 4 shares: every step kernel at 16,384 and 3
     done
   done
   ;;
+s34)  # the two-wave kernel over more rounds: 65,536 / 49,152 / 32,768 / 8,192 boards, large or small vs small2
+  for r in 1 2 3; do
+    for spec in 65536:large:300 49152:large:400 32768:large:600 8192:small:2000; do
+      bb=${spec%%:*}; rest=${spec#*:}; k=${rest%%:*}; st=${rest##*:}
+      for kk in $k small2; do
+        run ${kk}_${bb}_$r 300 python bench.py --global-batch $bb --steps $st --no-cpu-baseline --timing none --step-kernel $kk || exit 1; line ${kk}_${bb}_$r
+      done
+    done
+  done
+  ;;
 *) echo "unknown session $S"; exit 2;;
 esac
