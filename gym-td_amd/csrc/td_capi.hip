@@ -487,9 +487,16 @@ td_handle* td_create(const td_config* cfg, int map_size, int n_boards, int mode,
     const int resident = step_resident_boards(base_args(h), cus, 1);
     const int resident2 = step_resident_boards(base_args(h), cus, 2);
     // two-wave kernel up to this many rounds (TD-2p 20x20 multi-action at 16,384 boards:
-    // 303.3-303.6 vs 314-315 us per step with the large kernel, profiles/r04/s10)
-    const int rounds2 = h->multi ? (h->L == 20 && h->mode == TD_MODE_2P ? 8 : 0) : h->L == 10 ? 3 : h->L == 30 ? 10 : 0;
-    h->small_auto = n_boards <= resident2 ? 2 : n_boards <= resident ? 1 : n_boards <= rounds2 * resident ? 2 : 0;
+    // 303.3-303.6 vs 314-315 us per step with the large kernel, profiles/r04/s10; TD-def
+    // 10x10 at every batch above one round since round 5: 32,768 / 49,152 / 65,536 boards
+    // 107.5-107.9 / 156.5-156.8 / 203.4-204.1 vs 111.7-111.9 / 160.6-160.9 / 208.2-208.4 us,
+    // profiles/r05/s33, s34)
+    const int rounds2 = h->multi ? (h->L == 20 && h->mode == TD_MODE_2P ? 8 : 0)
+                                 : h->L == 10 ? (h->mode == TD_MODE_DEF ? (1 << 20) : 3) : h->L == 30 ? 10 : 0;
+    h->small_auto = n_boards <= resident2                            ? 2
+                    : n_boards <= resident                           ? 1
+                    : (int64_t)n_boards <= (int64_t)rounds2 * resident ? 2
+                                                                     : 0;
     if (apply_kernel(h, h->small_auto)) { std::string e = g_err; td_destroy(h); g_err = e; return nullptr; }
   }
   std::vector<uint32_t> seeds(B);

@@ -22,9 +22,9 @@ from gym_TD.engine import TDEngine  # noqa: E402
 
 from test_oracle_golden import _info_view  # noqa: E402
 
-# The three step kernels (td_set_step_kernel): the large-batch kernel of the metric's
-# 65,536 boards, the one-round kernel of the N = 8 share (8,192 boards), the two-wave
-# kernel of configs[1] (4,096 boards).  Every parity test below runs each of them.
+# The three step kernels (td_set_step_kernel): the large-batch kernel (20x20 / 30x30
+# batches beyond a few rounds of waves), the one-round kernel of the N = 8 share (8,192
+# boards), the two-wave kernel of the metric's 65,536 boards and configs[1] (4,096).  Every parity test below runs each of them.
 KERNELS = ("large", "small", "small2")
 
 
@@ -236,9 +236,9 @@ def test_full_size_properties(L, B, mode, multi, steps, kernel):
         if kernel == "auto" and torch.cuda.get_device_properties(0).multi_processor_count == 256:
             # td_create's rule on a 256-CU MI355X: two waves per board up to half a round of
             # waves, one round (8 per SIMD) -> small kernel, then two waves per board again
-            # over a few rounds (10x10: 3, 30x30: 10, TD-2p 20x20 multi-action: 8; other
-            # multi-action boards: large)
-            want = {(10, 4096): "small2", (10, 8192): "small", (10, 16384): "small2", (10, 65536): "large",
+            # over more rounds (TD-def 10x10: every batch, other 10x10 modes: 3, 30x30: 10,
+            # TD-2p 20x20 multi-action: 8; other multi-action boards: large)
+            want = {(10, 4096): "small2", (10, 8192): "small", (10, 16384): "small2", (10, 65536): "small2",
                     (20, 16384): "small2" if mode == "2p" and multi else "large",
                     (30, 16384): "small2"}[(L, B)]
             assert eng.step_kernel == want, eng.step_kernel_name
@@ -297,7 +297,7 @@ def test_full_size_properties(L, B, mode, multi, steps, kernel):
 
 # Every board of the BASELINE-sized batches against the C restatement for the first
 # steps (test_full_size_properties follows 12 boards per batch for 1,300 steps): the
-# metric's 65,536 x 10x10 on the large kernel, the N = 8 share (8,192, small kernel),
+# metric's 65,536 x 10x10 on the two-wave kernel, the N = 8 share (8,192, small kernel),
 # configs[1] (4,096, two-wave kernel), configs[2] (16,384 x TD-2p 20x20 multi-action) and
 # configs[4] per GPU (16,384 x 30x30).
 @pytest.mark.parametrize("L,B,mode,multi,steps", [
