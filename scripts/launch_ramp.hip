@@ -1,7 +1,8 @@
 // launch_ramp.hip -- diagnostic: how fast one-round grids of 64-thread workgroups get
 // their waves started on this part, and what slows the ramp: static LDS per workgroup,
 // the VGPR allocation, and work the already-started waves do (VALU, memory, sleep).
-// Each wave stores s_memrealtime (100 MHz, chip-wide) at its start and end.
+// Each wave stores s_memrealtime (100 MHz, chip-wide) at its start and end.  `wg <n>`
+// lines: the same waves packed n per workgroup (k_ramp_wg).
 //   hipcc --offload-arch=gfx950 -O3 scripts/launch_ramp.hip -o scripts/bin/launch_ramp
 #include <hip/hip_runtime.h>
 
@@ -70,6 +71,59 @@ __global__ __launch_bounds__(64) void k_ramp(uint64_t* t, float* buf, int iters)
   if (acc == -1.0f) buf[0] = acc;  // keeps the work
 }
 
+// NW independent waves per workgroup (wave w of block i is wave i * NW + w of the grid)
+template <int NW, int WORK>
+__global__ __launch_bounds__(64 * NW) void k_ramp_wg(uint64_t* t, float* buf, int iters) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  const int lane = threadIdx.x & 63, w = blockIdx.x * NW + (threadIdx.x >> 6);
+  float acc = (float)lane;
+  if constexpr (WORK == 1) {
+    for (int i = 0; i < iters; ++i) acc = acc * 1.0001f + 0.5f;
+  } else if constexpr (WORK == 5) {
+    __shared__ float q[64 * NW];
+    float* qw = q + 64 * (threadIdx.x >> 6);
+    qw[lane] = acc;
+    for (int i = 0; i < iters; ++i) {
+      acc = qw[(lane + (int)acc) & 63] + 1.0f;
+      qw[lane] = acc;
+    }
+  }
+  const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+  if (lane == 0) {
+    t[2 * w] = t0;
+    t[2 * w + 1] = t1;
+  }
+  if (acc == -1.0f) buf[0] = acc;
+}
+
+static int report(const char* name, int waves, uint64_t* dt) {
+  std::vector<uint64_t> h(2 * (size_t)waves);
+  CK(hipMemcpy(h.data(), dt, h.size() * 8, hipMemcpyDeviceToHost));
+  uint64_t s0 = ~0ull, s1 = 0, e1 = 0;
+  std::vector<double> life;
+  for (int i = 0; i < waves; ++i) {
+    s0 = std::min(s0, h[2 * i]);
+    s1 = std::max(s1, h[2 * i]);
+    e1 = std::max(e1, h[2 * i + 1]);
+    life.push_back((h[2 * i + 1] - h[2 * i]) / 100.0);
+  }
+  std::sort(life.begin(), life.end());
+  std::printf("%-22s waves %5d  start ramp %6.2f us  first start -> last end %6.2f us  wave life p50 %6.2f us\n", name, waves,
+              (s1 - s0) / 100.0, (e1 - s0) / 100.0, life[life.size() / 2]);
+  return 0;
+}
+
+template <int NW, int WORK>
+int run_wg(const char* what, int waves, int iters, uint64_t* dt, float* buf) {
+  for (int rep = 0; rep < 3; ++rep) {
+    hipLaunchKernelGGL((k_ramp_wg<NW, WORK>), dim3(waves / NW), dim3(64 * NW), 0, 0, dt, buf, iters);
+    CK(hipDeviceSynchronize());
+  }
+  char name[64];
+  std::snprintf(name, sizeof name, "wg %d %s", NW, what);
+  return report(name, waves, dt);
+}
+
 template <int LDS, int WORK, int PRIO = 0>
 int run(const char* name, int grid, int iters, uint64_t* dt, float* buf) {
   for (int rep = 0; rep < 3; ++rep) {
@@ -92,12 +146,29 @@ int run(const char* name, int grid, int iters, uint64_t* dt, float* buf) {
   return 0;
 }
 
-int main() {
+int main(int argc, char**) {
   uint64_t* dt = nullptr;
   float* buf = nullptr;
   CK(hipMalloc(&dt, 2 * 65536 * 8));
   CK(hipMalloc(&buf, (size_t)8192 * (4096 + 4608) * 4));
   CK(hipMemset(buf, 0, (size_t)8192 * (4096 + 4608) * 4));
+  if (argc > 1) {  // launch_ramp wg: one-round grids of 1-, 2-, 4- and 8-wave workgroups
+    for (int waves : {8192, 4096}) {
+      if (run_wg<1, 0>("empty", waves, 0, dt, buf) || run_wg<2, 0>("empty", waves, 0, dt, buf) ||
+          run_wg<4, 0>("empty", waves, 0, dt, buf) || run_wg<8, 0>("empty", waves, 0, dt, buf))
+        return 1;
+      for (int iters : {500, 5000, 20000}) {
+        char what[32];
+        std::snprintf(what, sizeof what, "valu %d", iters);
+        if (run_wg<1, 1>(what, waves, iters, dt, buf) || run_wg<2, 1>(what, waves, iters, dt, buf) ||
+            run_wg<4, 1>(what, waves, iters, dt, buf) || run_wg<8, 1>(what, waves, iters, dt, buf))
+          return 1;
+      }
+      if (run_wg<1, 5>("lds-chain 200", waves, 200, dt, buf) || run_wg<4, 5>("lds-chain 200", waves, 200, dt, buf))
+        return 1;
+    }
+    return 0;
+  }
   for (int grid : {8192}) {
     if (run<0, 1>("valu-short", grid, 500, dt, buf)) return 1;
     if (run<0, 6>("valu-short+sleep/32", grid, 500, dt, buf)) return 1;

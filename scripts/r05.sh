@@ -427,5 +427,22 @@ s35)  # final-build validation and profiles (TD-def 10x10 on the two-wave kernel
     rm -rf $O/pmc/${wl}_$bb/FETCH_SIZE $O/pmc/${wl}_$bb/WRITE_SIZE
   done
   ;;
+s36)  # live-slot loads in the two-wave kernel (live) vs the speculative 16 + 16 slots: parity, A/B, PMC; launch ramp of multi-wave workgroups
+  TDSTEP_LIB=$PWD/gym-td_amd/lib/libtdstep_live.so run pytest_live 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -q -x -k small2 --timeout 300 --timeout-method thread -p no:cacheprovider
+  rc=$?; grep -E "^(FAILED|E  )" $O/pytest_live.log | head -20; tail -1 $O/pytest_live.log; [ $rc -eq 0 ] || exit $rc
+  run ramp 120 scripts/bin/launch_ramp wg || exit 1; cat $O/ramp.log
+  for r in 1 2; do
+    for spec in 65536:300 32768:600 16384:1000 4096:2000; do
+      bb=${spec%%:*}; st=${spec##*:}
+      for v in base live; do
+        lib=$PWD/gym-td_amd/lib/libtdstep_$v.so; [ $v = base ] && lib=$PWD/gym-td_amd/lib/libtdstep.so
+        TDSTEP_LIB=$lib run ${v}_${bb}_$r 300 python bench.py --global-batch $bb --steps $st --no-cpu-baseline --timing none || exit 1; line ${v}_${bb}_$r
+      done
+    done
+  done
+  TDSTEP_LIB=$PWD/gym-td_amd/lib/libtdstep_live.so OUT=$O/pmc NAME=live_65536 B=65536 timeout -k 10 700 bash scripts/pmc_ab.sh || exit 1
+  TDSTEP_LIB=$PWD/gym-td_amd/lib/libtdstep_live.so OUT=$O/pmc NAME=live_4096 B=4096 timeout -k 10 700 bash scripts/pmc_ab.sh || exit 1
+  rm -rf $O/pmc/*/FETCH_SIZE $O/pmc/*/WRITE_SIZE
+  ;;
 *) echo "unknown session $S"; exit 2;;
 esac
