@@ -201,9 +201,10 @@ int td_step(td_handle* h, const td_step_io* io, void* stream);
  *   TD_KERNEL_SMALL2 td_step_kernel_small2 as SMALL, plus a second wave per board that
  *                                          writes half of the observation;
  *   TD_KERNEL_AUTO   td_create's rule: SMALL2 up to half a round of boards, SMALL up to one
- *                    round, SMALL2 again up to 3 rounds at L = 10 and 10 rounds at L = 30
- *                    (single-action boards), else LARGE (L = 10 / 20 / 30; other L only
- *                    have LARGE).
+ *                    round, SMALL2 again above that -- at any batch for single-action TD-def
+ *                    at L = 10, up to 3 rounds for the other L = 10 modes, 10 rounds at
+ *                    L = 30 (single-action) and 8 rounds for TD-2p multi-action at L = 20 --
+ *                    else LARGE (L = 10 / 20 / 30; other L only have LARGE).
  * The small kernels need a 16-B-aligned observation buffer; a td_step with any other
  * buffer runs LARGE.  td_set_step_kernel fails (and changes nothing) for a small kernel
  * at an L without one.  td_step_kernel returns the resolved kind, td_step_kernel_name the
