@@ -52,6 +52,57 @@ __global__ __launch_bounds__(64) void obs(char* out, int nb, int rowb) {
   }
 }
 
+// Store shapes (argv[1] == "shapes"): W bytes per lane per instruction (4 / 8 / 16), AUX
+// the buffer-store aux bits of the whole lines (the two shared lines plain), BPW boards per workgroup stepped one after the
+// other (a block of BPW consecutive boards, blocks spread over the XCDs as xcd_board
+// spreads boards), NW waves per workgroup splitting each board's row by instruction.
+// SPLIT 0: the NW waves take a board's instructions in turn; 1: each a contiguous share of
+// them; 2: each wave its own board (NW boards per workgroup, BPW must be 1).
+// THR >= 0: s_waitcnt vmcnt(THR) after every store instruction (stores in flight per wave)
+template <int W, int AUX, int BPW, int NW, int SPLIT = 0, int THR = -1>
+__global__ __launch_bounds__(64 * NW) void obs_shape(char* out, int nb, int rowb) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int per = SPLIT == 2 ? NW : BPW;
+  const int blk = xcd_board((int)blockIdx.x, nb / per);
+  for (int j = 0; j < BPW; ++j) {
+    const int b = SPLIT == 2 ? blk * NW + wv : blk * BPW + j;
+    const size_t start = (size_t)b * rowb;
+    const int mis = (int)(start & 127);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(out + start, 0, rowb, 0x00020000);
+    const int K = (rowb + mis + 64 * W - 1) / (64 * W);
+    const int q = (K + NW - 1) / NW;
+    const int k0 = SPLIT == 0 ? wv : SPLIT == 1 ? wv * q : 0;
+    const int k1 = SPLIT == 1 ? (k0 + q < K ? k0 + q : K) : K;
+    const int dk = SPLIT == 0 ? NW : 1;
+    for (int k = k0; k < k1; k += dk) {
+      const int o = k * 64 * W + lane * W - mis;
+      const unsigned off = o < 0 ? 0x80000000u : (unsigned)o;
+      // the two lines the board shares with its neighbours: plain stores (as the product)
+      const int line = (o + mis) >> 7;
+      const bool shared = (mis && line == 0) || (((rowb + mis) & 127) && line == ((rowb + mis) >> 7));
+      const unsigned ow = shared ? 0x80000000u : off, os = shared ? off : 0x80000000u;
+      if constexpr (W == 16) {
+        const u32x4 v{(unsigned)b, (unsigned)o, 0u, 0u};
+        __builtin_amdgcn_raw_buffer_store_b128(v, rs, ow, 0, AUX);
+        __builtin_amdgcn_raw_buffer_store_b128(v, rs, os, 0, 0);
+      } else if constexpr (W == 8) {
+        typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+        const u32x2 v{(unsigned)b, (unsigned)o};
+        __builtin_amdgcn_raw_buffer_store_b64(v, rs, ow, 0, AUX);
+        __builtin_amdgcn_raw_buffer_store_b64(v, rs, os, 0, 0);
+      } else {
+        __builtin_amdgcn_raw_buffer_store_b32((unsigned)o, rs, ow, 0, AUX);
+        __builtin_amdgcn_raw_buffer_store_b32((unsigned)o, rs, os, 0, 0);
+      }
+      if constexpr (THR == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if constexpr (THR == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+      if constexpr (THR == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      if constexpr (THR == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      if constexpr (THR == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    }
+  }
+}
+
 template <class F>
 static double timed(F launch, double bytes) {
   hipEvent_t a, b;
@@ -72,6 +123,33 @@ static double timed(F launch, double bytes) {
 }
 
 int main(int argc, char** argv) {
+  if (argc > 1 && argv[1][0] == 's') {
+    const int nb = 65536, rowb = 18000;
+    const size_t bytesz = (size_t)nb * rowb + 4096;
+    char* buf = nullptr;
+    CK(hipExtMallocWithFlags((void**)&buf, bytesz, hipDeviceMallocContiguous));
+    CK(hipMemset(buf, 0, bytesz));
+    const double bytes = (double)nb * rowb;
+#define SHAPE(W, AUX, BPW, NW, SPLIT, LDSB, THR)                                                              \
+  std::printf("shape W=%2d aux=%2d boards/wg=%2d waves/wg=%2d split=%d lds=%5d vmcnt=%2d  %.2f TB/s\n", W, AUX, BPW, NW, SPLIT, \
+              LDSB, THR,                                                                                        \
+              timed([&] { hipLaunchKernelGGL((obs_shape<W, AUX, BPW, NW, SPLIT, THR>), dim3(nb / (SPLIT == 2 ? NW : BPW)),   \
+                                             dim3(64 * NW), LDSB, 0, buf, nb, rowb); }, bytes))
+    std::printf("reference: nt + plain shared (xcd map) %.2f TB/s\n",
+                timed([&] { hipLaunchKernelGGL((obs<2, 0, true>), dim3(nb), dim3(64), 0, 0, buf, nb, rowb); }, bytes));
+    // waves per board (split 0 / 1), waves per workgroup each with its own board (split 2),
+    // fewer resident workgroups (dynamic LDS), 8-byte lanes
+    SHAPE(16, 2, 1, 1, 0, 0, -1); SHAPE(16, 2, 1, 2, 0, 0, -1); SHAPE(16, 2, 1, 4, 0, 0, -1); SHAPE(16, 2, 1, 8, 0, 0, -1);
+    SHAPE(16, 2, 1, 16, 0, 0, -1); SHAPE(16, 2, 1, 4, 1, 0, -1); SHAPE(16, 2, 1, 8, 1, 0, -1); SHAPE(16, 2, 1, 16, 1, 0, -1);
+    SHAPE(16, 2, 1, 4, 2, 0, -1); SHAPE(16, 2, 1, 16, 2, 0, -1);
+    SHAPE(16, 2, 1, 1, 0, 20480, -1); SHAPE(16, 2, 1, 1, 0, 40960, -1); SHAPE(16, 2, 1, 4, 0, 40960, -1);
+    SHAPE(8, 2, 1, 8, 0, 0, -1);
+    // one wave per board, stores in flight per wave capped
+    SHAPE(16, 2, 1, 1, 0, 0, 0); SHAPE(16, 2, 1, 1, 0, 0, 1); SHAPE(16, 2, 1, 1, 0, 0, 2); SHAPE(16, 2, 1, 1, 0, 0, 4);
+    SHAPE(16, 2, 1, 1, 0, 0, 8); SHAPE(16, 2, 1, 2, 0, 0, 1); SHAPE(16, 2, 1, 4, 0, 0, 0);
+    CK(hipFree(buf));
+    return 0;
+  }
   // argv[1] = 20 or 30: 16,384 boards of a 20x20 (72,000 B) or 30x30 (162,000 B) observation
   if (argc > 1) {
     const int L = std::atoi(argv[1]), nb = 16384, rowb = 45 * L * L * 4;

@@ -444,5 +444,42 @@ s36)  # live-slot loads in the two-wave kernel (live) vs the speculative 16 + 16
   TDSTEP_LIB=$PWD/gym-td_amd/lib/libtdstep_live.so OUT=$O/pmc NAME=live_4096 B=4096 timeout -k 10 700 bash scripts/pmc_ab.sh || exit 1
   rm -rf $O/pmc/*/FETCH_SIZE $O/pmc/*/WRITE_SIZE
   ;;
+s37)  # the observation store stream in other shapes (scripts/obs_ceiling.hip shapes): waves per board, boards in flight
+  run shapes 120 scripts/bin/obs_ceiling shapes || exit 1; cat $O/shapes.log
+  ;;
+s38)  # issue priority for the observation writer (s_setprio 1 / 3 inside write_obs_lines) vs the product
+  for r in 1 2; do
+    for spec in 65536:300 32768:600 8192:2000 4096:2000; do
+      bb=${spec%%:*}; st=${spec##*:}
+      for v in base p1 p3; do
+        lib=$PWD/gym-td_amd/lib/libtdstep_$v.so; [ $v = base ] && lib=$PWD/gym-td_amd/lib/libtdstep.so
+        TDSTEP_LIB=$lib run ${v}_${bb}_$r 300 python bench.py --global-batch $bb --steps $st --no-cpu-baseline --timing none || exit 1; line ${v}_${bb}_$r
+      done
+    done
+  done
+  ;;
+s39)  # td_step_kernel_group (16 / 8 boards per workgroup, the group's waves write its windows together): parity, A/B vs the product
+  TDSTEP_LIB=$PWD/gym-td_amd/lib/libtdstep_g16.so run pytest_g16 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -q -x -k "large" --timeout 300 --timeout-method thread -p no:cacheprovider
+  rc=$?; grep -E "^(FAILED|E  )" $O/pytest_g16.log | head -20; tail -1 $O/pytest_g16.log; [ $rc -le 1 ] || exit $rc
+  for r in 1 2; do
+    for spec in 65536:300 32768:600 16384:1000; do
+      bb=${spec%%:*}; st=${spec##*:}
+      run base_${bb}_$r 300 python bench.py --global-batch $bb --steps $st --no-cpu-baseline --timing none || exit 1; line base_${bb}_$r
+      for v in g16 g8; do
+        TDSTEP_LIB=$PWD/gym-td_amd/lib/libtdstep_$v.so run ${v}_${bb}_$r 300 python bench.py --global-batch $bb --steps $st --no-cpu-baseline --timing none --step-kernel large || exit 1; line ${v}_${bb}_$r
+      done
+    done
+  done
+  ;;
+s40)  # the group kernel's structure without the group writer (g16s: 16 boards per workgroup, each wave its own observation; g1s: one), and 4 boards per group
+  for spec in 65536:300 16384:1000; do
+    bb=${spec%%:*}; st=${spec##*:}
+    run base_${bb} 300 python bench.py --global-batch $bb --steps $st --no-cpu-baseline --timing none || exit 1; line base_${bb}
+    run large_${bb} 300 python bench.py --global-batch $bb --steps $st --no-cpu-baseline --timing none --step-kernel large || exit 1; line large_${bb}
+    for v in g1s g16s g4 g16; do
+      TDSTEP_LIB=$PWD/gym-td_amd/lib/libtdstep_$v.so run ${v}_${bb} 300 python bench.py --global-batch $bb --steps $st --no-cpu-baseline --timing none --step-kernel large || exit 1; line ${v}_${bb}
+    done
+  done
+  ;;
 *) echo "unknown session $S"; exit 2;;
 esac
