@@ -1118,12 +1118,6 @@ template <int NC, int LT, int KB = 0, int KE = -1, int G = 4, int PASS = 0>
 __device__ __forceinline__ void write_obs_lines(const Smem<NC>& S, int lane, float* out, bool any_enemy, bool wt,
                                                 int edge_wt = 1) {
   static_assert(LT >= 8, "a 128-B line spans at most two channel planes");
-#ifdef TD_WRITER_PRIO
-  struct PrioGuard {
-    __device__ PrioGuard() { __builtin_amdgcn_s_setprio(TD_WRITER_PRIO); }
-    __device__ ~PrioGuard() { __builtin_amdgcn_s_setprio(0); }
-  } prio_guard_;
-#endif
   constexpr int Q = LT * LT / 4, N4 = NCH * Q;
   constexpr int K = KE >= 0 ? KE : (N4 + 7 + 63) / 64;  // windows [KB, K) of the board's (N4 + 7 + 63) / 64
   constexpr uint32_t OOB = 0x80000000u;  // beyond the buffer's num_records: store dropped
@@ -1231,127 +1225,6 @@ __device__ __forceinline__ void write_obs_lines(const Smem<NC>& S, int lane, flo
     }
   }
 }
-
-#ifdef TD_GROUP_NB
-// The observation of a group of boards written by all of the group's NW waves together
-// (td_step_kernel_group): task t is window t % K of board t / K and goes to wave t % NW,
-// G tasks' LDS reads before their stores.  At any time the group writes the windows of
-// one or two boards: the observation stream of a step then has NW times fewer rows in
-// flight (scripts/obs_ceiling.hip shapes: 16 waves per board 7.0 TB/s, one 5.9).
-// anyb[j]: 0 / 1 board j without / with enemies, 2 not stepped (no observation).
-template <int NC, int LT, int NW, int G = 2>
-__device__ __forceinline__ void write_obs_group(const Smem<NC>* S, const uint32_t* anyb, int nbg, int wv, int lane,
-                                                float* obs0, bool wt, int edge_wt) {
-  constexpr int Q = LT * LT / 4, N4 = NCH * Q;
-  constexpr int K = (N4 + 7 + 63) / 64;
-  constexpr uint32_t OOB = 0x80000000u;
-  typedef Div24<Q, N4 + 64> DivQ;
-  const int T = nbg * K;
-  const int o_cell = (int)(reinterpret_cast<const char*>(S[0].cell) - reinterpret_cast<const char*>(&S[0]));
-  const int o_grp = (int)(reinterpret_cast<const char*>(&S[0].grp[0][0]) - reinterpret_cast<const char*>(&S[0]));
-  const int o_chv = (int)(reinterpret_cast<const char*>(S[0].chv) - reinterpret_cast<const char*>(&S[0]));
-  const int o_d9 = (int)(reinterpret_cast<const char*>(S[0].d9) - reinterpret_cast<const char*>(&S[0]));
-  const int o_gst = (int)(reinterpret_cast<const char*>(&S[0].gst[0][0]) - reinterpret_cast<const char*>(&S[0]));
-  // the boards' flags as wave-uniform bit masks (no per-task LDS read or divergent branch)
-  const uint32_t am = lane < NW ? anyb[lane] : 2u;
-  const uint64_t live = __ballot(am <= 1u), enem = __ballot(am == 1u);
-  for (int t0 = wv; t0 < T; t0 += NW * G) {
-    uint4 A[G];
-    uint32_t W[G];
-#pragma unroll
-    for (int jj = 0; jj < G; ++jj) {
-      const int t = t0 + jj * NW;
-      if (t >= T) continue;  // wave-uniform
-      const int j = t / K, k = t - j * K;
-      if (!((live >> j) & 1u)) continue;
-      const char* const sb = reinterpret_cast<const char*>(&S[j]);
-      const float* const out = obs0 + (size_t)j * N4 * 4;
-      const int mis = (int)((reinterpret_cast<uintptr_t>(out) >> 4) & 7u);
-      const uint32_t wc = (ObsWinTab<LT>::tab.w[mis][k >> 3] >> (4 * (k & 7))) & 7u;
-      int i = lane - mis + 64 * k;
-      if (wc & 4u) i = i < 0 ? 0 : (i > N4 - 1 ? N4 - 1 : i);
-      const int ch = DivQ::div(i), q = i - ch * Q;
-      A[jj] = *reinterpret_cast<const uint4*>(sb + o_cell + 16 * q);
-      if ((wc & 3u) == 1) {
-        W[jj] = *reinterpret_cast<const uint32_t*>(sb + o_chv + 4 * ch);
-      } else if ((wc & 3u) >= 2) {
-        const int e = ch - 25;
-        const int wa = o_grp + (e & 3) * NC + 4 * q, wb = o_chv + 4 * ch, m = -(int)((unsigned)e < 16u);
-        const int wo = wb ^ ((wa ^ wb) & m);
-        W[jj] = *reinterpret_cast<const uint32_t*>(sb + wo);
-      } else {
-        W[jj] = 0u;
-      }
-    }
-#pragma unroll
-    for (int jj = 0; jj < G; ++jj) {
-      const int t = t0 + jj * NW;
-      if (t >= T) continue;
-      const int j = t / K, k = t - j * K;
-      if (!((live >> j) & 1u)) continue;
-      const bool any_enemy = ((enem >> j) & 1u) != 0u;
-      const char* const sb = reinterpret_cast<const char*>(&S[j]);
-      float* const out = obs0 + (size_t)j * N4 * 4;
-      const int mis = (int)((reinterpret_cast<uintptr_t>(out) >> 4) & 7u);
-      const int head = mis ? 8 - mis : 0, tail = ((N4 + mis) & ~7) - mis;
-      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(out, 0, N4 * 16, 0x00020000);
-      const uint32_t wc = (ObsWinTab<LT>::tab.w[mis][k >> 3] >> (4 * (k & 7))) & 7u;
-      const bool edge = (wc & 4u) != 0;
-      const int i = lane - mis + 64 * k;
-      const int iu = edge ? (i < 0 ? 0 : (i > N4 - 1 ? N4 - 1 : i)) : i;
-      const int ch = DivQ::div(iu);
-      const int e = ch - 25;
-      const bool isen = (unsigned)e < 16u, isd9 = ch == 9, isbin = ((kChBin >> ch) & 1ull) != 0;
-      const uint32_t a4[4] = {A[jj].x, A[jj].y, A[jj].z, A[jj].w};
-      float v[4];
-      if ((wc & 3u) == 0) {
-#pragma unroll
-        for (int c = 0; c < 4; ++c) v[c] = (float)((a4[c] >> ch) & 1u);
-      } else if ((wc & 3u) == 1) {
-        const float cv = __uint_as_float(W[jj]);
-#pragma unroll
-        for (int c = 0; c < 4; ++c) v[c] = cv;
-      } else if ((wc & 3u) == 2 && !any_enemy) {
-#pragma unroll
-        for (int c = 0; c < 4; ++c) v[c] = 0.0f;
-      } else {
-        if (isbin) {
-#pragma unroll
-          for (int c = 0; c < 4; ++c) v[c] = (float)((a4[c] >> (ch & 31)) & 1u);
-        } else if (isd9) {
-#pragma unroll
-          for (int c = 0; c < 4; ++c) v[c] = *reinterpret_cast<const float*>(sb + o_d9 + 4 * (int)(a4[c] >> 24));
-        } else if (isen && any_enemy) {
-#pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            const uint32_t gh = (W[jj] >> (8 * c)) & 0xffu;
-            const float f = *reinterpret_cast<const float*>(sb + o_gst + 16 * (int)(gh & 0x7fu) + 4 * ((e >> 2) & 3));
-            v[c] = gh != 0xffu ? f : 0.0f;
-          }
-        } else {
-          const float cv = isen ? 0.0f : __uint_as_float(W[jj]);
-#pragma unroll
-          for (int c = 0; c < 4; ++c) v[c] = cv;
-        }
-      }
-      const f32x4 val = f32x4{v[0], v[1], v[2], v[3]};
-      const uint32_t off = (uint32_t)i * 16u;
-      if (wt) {
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, val), rs, off, 0, 16 /* sc1 */);
-      } else if (!edge) {
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, val), rs, off, 0, 2 /* nt */);
-      } else {
-        const bool shared = i < head || i >= tail;
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, val), rs, shared ? OOB : off, 0, 2 /* nt */);
-        if (edge_wt == 2)
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, val), rs, shared ? off : OOB, 0, 0 /* plain */);
-        else
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, val), rs, shared ? off : OOB, 0, 16 /* sc1 */);
-      }
-    }
-  }
-}
-#endif
 
 // ---------------------------------------------------------------------------
 // board load / reset / store
@@ -1757,12 +1630,9 @@ constexpr int obs_late_half() {
 // SPLIT: the board's workgroup has a second wave (td_step_kernel_small2) that waits at
 // the one workgroup barrier of this path and then writes the second half of the
 // observation windows.
-// NOOBS (td_step_kernel_group): no observation here; *any_out = whether the board has
-// enemies (the group's waves write the windows together), left as is for a board that
-// is not stepped.
-template <int NC, int LT, int MODE, bool SCAN, bool SMALL, bool SPLIT = false, bool NOOBS = false>
+template <int NC, int LT, int MODE, bool SCAN, bool SMALL, bool SPLIT = false>
 __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const StepArgs& a, int b, const Prefetch& P,
-                                           StepOut* so = nullptr, uint32_t* any_out = nullptr) {
+                                           StepOut* so = nullptr) {
   const TdDevCfg& C = x.C;
   uint32_t* const opp = a.opp_mt + (size_t)b * OPP_WORDS;
   uint32_t* const hot = a.opp_hot + (size_t)b * HOT_WORDS;
@@ -1990,9 +1860,7 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
     store_outputs(a, b, reward, ep_ret, real_def, ep_steps, fail_def, done, win, allow, cool, x.lane);
     // the observation last: nothing of the step is live any more, the writer has the registers
     STAMP(6);
-    if constexpr (NOOBS) {
-      *any_out = u.n > 0 ? 1u : 0u;
-    } else if constexpr (LT != 0) {
+    if constexpr (LT != 0) {
       if ((reinterpret_cast<uintptr_t>(a.obs) & 15u) == 0) {
         write_obs_lines<NC, LT>(S, x.lane, obs, u.n > 0, wt, a.edge_wt);
       } else {
@@ -2101,44 +1969,6 @@ __global__ __launch_bounds__(128) TD_SMALL2_ATTR void td_step_kernel_small2(Step
                                                             a.edge_wt);
   }
 }
-
-#ifdef TD_GROUP_NB
-// Experimental: TD_GROUP_NB boards per workgroup, one wave each; the boards step as in
-// td_step_kernel_small without their observation, then all the group's waves write the
-// group's windows together (write_obs_group).
-template <int LT, int MODE, bool SCAN>
-__global__ __launch_bounds__(64 * TD_GROUP_NB) __attribute__((amdgpu_waves_per_eu(8, 8))) void td_step_kernel_group(
-    StepArgs a_) {
-  const StepArgs& a = kargs(a_);
-  constexpr int NC = LT * LT, NW = TD_GROUP_NB;
-  __shared__ Smem<NC> S[NW];
-  __shared__ uint32_t anyb[NW];
-  // the wave index as a wave-uniform (scalar) value: S[wv] is then a scalar base
-  const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6), lane = (int)threadIdx.x & 63;
-  const int ng = (a.B + NW - 1) / NW;
-  if ((int)blockIdx.x >= ng) return;  // the whole workgroup
-  const int g = a.xcd_map ? xcd_board((int)blockIdx.x, ng) : (int)blockIdx.x;
-  const int b = g * NW + wv;
-  uint32_t any = 2u;
-  if (b < a.B) {
-    stage_cfg(S[wv], a.cfg, lane);
-    const Ctx x{S[wv].cfg, LT, NC, lane, a.cfgs, a.epoch};
-    Prefetch P;
-    prefetch_issue<PF_SMALL, PF_SMALL>(P, a, b, lane, NC, MODE != MODE_ATK && !a.multi);
-#ifdef TD_GROUP_SELF  // diagnostic: each wave writes its own board (no barrier, no group writer)
-    step_board<NC, LT, MODE, SCAN, true, false, false>(S[wv], x, a, b, P);
-  }
-  return;
-#else
-    step_board<NC, LT, MODE, SCAN, true, false, true>(S[wv], x, a, b, P, nullptr, &any);
-  }
-#endif
-  if (lane == 0) anyb[wv] = any;
-  __syncthreads();
-  const int nbg = a.B - g * NW < NW ? a.B - g * NW : NW;
-  write_obs_group<NC, LT, NW>(S, anyb, nbg, wv, lane, a.obs + (size_t)g * NW * NCH * NC, a.obs_wt != 0, a.edge_wt);
-}
-#endif
 
 // The built-in opponents called on their own, between steps (TDGymBasic.py:81-292,
 // called directly by demo.py:78-79): random_enemy_lv{0,1} (side 0) or
@@ -2493,23 +2323,12 @@ static hipError_t launch2(const StepArgs& a, hipStream_t s, bool reset, hipEvent
     if (ev0) hipExtLaunchKernelGGL(k, dim3(a.B), dim3(128), 0, s, ev0, ev1, 0, a);       \
     else hipLaunchKernelGGL(k, dim3(a.B), dim3(128), 0, s, a);                           \
   } while (0)
-#ifdef TD_GROUP_NB
-#define TD_LAUNCHG(k)                                                                                        \
-  do {                                                                                                       \
-    const int ng_ = (a.B + TD_GROUP_NB - 1) / TD_GROUP_NB;                                                   \
-    if (ev0) hipExtLaunchKernelGGL(k, dim3(ng_), dim3(64 * TD_GROUP_NB), 0, s, ev0, ev1, 0, a);             \
-    else hipLaunchKernelGGL(k, dim3(ng_), dim3(64 * TD_GROUP_NB), 0, s, a);                                 \
-  } while (0)
-#endif
   const bool aligned = (reinterpret_cast<uintptr_t>(a.obs) & 15u) == 0;
   if (reset) {
     hipLaunchKernelGGL(td_reset_kernel<LT>, dim3(a.B), dim3(64), 0, s, a);
   } else if constexpr (LT != 0) {
     if (a.small == 2 && aligned) TD_STEP_DISPATCH(td_step_kernel_small2, LT, a, TD_LAUNCH2);
     else if (a.small && aligned) TD_STEP_DISPATCH(td_step_kernel_small, LT, a, TD_LAUNCH);
-#ifdef TD_GROUP_NB
-    else if (LT == 10 && aligned) TD_STEP_DISPATCH(td_step_kernel_group, 10, a, TD_LAUNCHG);
-#endif
     else TD_STEP_DISPATCH(td_step_kernel, LT, a, TD_LAUNCH);
   } else {
     TD_STEP_DISPATCH(td_step_kernel, LT, a, TD_LAUNCH);
