@@ -507,5 +507,19 @@ s41)  # final-build validation and profiles on the round's last sources (s35's s
     rm -rf $O/pmc/${wl}_$bb/FETCH_SIZE $O/pmc/${wl}_$bb/WRITE_SIZE
   done
   ;;
+s42)  # fewer boards per CU in the two-wave kernel (extra dynamic LDS per workgroup, TD_DYN_LDS in the dyn build): 10x10 65,536, 2p, 30x30
+  L=$PWD/gym-td_amd/lib/libtdstep_dyn.so
+  for r in 1 2; do
+    for d in 0 7600 13200; do
+      TD_DYN_LDS=$d TDSTEP_LIB=$L run d10_${d}_$r 300 python bench.py --steps 300 --no-cpu-baseline --timing none --step-kernel small2 || exit 1; line d10_${d}_$r
+    done
+    for d in 0 5200 10800; do
+      TD_DYN_LDS=$d TDSTEP_LIB=$L run d20_${d}_$r 300 python bench.py --workload 2p-middle-multi --steps 200 --no-cpu-baseline --timing none --step-kernel small2 || exit 1; line d20_${d}_$r
+    done
+    for d in 0 1200 3400; do
+      TD_DYN_LDS=$d TDSTEP_LIB=$L run d30_${d}_$r 300 python bench.py --workload def-large --global-batch 16384 --steps 200 --no-cpu-baseline --timing none --step-kernel small2 || exit 1; line d30_${d}_$r
+    done
+  done
+  ;;
 *) echo "unknown session $S"; exit 2;;
 esac
