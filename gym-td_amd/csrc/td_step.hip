@@ -2318,15 +2318,10 @@ static hipError_t launch2(const StepArgs& a, hipStream_t s, bool reset, hipEvent
     if (ev0) hipExtLaunchKernelGGL(k, dim3(a.B), dim3(64), 0, s, ev0, ev1, 0, a);       \
     else hipLaunchKernelGGL(k, dim3(a.B), dim3(64), 0, s, a);                           \
   } while (0)
-#ifdef TD_DYN_LDS_KNOB  // diagnostic build: extra dynamic LDS per two-wave workgroup (fewer boards per CU)
-  static const int dyn_lds = getenv("TD_DYN_LDS") ? atoi(getenv("TD_DYN_LDS")) : 0;
-#else
-  constexpr int dyn_lds = 0;
-#endif
 #define TD_LAUNCH2(k)                                                                    \
   do {                                                                                   \
-    if (ev0) hipExtLaunchKernelGGL(k, dim3(a.B), dim3(128), dyn_lds, s, ev0, ev1, 0, a); \
-    else hipLaunchKernelGGL(k, dim3(a.B), dim3(128), dyn_lds, s, a);                     \
+    if (ev0) hipExtLaunchKernelGGL(k, dim3(a.B), dim3(128), 0, s, ev0, ev1, 0, a);       \
+    else hipLaunchKernelGGL(k, dim3(a.B), dim3(128), 0, s, a);                           \
   } while (0)
   const bool aligned = (reinterpret_cast<uintptr_t>(a.obs) & 15u) == 0;
   if (reset) {
