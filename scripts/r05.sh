@@ -521,5 +521,18 @@ s42)  # fewer boards per CU in the two-wave kernel (extra dynamic LDS per workgr
     done
   done
   ;;
+s43)  # the two-wave kernel without the early binary-plane pass (ne: both waves write after the step, windows split at 9) vs the product
+  TDSTEP_LIB=$PWD/gym-td_amd/lib/libtdstep_ne.so run pytest_ne 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -q -x -k small2 --timeout 300 --timeout-method thread -p no:cacheprovider
+  rc=$?; grep -E "^(FAILED|E  )" $O/pytest_ne.log | head -20; tail -1 $O/pytest_ne.log; [ $rc -le 1 ] || exit $rc
+  for r in 1 2; do
+    for spec in 65536:300 32768:600 16384:1000 4096:2000; do
+      bb=${spec%%:*}; st=${spec##*:}
+      for v in base ne; do
+        lib=$PWD/gym-td_amd/lib/libtdstep_$v.so; [ $v = base ] && lib=$PWD/gym-td_amd/lib/libtdstep.so
+        TDSTEP_LIB=$lib run ${v}_${bb}_$r 300 python bench.py --global-batch $bb --steps $st --no-cpu-baseline --timing none --step-kernel small2 || exit 1; line ${v}_${bb}_$r
+      done
+    done
+  done
+  ;;
 *) echo "unknown session $S"; exit 2;;
 esac
