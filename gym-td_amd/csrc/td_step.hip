@@ -1615,9 +1615,6 @@ __host__ __device__ constexpr int obs_half() { return ((NCH * LT * LT / 4 + 7 + 
 // the second wave's share of the rest, so both waves write half of the remaining
 // windows (counted at a line-aligned board; ObsWinTab class != 0).
 template <int LT>
-#ifndef TD_NO_EARLY  // diagnostic: no early binary-plane pass, the two waves split the windows at 9
-#define TD_NO_EARLY 0
-#endif
 constexpr int obs_late_half() {
   constexpr int K = (NCH * LT * LT / 4 + 7 + 63) / 64;
   int late = 0;
@@ -1849,7 +1846,7 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
     __syncthreads();
     STAMP(6);
     if (was_reset) write_obs_lines<NC, LT>(S, x.lane, obs, u.n > 0, wt, a.edge_wt);
-    else write_obs_lines<NC, LT, 0, TD_NO_EARLY ? 9 : obs_late_half<LT>(), 4, TD_NO_EARLY ? 0 : 2>(S, x.lane, obs, u.n > 0, wt, a.edge_wt);
+    else write_obs_lines<NC, LT, 0, obs_late_half<LT>(), 4, 2>(S, x.lane, obs, u.n > 0, wt, a.edge_wt);
   } else {
     enemy_stats(S, u, x);  // no-op for a board without enemies (e.g. just reset)
     STAMP(13);
@@ -1952,7 +1949,7 @@ __global__ __launch_bounds__(128) TD_SMALL2_ATTR void td_step_kernel_small2(Step
     if constexpr (SCAN2) {  // the real actions, beside the step (grp[1] is not touched before (B))
       if (S.early_go && a.real_def) scan_write_real(S, lane, NC, a.real_def + (size_t)b * 6 * NC);
     }
-    if (!TD_NO_EARLY && S.early_go) {
+    if (S.early_go) {
       write_obs_lines<NC, LT, 0, -1, 4, 1>(S, lane, obs, false, a.obs_wt != 0, a.edge_wt);
       // landed before (B): after an auto-reset the first wave rewrites these windows
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1968,7 +1965,7 @@ __global__ __launch_bounds__(128) TD_SMALL2_ATTR void td_step_kernel_small2(Step
     }
     __syncthreads();  // (C) statistics and broadcast channels in LDS
     if (go == 1u)
-      write_obs_lines<NC, LT, TD_NO_EARLY ? 9 : obs_late_half<LT>(), -1, 4, TD_NO_EARLY ? 0 : 2>(S, lane, obs, SO.any != 0u, a.obs_wt != 0,
+      write_obs_lines<NC, LT, obs_late_half<LT>(), -1, 4, 2>(S, lane, obs, SO.any != 0u, a.obs_wt != 0,
                                                             a.edge_wt);
   }
 }
