@@ -534,5 +534,18 @@ s43)  # the two-wave kernel without the early binary-plane pass (ne: both waves 
     done
   done
   ;;
+s44)  # td_step_kernel_wq (8 / 4 boards per workgroup + as many writer waves fed through an LDS queue): parity, A/B vs the product
+  TDSTEP_LIB=$PWD/gym-td_amd/lib/libtdstep_wq8.so run pytest_wq8 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -q -x -k "large" --timeout 300 --timeout-method thread -p no:cacheprovider
+  rc=$?; grep -E "^(FAILED|E  )" $O/pytest_wq8.log | head -20; tail -1 $O/pytest_wq8.log; [ $rc -le 1 ] || exit $rc
+  for r in 1 2; do
+    for spec in 65536:300 32768:600 16384:1000; do
+      bb=${spec%%:*}; st=${spec##*:}
+      run base_${bb}_$r 300 python bench.py --global-batch $bb --steps $st --no-cpu-baseline --timing none || exit 1; line base_${bb}_$r
+      for v in wq8 wq4; do
+        TDSTEP_LIB=$PWD/gym-td_amd/lib/libtdstep_$v.so run ${v}_${bb}_$r 300 python bench.py --global-batch $bb --steps $st --no-cpu-baseline --timing none --step-kernel large || exit 1; line ${v}_${bb}_$r
+      done
+    done
+  done
+  ;;
 *) echo "unknown session $S"; exit 2;;
 esac
