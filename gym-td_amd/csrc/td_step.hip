@@ -1226,123 +1226,6 @@ __device__ __forceinline__ void write_obs_lines(const Smem<NC>& S, int lane, flo
   }
 }
 
-#ifdef TD_WQ
-// Experimental (td_step_kernel_wq): windows kstart, kstart + NWR, ... of one board.
-template <int NC, int LT, int NWR, int G = 3>
-__device__ __forceinline__ void write_obs_part(const Smem<NC>& S, int lane, float* out, bool any_enemy, bool wt,
-                                                int edge_wt, int kstart) {
-  constexpr int PASS = 0;
-  static_assert(LT >= 8, "a 128-B line spans at most two channel planes");
-  constexpr int Q = LT * LT / 4, N4 = NCH * Q;
-  constexpr int K = (N4 + 7 + 63) / 64;  // windows [KB, K) of the board's (N4 + 7 + 63) / 64
-  constexpr uint32_t OOB = 0x80000000u;  // beyond the buffer's num_records: store dropped
-  const char* const sb = reinterpret_cast<const char*>(&S);
-  const int o_cell = (int)(reinterpret_cast<const char*>(S.cell) - sb);  // packed cell words (pack_obs_cells)
-  const int o_grp = (int)(reinterpret_cast<const char*>(&S.grp[0][0]) - sb);
-  const int o_chv = (int)(reinterpret_cast<const char*>(S.chv) - sb);
-  const int o_d9 = (int)(reinterpret_cast<const char*>(S.d9) - sb);
-  const int o_gst = (int)(reinterpret_cast<const char*>(&S.gst[0][0]) - sb);
-  const int mis = (int)((reinterpret_cast<uintptr_t>(out) >> 4) & 7u);  // units of the line before the board
-  const int head = mis ? 8 - mis : 0, tail = ((N4 + mis) & ~7) - mis;   // [0, head), [tail, N4): shared lines
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(out, 0, N4 * 16, 0x00020000);
-  const int i0 = lane - mis;
-  typedef Div24<Q, N4 + 64> DivQ;  // unit -> channel (every unit read is in [0, N4))
-  // the window's channel class and edge bit (wave-uniform, ObsWinTab)
-  auto wclass = [&](int k) { return (ObsWinTab<LT>::tab.w[mis][k >> 3] >> (4 * (k & 7))) & 7u; };
-  // only a window at either end of the board holds lanes outside it (i < 0, i >= N4):
-  // clamp there, so every lane reads LDS inside the board image
-  auto unit = [&](int i, uint32_t wc) { return (wc & 4u) ? (i < 0 ? 0 : (i > N4 - 1 ? N4 - 1 : i)) : i; };
-  for (int k0 = kstart; k0 < K; k0 += NWR * G) {
-    uint4 A[G];
-    uint32_t W[G];
-#pragma unroll
-    for (int j = 0; j < G; ++j) {
-      const int k = k0 + j * NWR;
-      if (k < K) {
-        const uint32_t wc = wclass(k);
-        if (PASS != 0 && (((wc & 3u) == 0) != (PASS == 1))) continue;  // wave-uniform
-        const int i = unit(i0 + 64 * k, wc);
-        const int ch = DivQ::div(i), q = i - ch * Q;
-        A[j] = *reinterpret_cast<const uint4*>(sb + o_cell + 16 * q);
-        if ((wc & 3u) == 1) {  // broadcast channels only: the channel's value
-          W[j] = *reinterpret_cast<const uint32_t*>(sb + o_chv + 4 * ch);
-        } else if ((wc & 3u) >= 2) {
-          // enemy plane: the cell quad's group bytes; else the channel's broadcast value
-          // (bit select: a ternary here compiled to a divergent branch)
-          const int e = ch - 25;
-          const int wa = o_grp + (e & 3) * NC + 4 * q, wb = o_chv + 4 * ch, m = -(int)((unsigned)e < 16u);
-          const int wo = wb ^ ((wa ^ wb) & m);
-          W[j] = *reinterpret_cast<const uint32_t*>(sb + wo);
-        } else {
-          W[j] = 0u;  // binary planes only: the cell quad is all
-        }
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < G; ++j) {
-      const int k = k0 + j * NWR;
-      if (k >= K) continue;
-      const uint32_t wc = wclass(k);
-      if (PASS != 0 && (((wc & 3u) == 0) != (PASS == 1))) continue;
-      const bool edge = (wc & 4u) != 0;  // the window holds a line shared with a neighbour
-      const int i = i0 + 64 * k;
-      const int ch = DivQ::div(unit(i, wc));
-      const int e = ch - 25;
-      const bool isen = (unsigned)e < 16u, isd9 = ch == 9, isbin = ((kChBin >> ch) & 1ull) != 0;
-      const uint32_t a4[4] = {A[j].x, A[j].y, A[j].z, A[j].w};
-      float v[4];
-      if ((wc & 3u) == 0) {
-#pragma unroll
-        for (int c = 0; c < 4; ++c) v[c] = (float)((a4[c] >> ch) & 1u);
-      } else if ((wc & 3u) == 1) {
-        const float cv = __uint_as_float(W[j]);
-#pragma unroll
-        for (int c = 0; c < 4; ++c) v[c] = cv;
-      } else if ((wc & 3u) == 2 && !any_enemy) {
-#pragma unroll
-        for (int c = 0; c < 4; ++c) v[c] = 0.0f;
-      } else {
-        // a window of several channel kinds: each lane takes its own channel's path
-        // (a select over every kind's value measured 1.5 % slower at 8,192 boards)
-        if (isbin) {
-#pragma unroll
-          for (int c = 0; c < 4; ++c) v[c] = (float)((a4[c] >> (ch & 31)) & 1u);
-        } else if (isd9) {  // channel 9 by distance
-#pragma unroll
-          for (int c = 0; c < 4; ++c) v[c] = *reinterpret_cast<const float*>(sb + o_d9 + 4 * (int)(a4[c] >> 24));
-        } else if (isen && any_enemy) {  // enemy stats by the cell's group head
-#pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            const uint32_t g = (W[j] >> (8 * c)) & 0xffu;
-            const float f = *reinterpret_cast<const float*>(sb + o_gst + 16 * (int)(g & 0x7fu) + 4 * ((e >> 2) & 3));
-            v[c] = g != 0xffu ? f : 0.0f;
-          }
-        } else {
-          const float cv = isen ? 0.0f : __uint_as_float(W[j]);
-#pragma unroll
-          for (int c = 0; c < 4; ++c) v[c] = cv;
-        }
-      }
-      const f32x4 val = f32x4{v[0], v[1], v[2], v[3]};
-      const uint32_t off = (uint32_t)i * 16u;  // i < 0 or i >= N4: out of range already
-      if (wt) {  // wave-uniform
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, val), rs, off, 0, 16 /* sc1 */);
-      } else if (!edge) {  // whole lines of this board only
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, val), rs, off, 0, 2 /* nt */);
-      } else {
-        const bool shared = i < head || i >= tail;  // a line shared with a neighbouring board
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, val), rs, shared ? OOB : off, 0, 2 /* nt */);
-        if (edge_wt == 2)
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, val), rs, shared ? off : OOB, 0, 0 /* plain */);
-        else
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, val), rs, shared ? off : OOB, 0, 16 /* sc1 */);
-      }
-    }
-  }
-}
-
-#endif
-
 // ---------------------------------------------------------------------------
 // board load / reset / store
 // ---------------------------------------------------------------------------
@@ -1747,9 +1630,9 @@ constexpr int obs_late_half() {
 // SPLIT: the board's workgroup has a second wave (td_step_kernel_small2) that waits at
 // the one workgroup barrier of this path and then writes the second half of the
 // observation windows.
-template <int NC, int LT, int MODE, bool SCAN, bool SMALL, bool SPLIT = false, bool NOOBS = false>
+template <int NC, int LT, int MODE, bool SCAN, bool SMALL, bool SPLIT = false>
 __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const StepArgs& a, int b, const Prefetch& P,
-                                           StepOut* so = nullptr, uint32_t* any_out = nullptr) {
+                                           StepOut* so = nullptr) {
   const TdDevCfg& C = x.C;
   uint32_t* const opp = a.opp_mt + (size_t)b * OPP_WORDS;
   uint32_t* const hot = a.opp_hot + (size_t)b * HOT_WORDS;
@@ -1977,9 +1860,7 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
     store_outputs(a, b, reward, ep_ret, real_def, ep_steps, fail_def, done, win, allow, cool, x.lane);
     // the observation last: nothing of the step is live any more, the writer has the registers
     STAMP(6);
-    if constexpr (NOOBS) {
-      *any_out = u.n > 0 ? 1u : 0u;
-    } else if constexpr (LT != 0) {
+    if constexpr (LT != 0) {
       if ((reinterpret_cast<uintptr_t>(a.obs) & 15u) == 0) {
         write_obs_lines<NC, LT>(S, x.lane, obs, u.n > 0, wt, a.edge_wt);
       } else {
@@ -2088,63 +1969,6 @@ __global__ __launch_bounds__(128) TD_SMALL2_ATTR void td_step_kernel_small2(Step
                                                             a.edge_wt);
   }
 }
-
-#ifdef TD_WQ
-// Experimental: TD_WQ boards per workgroup, one stepping wave each, plus TD_WQ writer waves.
-// A stepping wave steps its board without the observation, then appends the board to the
-// workgroup's LDS queue; the writer waves take the queue in order and write each board's
-// windows together (window k by writer k % TD_WQ), so a CU writes few boards' rows at a
-// time while its other waves step.  Writers wait for a queue entry with a bounded poll.
-template <int LT, int MODE, bool SCAN>
-__global__ __launch_bounds__(128 * TD_WQ) __attribute__((amdgpu_waves_per_eu(8, 8))) void td_step_kernel_wq(
-    StepArgs a_) {
-  const StepArgs& a = kargs(a_);
-  constexpr int NC = LT * LT, NB = TD_WQ;
-  __shared__ Smem<NC> S[NB];
-  __shared__ uint32_t qtail, qid[NB], anyb[NB];
-  const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6), lane = (int)threadIdx.x & 63;
-  const int ng = (a.B + NB - 1) / NB;
-  if ((int)blockIdx.x >= ng) return;  // the whole workgroup
-  if (threadIdx.x < NB) qid[threadIdx.x] = 0u;
-  if (threadIdx.x == 0) qtail = 0u;
-  __syncthreads();
-  const int g = a.xcd_map ? xcd_board((int)blockIdx.x, ng) : (int)blockIdx.x;
-  if (wv < NB) {
-    const int b = g * NB + wv;
-    uint32_t any = 2u;
-    if (b < a.B) {
-      stage_cfg(S[wv], a.cfg, lane);
-      const Ctx x{S[wv].cfg, LT, NC, lane, a.cfgs, a.epoch};
-      Prefetch P;
-      prefetch_issue<PF_SMALL, PF_SMALL>(P, a, b, lane, NC, MODE != MODE_ATK && !a.multi);
-      step_board<NC, LT, MODE, SCAN, true, false, true>(S[wv], x, a, b, P, nullptr, &any);
-    }
-    wsync();  // the board image is in LDS before the board is queued
-    if (lane == 0) {
-      anyb[wv] = any;
-      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): anyb lands first
-      const uint32_t slot = atomicAdd(&qtail, 1u);
-      __atomic_store_n(&qid[slot], (uint32_t)wv + 1u, __ATOMIC_RELAXED);
-    }
-    return;
-  }
-  const int wq = wv - NB;
-  for (int q = 0; q < NB; ++q) {
-    uint32_t id = 0;
-    for (int spin = 0; spin < (1 << 14); ++spin) {  // bounded (about 1 ms): never a hang
-      id = __builtin_amdgcn_readfirstlane(__atomic_load_n(&qid[q], __ATOMIC_RELAXED));
-      if (id != 0u) break;
-      __builtin_amdgcn_s_sleep(2);
-    }
-    if (id == 0u) return;
-    const int j = (int)id - 1;
-    const uint32_t any = __builtin_amdgcn_readfirstlane(anyb[j]);
-    if (any > 1u) continue;
-    write_obs_part<NC, LT, NB>(S[j], lane, a.obs + (size_t)(g * NB + j) * NCH * NC, any != 0u, a.obs_wt != 0,
-                               a.edge_wt, wq);
-  }
-}
-#endif
 
 // The built-in opponents called on their own, between steps (TDGymBasic.py:81-292,
 // called directly by demo.py:78-79): random_enemy_lv{0,1} (side 0) or
@@ -2499,23 +2323,12 @@ static hipError_t launch2(const StepArgs& a, hipStream_t s, bool reset, hipEvent
     if (ev0) hipExtLaunchKernelGGL(k, dim3(a.B), dim3(128), 0, s, ev0, ev1, 0, a);       \
     else hipLaunchKernelGGL(k, dim3(a.B), dim3(128), 0, s, a);                           \
   } while (0)
-#ifdef TD_WQ
-#define TD_LAUNCHQ(k)                                                                                        \
-  do {                                                                                                       \
-    const int ng_ = (a.B + TD_WQ - 1) / TD_WQ;                                                               \
-    if (ev0) hipExtLaunchKernelGGL(k, dim3(ng_), dim3(128 * TD_WQ), 0, s, ev0, ev1, 0, a);                  \
-    else hipLaunchKernelGGL(k, dim3(ng_), dim3(128 * TD_WQ), 0, s, a);                                      \
-  } while (0)
-#endif
   const bool aligned = (reinterpret_cast<uintptr_t>(a.obs) & 15u) == 0;
   if (reset) {
     hipLaunchKernelGGL(td_reset_kernel<LT>, dim3(a.B), dim3(64), 0, s, a);
   } else if constexpr (LT != 0) {
     if (a.small == 2 && aligned) TD_STEP_DISPATCH(td_step_kernel_small2, LT, a, TD_LAUNCH2);
     else if (a.small && aligned) TD_STEP_DISPATCH(td_step_kernel_small, LT, a, TD_LAUNCH);
-#ifdef TD_WQ
-    else if (LT == 10 && aligned) TD_STEP_DISPATCH(td_step_kernel_wq, 10, a, TD_LAUNCHQ);
-#endif
     else TD_STEP_DISPATCH(td_step_kernel, LT, a, TD_LAUNCH);
   } else {
     TD_STEP_DISPATCH(td_step_kernel, LT, a, TD_LAUNCH);
