@@ -547,5 +547,13 @@ s44)  # td_step_kernel_wq (8 / 4 boards per workgroup + as many writer waves fed
     done
   done
   ;;
+s45)  # the round's closing check on the final tree: GPU suite, smoke, the driver's command twice
+  gpusuite 900; rc=$?; [ $rc -le 1 ] || exit $rc
+  run smoke 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" || exit 1
+  for r in 1 2; do
+    run bench_driver_$r 300 python bench.py --gpus 1 --steps 20 --warmup 5 || exit 1; line bench_driver_$r
+  done
+  grep -h '"traffic"' $O/bench_driver_1.log | grep -o '"traffic": [^,]*' | head -1
+  ;;
 *) echo "unknown session $S"; exit 2;;
 esac
