@@ -555,5 +555,25 @@ s45)  # the round's closing check on the final tree: GPU suite, smoke, the drive
   done
   grep -h '"traffic"' $O/bench_driver_1.log | grep -o '"traffic": [^,]*' | head -1
   ;;
+s46)  # the queue-fed writer kernel with 1 / 2 boards per workgroup (libs built from the s44 commit): does the per-workgroup max-of-boards cost explain s44?
+  TDSTEP_LIB=$PWD/gym-td_amd/lib/libtdstep_wq1.so run pytest_wq1 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -q -x -k "large and batched" --timeout 300 --timeout-method thread -p no:cacheprovider
+  rc=$?; tail -1 $O/pytest_wq1.log; [ $rc -le 1 ] || exit $rc
+  for spec in 65536:300 16384:1000; do
+    bb=${spec%%:*}; st=${spec##*:}
+    run base_${bb} 300 python bench.py --global-batch $bb --steps $st --no-cpu-baseline --timing none || exit 1; line base_${bb}
+    for v in wq1 wq2; do
+      TDSTEP_LIB=$PWD/gym-td_amd/lib/libtdstep_$v.so run ${v}_${bb} 300 python bench.py --global-batch $bb --steps $st --no-cpu-baseline --timing none --step-kernel large || exit 1; line ${v}_${bb}
+    done
+  done
+  ;;
+s47)  # the queue-fed writer kernel without scratch (7 waves per SIMD: 67 VGPRs, no spill; 1 / 2 boards per workgroup) vs the product
+  for spec in 65536:300 16384:1000; do
+    bb=${spec%%:*}; st=${spec##*:}
+    run base_${bb} 300 python bench.py --global-batch $bb --steps $st --no-cpu-baseline --timing none || exit 1; line base_${bb}
+    for v in wq1w7 wq2w7; do
+      TDSTEP_LIB=$PWD/gym-td_amd/lib/libtdstep_$v.so run ${v}_${bb} 300 python bench.py --global-batch $bb --steps $st --no-cpu-baseline --timing none --step-kernel large || exit 1; line ${v}_${bb}
+    done
+  done
+  ;;
 *) echo "unknown session $S"; exit 2;;
 esac
