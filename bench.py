@@ -75,7 +75,8 @@ DATA = {("def", False): "synthetic: uniform random defender actions, built-in lv
 N_ACTION_BUFS = 8  # distinct pre-drawn action batches cycled through the timed steps (multi-action shapes)
 EVENT_EVERY = 8  # timed steps per sampled kernel duration when the warm-up gives no step time (--warmup 0)
 
-FLAG_BITS = (("enemy_overflow", 1), ("tower_overflow", 2), ("bad_action", 4), ("no_layout", 8), ("bad_move", 16))
+FLAG_BITS = (("enemy_overflow", 1), ("tower_overflow", 2), ("bad_action", 4), ("no_layout", 8), ("bad_move", 16),
+             ("claim_timeout", 32))
 
 # The step kernel is sampled inside the timed region itself, on every k-th launch.  A
 # launch bound to a timing-event pair (td_kernel_timing) delays the next dispatch by about
@@ -88,20 +89,47 @@ FLAG_BITS = (("enemy_overflow", 1), ("tower_overflow", 2), ("bad_action", 4), ("
 # 1,200 burn-in steps, 228.0 after 1,456, 231.9 after 1,520, r05/s10).
 EVENT_COST_US = 3.0
 EVENT_PERTURB = 0.01
+MIN_SAMPLES = 4  # sampled launches per rank at least (when the timed steps allow it)
 
 
 def event_every(steps, warm_step_us=None, override=None):
     """Timed launches per sampled kernel duration: the smallest k with EVENT_COST_US / k
-    below EVENT_PERTURB of the warm-up's step time, at least 2, at most ceil(steps / 2).
-    The driver's 20 steps at 65,536 boards (~210 us): every 2nd launch, 10 samples
-    (kernel 205.7-207.4 us in steps of 209.0-209.9, against 209.8-210.4 without events,
-    r05/s10).  Without a warm-up step time: every EVENT_EVERY-th."""
+    below EVENT_PERTURB of the warm-up's step time, at least 2, but never so large that the
+    timed steps hold fewer than MIN_SAMPLES samples (k <= steps // MIN_SAMPLES, at least 1).
+    The driver's 20 steps at 65,536 boards (~204 us): every 2nd launch, 10 samples; at the
+    N = 8 share (8,192 boards, ~32 us) every 5th, 4 samples per rank.
+    Without a warm-up step time: every EVENT_EVERY-th, within the same cap."""
     if override:
         return max(1, int(override))
+    cap = max(1, steps // MIN_SAMPLES)
     if not (warm_step_us and warm_step_us > 0):
-        return EVENT_EVERY
-    k = math.ceil(EVENT_COST_US / (EVENT_PERTURB * warm_step_us))
-    return int(max(2, min(k, (steps + 1) // 2)))
+        return int(min(EVENT_EVERY, cap))
+    k = max(2, math.ceil(EVENT_COST_US / (EVENT_PERTURB * warm_step_us)))
+    return int(min(k, cap))
+
+
+def timed_region(run, sync, barrier=None, clock=time.perf_counter):
+    """Time run() -- the K timed steps -- on this rank.  Opening: sync, barrier (every rank
+    starts together), sync, clock.  Closing: sync, clock -- the rank's own steps end there --
+    then the closing barrier and a sync, timed on their own.  The closing barrier is outside
+    the timed region: at N = 8 a rank times only ~20 x 32 us, and a
+    barrier's latency and release skew would be charged to the metric; the MAX over ranks of
+    the returned times is the whole job's.  Returns (elapsed s, closing barrier s)."""
+    sync()
+    if barrier is not None:
+        barrier()
+    sync()
+    t0 = clock()
+    run()
+    sync()
+    elapsed = clock() - t0
+    barrier_s = 0.0
+    if barrier is not None:
+        tb = clock()
+        barrier()
+        sync()
+        barrier_s = clock() - tb
+    return elapsed, barrier_s
 
 
 def kernel_vs_step(avg_kernel_us, step_us):
@@ -121,6 +149,16 @@ def algorithmic_bytes(L, mode="def", multi=False):
     act = (6 * L * L * 8 if multi else 8) if mode != "atk" else 0
     act += 3 * 8 * 8 if mode != "def" else 0
     return obs + act + 8 + 1
+
+
+def stagger_mask(k, gidx, period):
+    """The burn-in's explicit resets before step k: the boards whose global index is k modulo
+    the episode limit (``period``, 1,200 steps), for 0 < k < period, so that after a full
+    burn-in the episode phases are spread uniformly.  None when no board is reset."""
+    if k <= 0 or k >= period:
+        return None
+    m = (np.asarray(gidx) % period) == k
+    return m if m.any() else None
 
 
 def partition(workload, world, global_batch=None, boards_per_gpu=None):
@@ -334,17 +372,20 @@ def init_dist(gpu, backend="nccl"):
     return torch.device("cpu")
 
 
-def collect(elapsed, avg_kernel_s, warm_step_s, ep_stats, ep_recs, coll):
-    """After the timed region: the MAX of the clocks over ranks (one all_reduce) and the
+def collect(elapsed, avg_kernel_s, warm_step_s, ep_stats, ep_recs, coll, barrier_s=0.0):
+    """After the timed region: the MAX of the clocks over ranks (one all_reduce), each
+    rank's own clocks (elapsed, kernel mean, warm-up step, closing barrier; f64 [4]), the
     timed steps' episode statistics (per-rank count / return sum, f64 [2]) and per-board
     last-episode records (16 B per board) gathered to rank 0 -- the only exchange of a run,
     over RCCL on GPUs.  Returns ((elapsed, avg_kernel_s, warm_step_s), per_rank [W, 2],
-    (ret, length, win)); the last two are None off rank 0."""
+    (ret, length, win), clocks [W, 4]); the last three are None off rank 0."""
     from gym_TD import shard
-    t = shard.max_over_ranks(torch.tensor([elapsed, avg_kernel_s, warm_step_s], dtype=torch.float64, device=coll))
+    mine = torch.tensor([elapsed, avg_kernel_s, warm_step_s, barrier_s], dtype=torch.float64, device=coll)
+    clocks = shard.gather_stats(mine.clone())
+    t = shard.max_over_ranks(mine[:3].clone())
     per_rank = shard.gather_stats(ep_stats.to(coll))
     recs = shard.gather_episode_records(*[x.to(coll) for x in ep_recs])
-    return tuple(float(v) for v in t.cpu()), per_rank, recs
+    return tuple(float(v) for v in t.cpu()), per_rank, recs, (clocks.cpu().numpy() if clocks is not None else None)
 
 
 # --------------------------------------------------------------------------- main
@@ -430,10 +471,9 @@ def main():
     period = P.hyper_parameters.max_episode_steps
     gidx = np.arange(B) + rank * B
     for k in range(args.burnin):
-        if args.stagger and k < period and k > 0:
-            m = (gidx % period) == k
-            if m.any():
-                eng.reset(m)  # a failing draw leaves the board in its first episode (the reference raises)
+        m = stagger_mask(k, gidx, period) if args.stagger else None
+        if m is not None:
+            eng.reset(m)  # the boards' next staged layouts (tests/test_gpu_steady.py checks this recipe)
         d, a = (pool[k % N_ACTION_BUFS] if multi else draw(1)[0])
         eng.step(def_act=d, atk_act=a)
     acts = pool if multi else draw(K)
@@ -467,17 +507,8 @@ def main():
         ev = {k: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for k in sampled}
     eng.episode_stats(clear=True)  # the device accumulates finished episodes of the timed steps
 
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    run_steps(K, 0)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
+    elapsed, barrier_s = timed_region(lambda: run_steps(K, 0), lambda: torch.cuda.synchronize(dev),
+                                      dist.barrier if world > 1 else None)
 
     # snapshots of the timed steps' episode statistics and flags (stream-ordered copies)
     flags = eng.flags()
@@ -493,8 +524,9 @@ def main():
     avg_kernel_s = float(np.mean(kern_ms)) / 1e3 if kern_ms else float("nan")
     # after timing: MAX of the clocks over ranks, and the episode statistics of the
     # timed steps gathered to rank 0 (the only exchange; RCCL on GPUs)
-    (elapsed, avg_kernel_s, warm_step_s), per_rank, recs = collect(
-        elapsed, avg_kernel_s, warm_step_s, ep_stats, ep_recs, coll)
+    guard_to = eng.guard_timeouts()
+    (elapsed, avg_kernel_s, warm_step_s), per_rank, recs, clocks = collect(
+        elapsed, avg_kernel_s, warm_step_s, ep_stats, ep_recs, coll, barrier_s)
     reported_world = dist.get_world_size() if world > 1 else 1  # what the process group (RCCL) reports
 
     if rank == 0:
@@ -523,6 +555,8 @@ def main():
                          "kernel": eng.step_kernel_name,
                          "avg_kernel_us": avg_kernel_s * 1e6,
                          "kernel_samples": len(kern_ms) * world,
+                         "kernel_samples_per_rank": len(kern_ms),
+                         "low_sample_count": len(kern_ms) < MIN_SAMPLES,
                          "kernel_exceeds_step": exceeds,
                          "kernel_timing": {"dispatch": "dispatch-packet timestamps (td_kernel_timing) of every %dth launch "
                                                        "of the timed region (%d samples; warm-up %.2f us per step)" % (
@@ -530,7 +564,14 @@ def main():
                                            "marker": "torch event pairs around every %dth launch of the timed region" % every,
                                            "none": "not timed"}[args.timing],
                          "algorithmic_bytes_per_launch": B * bpe},
+            "per_rank_ms_per_step": [float(c[0]) / K * 1e3 for c in clocks],
+            "per_rank_avg_kernel_us": [float(c[1]) * 1e6 for c in clocks],
+            "closing_barrier_us": [float(c[3]) * 1e6 for c in clocks],
+            "timed_region": "each rank's clock from the opening barrier + synchronize to its own synchronize after "
+                            "its K steps (the closing barrier follows, outside it: closing_barrier_us); value uses "
+                            "the MAX over ranks",
             "board_flags_nonzero": int((flags != 0).sum()),
+            "guard_timeouts_rank0": int(guard_to),
             "board_flags": {name: int(((flags & bit) != 0).sum()) for name, bit in FLAG_BITS if ((flags & bit) != 0).any()},
             "episodes": {"finished": int(per_rank[:, 0].sum()),
                          "mean_return": float(per_rank[:, 1].sum() / max(float(per_rank[:, 0].sum()), 1.0)),

@@ -117,6 +117,9 @@ constexpr uint64_t kChConst = kChAll & ~(kChBin | kChD9 | kChEnemy);
 __device__ __forceinline__ bool take_dry_ring(const StepArgs& a, int b, uint32_t head, int* flags) {
   uint32_t* const slot = a.nxt + ((size_t)b * NSLOT + head % NSLOT) * a.slot_words;
   const uint32_t want = slot_tag(head);
+  // a board whose earlier wait already gave up does not wait again (every later step of a
+  // claim never given back would otherwise stall 1 s): it takes the layout if it is there
+  if (*flags & FLAG_CLAIM_TIMEOUT) return ld_relaxed(slot) == want;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   for (;;) {
     if (ld_relaxed(a.lay_claim + b) == 0u) return ld_relaxed(slot) == want;

@@ -12,11 +12,14 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/tdstep.h"
+#include "../../include/td_diag.h"
 #include "td_kernels.h"
 #include "td_layout.h"
 #include "td_rng.h"
@@ -185,11 +188,20 @@ int check_cfg(const td_config& c) {
 // Device allocations.  The library's own arrays are plain hipMalloc: every state array
 // physically contiguous as well measured slower at most sizes (8,192 boards 35.1 vs 32.5
 // us, 65,536 215.0 vs 210.4, profiles/r04/s25).  Callers' output buffers: td_alloc_device.
-static hipError_t dev_malloc(void** p, size_t bytes, bool contiguous) {
-  if (contiguous && hipExtMallocWithFlags(p, bytes, hipDeviceMallocContiguous) == hipSuccess) return hipSuccess;
+// *granted: whether the block is physically contiguous (a refused request falls back).
+static hipError_t dev_malloc(void** p, size_t bytes, bool contiguous, bool* granted) {
+  *granted = false;
+  if (contiguous && hipExtMallocWithFlags(p, bytes, hipDeviceMallocContiguous) == hipSuccess) {
+    *granted = true;
+    return hipSuccess;
+  }
   (void)hipGetLastError();  // (a refused contiguous request is not the caller's error)
   return hipMalloc(p, bytes);
 }
+
+// Live td_alloc_device blocks and how each was placed (td_alloc_is_contiguous).
+std::mutex g_blocks_mu;
+std::unordered_map<const void*, bool> g_blocks;
 
 template <class T>
 int dalloc(T** p, size_t n) {
@@ -325,7 +337,8 @@ int td_alloc_device(size_t bytes, int device, int contiguous, void** out) {
   int prev = 0;
   HIP_OK(hipGetDevice(&prev));
   HIP_OK(hipSetDevice(device));
-  hipError_t e = dev_malloc(out, bytes, contiguous != 0);
+  bool granted = false;
+  hipError_t e = dev_malloc(out, bytes, contiguous != 0, &granted);
   if (e == hipSuccess) e = hipMemset(*out, 0, bytes);
   if (e == hipSuccess) e = hipDeviceSynchronize();  // zeroed before any stream uses it
   (void)hipSetDevice(prev);  // (the caller's current device is left as it was)
@@ -334,12 +347,25 @@ int td_alloc_device(size_t bytes, int device, int contiguous, void** out) {
     *out = nullptr;
     return fail("td_alloc_device: %s", hipGetErrorString(e));
   }
+  std::lock_guard<std::mutex> g(g_blocks_mu);
+  g_blocks[*out] = granted;
   return 0;
 }
 
 int td_free_device(void* p) {
-  if (p) HIP_OK(hipFree(p));
+  if (!p) return 0;
+  {
+    std::lock_guard<std::mutex> g(g_blocks_mu);
+    g_blocks.erase(p);
+  }
+  HIP_OK(hipFree(p));
   return 0;
+}
+
+int td_alloc_is_contiguous(const void* p) {
+  std::lock_guard<std::mutex> g(g_blocks_mu);
+  auto it = g_blocks.find(p);
+  return it == g_blocks.end() ? -1 : it->second ? 1 : 0;
 }
 
 void td_step_io_init(td_step_io* io) {

@@ -2261,6 +2261,9 @@ __global__ __launch_bounds__(64) void td_refill_kernel(StepArgs a, int guard) {
       const int bb = base + l;
       if (!claim_board(a.lay_claim + bb, lane)) {  // another refill is drawing its layouts
         if (!guard) continue;
+        // a board whose claim wait already gave up is not waited for again (a claim never
+        // given back would stall every guard launch 1 s); it is not counted twice either
+        if (ld_relaxed((const uint32_t*)&a.hdr[bb].flags) & FLAG_CLAIM_TIMEOUT) continue;
         // the holder is a resident side-refill wave that gives the claim back after its
         // walk budget; bounded all the same (1 s, as take_dry_ring): a claim never given
         // back leaves this board's ring short -- its episode end is then flagged

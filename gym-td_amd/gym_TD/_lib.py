@@ -64,6 +64,7 @@ def _load():
         "td_step_io_init": (None, [ctypes.POINTER(TdStepIO)]),
         "td_alloc_device": (ctypes.c_int, [ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
         "td_free_device": (ctypes.c_int, [ctypes.c_void_p]),
+        "td_alloc_is_contiguous": (ctypes.c_int, [ctypes.c_void_p]),
         "td_last_error": (ctypes.c_char_p, []),
         "td_config_default": (None, [ctypes.POINTER(TdConfig)]),
         "td_create": (c_vp, [ctypes.POINTER(TdConfig), ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
@@ -92,15 +93,16 @@ def _load():
         "td_episode_records": (ctypes.c_int, [c_vp, c_vp, c_vp]),
         "td_opponent": (ctypes.c_int, [c_vp, ctypes.c_int, ctypes.c_int, c_u8p, c_vp]),
         "td_set_refill_interval": (ctypes.c_int, [c_vp, ctypes.c_int]),
-        "td_set_step_kernel": (ctypes.c_int, [c_vp, ctypes.c_int]),
         "td_step_kernel": (ctypes.c_int, [c_vp]),
         "td_step_kernel_name": (ctypes.c_char_p, [c_vp]),
         "td_config_epoch": (ctypes.c_int, [c_vp]),
         "td_kernel_timing": (ctypes.c_int, [c_vp, ctypes.c_int, ctypes.c_int]),
         "td_kernel_times": (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_float), ctypes.c_int]),
+        "td_guard_timeouts": (ctypes.c_int, [c_vp, ctypes.c_int]),
+        # test / measurement hooks (include/td_diag.h): not the drop-in surface
+        "td_set_step_kernel": (ctypes.c_int, [c_vp, ctypes.c_int]),
         "td_board_map": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, c_i32p]),
         "td_set_store_policy": (ctypes.c_int, [c_vp, ctypes.c_int, ctypes.c_int]),
-        "td_guard_timeouts": (ctypes.c_int, [c_vp, ctypes.c_int]),
         "td_debug_set_claim": (ctypes.c_int, [c_vp, ctypes.c_int, ctypes.c_int]),
         "td_py_seed": (None, [c_u32p, ctypes.c_uint32]),
         "td_np_seed": (None, [c_u32p, ctypes.c_uint32]),

@@ -95,7 +95,9 @@ def device_zeros(shape, dtype, device, contiguous=None):
         del blk  # (frees the block)
         return torch.zeros(shape, dtype=dtype, device=dev)
     t._td_block = True  # (tests: the block was adopted)
-    t._td_contig = contig  # (requested physically contiguous: TDEngine.obs_alloc)
+    # how the block was placed (a refused contiguous request is a plain allocation):
+    # TDEngine.obs_alloc, by which bench.py keys its PMC traffic records
+    t._td_contig = _lib.lib.td_alloc_is_contiguous(p.value) == 1
     return t
 
 

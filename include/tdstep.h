@@ -127,6 +127,11 @@ int td_step_io_size(void);
  * work that writes it is done). */
 int td_alloc_device(size_t bytes, int device, int contiguous, void** out);
 int td_free_device(void* p);
+/* How td_alloc_device placed block p: 1 physically contiguous, 0 a plain allocation (a
+ * contiguous request the driver refused falls back to one), -1 not a live td_alloc_device
+ * block.  (A placement a caller records -- e.g. to key a measurement by it -- is this one,
+ * not the request.) */
+int td_alloc_is_contiguous(const void* p);
 /* Zero *io and set its size / abi words (a C caller's initialiser; writes td_step_io_size()
  * bytes, so io must be this header's td_step_io). */
 void td_step_io_init(td_step_io* io);
@@ -206,12 +211,11 @@ int td_step(td_handle* h, const td_step_io* io, void* stream);
  *                    L = 30 (single-action) and 8 rounds for TD-2p multi-action at L = 20 --
  *                    else LARGE (L = 10 / 20 / 30; other L only have LARGE).
  * The small kernels need a 16-B-aligned observation buffer; a td_step with any other
- * buffer runs LARGE.  td_set_step_kernel fails (and changes nothing) for a small kernel
- * at an L without one.  td_step_kernel returns the resolved kind, td_step_kernel_name the
+ * buffer runs LARGE.  (Forcing a kind is a test hook: td_set_step_kernel, td_diag.h.)
+ * td_step_kernel returns the resolved kind, td_step_kernel_name the
  * kernel's name as rocprofv3 shows it ("td_step_kernel_small<10, 0, false>": L, mode,
  * multi-action scan). */
 enum td_step_kernel_kind { TD_KERNEL_AUTO = 0, TD_KERNEL_LARGE = 1, TD_KERNEL_SMALL = 2, TD_KERNEL_SMALL2 = 3 };
-int td_set_step_kernel(td_handle* h, int kind);
 int td_step_kernel(td_handle* h);
 const char* td_step_kernel_name(td_handle* h);
 
@@ -279,29 +283,10 @@ int td_export_state(td_handle* h, int b0, int count, void* host_dst);
 int td_import_state(td_handle* h, int b0, int count, const void* host_src);
 int td_get_flags(td_handle* h, int32_t* host_flags);
 
-/* The board each step-kernel block steps (diagnostic; no GPU needed): out[i] for blocks
- * i in [0, n_boards): the XCD-contiguous map of every step kernel (block i runs on XCD
- * i % 8 and steps the (i / 8)-th board of that XCD's contiguous range).  kind 0 and 1 give
- * the same map (kind 1 named the small kernels' board-order lists, removed in round 5).
- * xcd_map = 0: block i = board i. */
-int td_board_map(int n_boards, int kind, int xcd_map, int32_t* out);
-
-/* How the step kernels place boards and store the two observation lines a board shares
- * with its neighbours (18,000 B per board at 10x10 is not a multiple of 128):
- *   xcd_map 1 (default): the XCD-contiguous board map (td_board_map kind 0); 0: block i = board i;
- *   edge_wt 2 (default): plain write-back stores, merged in the XCD's L2; 1: write-through.
- * Results are the same bytes for every policy (tests/test_gpu_store_policy.py); the defaults
- * are the fastest measured.  Synchronises the device. */
-int td_set_store_policy(td_handle* h, int xcd_map, int edge_wt);
-
 /* Ring-guard waits for a board's refill claim that gave up after 1 s (a claim never given
  * back): the board is flagged TD_FLAG_CLAIM_TIMEOUT and its ring may run short.  Returns the
  * count since the last clear (clear != 0 zeroes it).  Synchronous. */
 int td_guard_timeouts(td_handle* h, int clear);
-
-/* Diagnostic (tests): hold (held = 1) or give back (0) board b's refill claim, as a refill
- * wave drawing its layouts holds it.  Synchronises the device. */
-int td_debug_set_claim(td_handle* h, int board, int held);
 
 /* Host-side RNG helpers (exposed for tests and for seeding from Python states). */
 void td_py_seed(uint32_t* mt625, uint32_t seed);

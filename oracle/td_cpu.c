@@ -140,7 +140,7 @@ typedef struct {
   int n_tw;
   double cost_def, cost_atk, progress;
   int base_LP, steps, fail_code;
-  float elp[4][4][MAXL][MAXL];
+  float elp[4 * 4 * MAXL * MAXL];  /* [4][4][L][L], dense at the board's L (ELP) */
   int attacker_cd, defender_cd;
   int overflow;
 } Env;
@@ -152,6 +152,9 @@ typedef struct {
   int L, err;
   uint8_t field[MAXL][MAXL], rot[MAXL][MAXL];
 } Gen;
+
+#define ELP(e, k, t, r, c) ((e)->elp[((((k) * 4 + (t)) * (e)->L + (r)) * (e)->L) + (c)])
+#define ELP_BYTES(e) ((size_t)16 * (e)->L * (e)->L * sizeof(float))
 
 static int g_inner(const Gen* g, int r, int c) { return r > 0 && r < g->L - 1 && c > 0 && c < g->L - 1; }
 static const int STEP[4][2] = {{1, 0}, {0, -1}, {-1, 0}, {0, 1}};  /* :15 */
@@ -348,7 +351,7 @@ static void board_init(Env* e, const Road* roads, int nr) {
   e->steps = 0;
   e->progress = 0.0;
   e->fail_code = FC_OK;
-  memset(e->elp, 0, sizeof e->elp);
+  memset(e->elp, 0, ELP_BYTES(e));
 }
 
 /* TDGymBasic.reset (:37-55): 0 or the road error (the board is left unchanged) */
@@ -388,7 +391,7 @@ static void get_states(const Env* e, float* s) {
       S(14, r, cc) = e->map[6][r][cc] == 0 ? 1.0f : 0.0f;
       for (int t = 0; t < 4; ++t) {
         S(21 + t, r, cc) = v21[t];
-        for (int k = 0; k < 4; ++k) S(25 + 4 * k + t, r, cc) = e->elp[k][t][r][cc];
+        for (int k = 0; k < 4; ++k) S(25 + 4 * k + t, r, cc) = ELP(e, k, t, r, cc);
         S(41 + t, r, cc) = v41[t];
       }
     }
@@ -591,28 +594,28 @@ static double board_step(Env* e) {
   e->cost_atk = e->cost_atk + rate < c->max_cost ? e->cost_atk + rate : c->max_cost;
   e->cost_def = e->cost_def + c->defender_cost_rate < c->max_cost ? e->cost_def + c->defender_cost_rate : c->max_cost;
   /* enemy_LP planes (:355-365), numpy-2 float32: min / max / sequential sum / count */
-  memset(e->elp, 0, sizeof e->elp);
+  memset(e->elp, 0, ELP_BYTES(e));
   const int L = e->L;
   for (int t = 0; t < 4; ++t)
     for (int r = 0; r < L; ++r)
-      for (int cc = 0; cc < L; ++cc) e->elp[0][t][r][cc] = 1.0f;
+      for (int cc = 0; cc < L; ++cc) ELP(e, 0, t, r, cc) = 1.0f;
   for (int i = 0; i < e->n_en; ++i) {
     const Enemy* en = &e->en[i];
     const float r = (float)(en->LP / en->maxLP);
-    float* mn = &e->elp[0][en->type][en->r][en->c];
-    float* mx = &e->elp[1][en->type][en->r][en->c];
+    float* mn = &ELP(e, 0, en->type, en->r, en->c);
+    float* mx = &ELP(e, 1, en->type, en->r, en->c);
     if (r < *mn) *mn = r;
     if (r > *mx) *mx = r;
-    e->elp[2][en->type][en->r][en->c] += r;
-    e->elp[3][en->type][en->r][en->c] += 1.0f;
+    ELP(e, 2, en->type, en->r, en->c) += r;
+    ELP(e, 3, en->type, en->r, en->c) += 1.0f;
   }
   for (int t = 0; t < 4; ++t)
     for (int r = 0; r < L; ++r)
       for (int cc = 0; cc < L; ++cc) {
-        const float n = e->elp[3][t][r][cc];
-        if (!(n > 0)) { e->elp[0][t][r][cc] = 0.0f; e->elp[2][t][r][cc] = 0.0f; }
-        else e->elp[2][t][r][cc] = e->elp[2][t][r][cc] / n;
-        e->elp[3][t][r][cc] = n / (float)MAX_CLUSTER;
+        const float n = ELP(e, 3, t, r, cc);
+        if (!(n > 0)) { ELP(e, 0, t, r, cc) = 0.0f; ELP(e, 2, t, r, cc) = 0.0f; }
+        else ELP(e, 2, t, r, cc) = ELP(e, 2, t, r, cc) / n;
+        ELP(e, 3, t, r, cc) = n / (float)MAX_CLUSTER;
       }
   return reward;
 }
@@ -892,4 +895,152 @@ long long tdc_bench(int L, int mode, int multi, int n_envs, double seconds, int 
   }
   if (wall) *wall = t_max;
   return total;
+}
+
+/* ------------------------------------------------------------------ batched checker
+ * n independent envs stepped together on OpenMP threads, as the device steps a batch: the
+ * every-board steady-state parity test (tests/test_gpu_steady.py) runs bench.py's burn-in
+ * recipe on the device and here side by side.  Resets follow the device's auto-reset
+ * semantics: the next layout draw that succeeds (TDGymBasic.reset, TDGymBasic.py:37-55;
+ * failing draws -- where the reference raises, TDRoadGen.py:177-189 -- skipped, at most
+ * LAYOUT_RETRIES + 1 draws; a board with none keeps its state and is flagged). */
+#define LAYOUT_RETRIES 64
+typedef struct {
+  int n, L, mode, multi, threads;
+  Env** envs;
+  int* no_layout;
+} Batch;
+
+static int reset_skipping(Env* e) {
+  for (int k = 0; k <= LAYOUT_RETRIES; ++k)
+    if (env_reset(e) == 0) return 0;
+  return 1;
+}
+
+static void set_threads(int threads) {
+#ifdef _OPENMP
+  if (threads > 0) omp_set_num_threads(threads);
+#else
+  (void)threads;
+#endif
+}
+
+/* status[b]: 0, or 1 when no initial draw of board b succeeded.  Returns NULL on a bad
+ * argument or an allocation failure. */
+void* tdc_batch_new(int n, int L, int mode, int difficulty, int multi, const uint32_t* np_seeds,
+                    const uint32_t* py_seeds, const double* cfg, int road_attempts, int threads, int* status) {
+  if (n < 1 || L < 4 || L > MAXL) return NULL;
+  Batch* bt = (Batch*)calloc(1, sizeof(Batch));
+  if (!bt) return NULL;
+  bt->n = n; bt->L = L; bt->mode = mode; bt->multi = multi; bt->threads = threads;
+  bt->envs = (Env**)calloc((size_t)n, sizeof(Env*));
+  bt->no_layout = (int*)calloc((size_t)n, sizeof(int));
+  if (!bt->envs || !bt->no_layout) { free(bt->envs); free(bt->no_layout); free(bt); return NULL; }
+  int oom = 0;
+  set_threads(threads);
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 64) reduction(| : oom)
+#endif
+  for (int b = 0; b < n; ++b) {
+    int st = 0;
+    Env* e = (Env*)tdc_new(L, mode, difficulty, multi, np_seeds[b], py_seeds[b], cfg, road_attempts, &st);
+    if (!e) { oom = 1; continue; }
+    if (st) st = reset_skipping(e);  /* the first draw failed: the next ones from the same stream */
+    bt->envs[b] = e;
+    bt->no_layout[b] = st != 0;
+    if (status) status[b] = st != 0;
+  }
+  if (oom) {
+    for (int b = 0; b < n; ++b) free(bt->envs[b]);
+    free(bt->envs); free(bt->no_layout); free(bt);
+    return NULL;
+  }
+  return bt;
+}
+
+void tdc_batch_free(void* p) {
+  Batch* bt = (Batch*)p;
+  if (!bt) return;
+  for (int b = 0; b < bt->n; ++b) free(bt->envs[b]);
+  free(bt->envs); free(bt->no_layout); free(bt);
+}
+
+/* Explicit reset of the boards with mask[b] != 0 (next succeeding draw).  Returns the
+ * number of masked boards that found no layout (they keep their state). */
+int tdc_batch_reset(void* p, const uint8_t* mask) {
+  Batch* bt = (Batch*)p;
+  int missed = 0;
+  set_threads(bt->threads);
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 64) reduction(+ : missed)
+#endif
+  for (int b = 0; b < bt->n; ++b) {
+    if (mask && !mask[b]) continue;
+    if (reset_skipping(bt->envs[b])) { bt->no_layout[b] = 1; ++missed; }
+  }
+  return missed;
+}
+
+/* One step of every board that has a layout.  def_act int64 [n] (discrete) or [n][6][L][L]
+ * (multi-action), atk_act int64 [n][3][8] (NULL in TD-def), reward f64 [n], done u8 [n],
+ * obs f32 [n][45][L][L] or NULL (not built: faster burn-in).  autoreset != 0: a board that
+ * finishes starts its next episode and obs holds that episode's first observation.
+ * Boards without a layout are not stepped (reward 0, done 0, obs zeros).  Returns the
+ * number of boards that finished. */
+int tdc_batch_step(void* p, const int64_t* def_act, const int64_t* atk_act, double* reward, uint8_t* done,
+                   float* obs, int autoreset) {
+  Batch* bt = (Batch*)p;
+  const int L = bt->L;
+  const size_t nd = bt->multi ? (size_t)6 * L * L : 1, no = (size_t)NCH * L * L;
+  int finished = 0;
+  set_threads(bt->threads);
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 64) reduction(+ : finished)
+#endif
+  for (int b = 0; b < bt->n; ++b) {
+    Env* e = bt->envs[b];
+    float* ob = obs ? obs + no * (size_t)b : NULL;
+    if (bt->no_layout[b]) {
+      reward[b] = 0.0;
+      done[b] = 0;
+      if (ob) memset(ob, 0, no * sizeof(float));
+      continue;
+    }
+    static const int64_t empty_atk[24] = {4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4};
+    const int64_t* da = def_act ? def_act + nd * (size_t)b : NULL;
+    const int64_t* aa = atk_act ? atk_act + (size_t)24 * b : empty_atk;
+    int64_t idle = 6 * L * L;
+    int d = 0;
+    reward[b] = env_step(e, da ? da : &idle, aa, &d);
+    done[b] = (uint8_t)d;
+    if (d) {
+      ++finished;
+      if (autoreset && reset_skipping(e)) bt->no_layout[b] = 1;
+    }
+    if (ob) get_states(e, ob);
+  }
+  return finished;
+}
+
+/* Every board's observation (f32 [n][45][L][L]). */
+void tdc_batch_obs(void* p, float* obs) {
+  Batch* bt = (Batch*)p;
+  const size_t no = (size_t)NCH * bt->L * bt->L;
+  set_threads(bt->threads);
+#ifdef _OPENMP
+#pragma omp parallel for schedule(static)
+#endif
+  for (int b = 0; b < bt->n; ++b) get_states(bt->envs[b], obs + no * (size_t)b);
+}
+
+/* no_layout flags (int32 [n]): 1 where a reset found no layout. */
+void tdc_batch_flags(void* p, int32_t* out) {
+  Batch* bt = (Batch*)p;
+  for (int b = 0; b < bt->n; ++b) out[b] = bt->no_layout[b];
+}
+
+/* canon.state_bytes of board b (tdc_state_bytes). */
+int tdc_batch_state_bytes(void* p, int b, uint8_t* out, int cap) {
+  Batch* bt = (Batch*)p;
+  return tdc_state_bytes(bt->envs[b], out, cap);
 }

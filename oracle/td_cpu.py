@@ -50,6 +50,18 @@ def lib():
         L.tdc_bench.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_double,
                                 ctypes.c_int, ctypes.c_uint32, f64p, ctypes.POINTER(ctypes.c_double)]
         L.tdc_bench.restype = ctypes.c_longlong
+        L.tdc_batch_new.restype = vp
+        L.tdc_batch_new.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, vp,
+                                    f64p, ctypes.c_int, ctypes.c_int, vp]
+        L.tdc_batch_free.argtypes = [vp]
+        L.tdc_batch_reset.argtypes = [vp, vp]
+        L.tdc_batch_reset.restype = ctypes.c_int
+        L.tdc_batch_step.argtypes = [vp, vp, vp, vp, vp, vp, ctypes.c_int]
+        L.tdc_batch_step.restype = ctypes.c_int
+        L.tdc_batch_obs.argtypes = [vp, vp]
+        L.tdc_batch_flags.argtypes = [vp, vp]
+        L.tdc_batch_state_bytes.argtypes = [vp, ctypes.c_int, vp, ctypes.c_int]
+        L.tdc_batch_state_bytes.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -149,3 +161,75 @@ def bench(L, mode, multi, n_envs, seconds, threads, seed=90001, cfg=None):
     n = lib().tdc_bench(int(L), MODES[mode], int(bool(multi)), int(n_envs), float(seconds), int(threads),
                         int(seed), c.ctypes.data, ctypes.byref(wall))
     return int(n), float(wall.value)
+
+
+class Batch(object):
+    """n envs of the C restatement stepped together on OpenMP threads (tdc_batch_*): the
+    every-board checker of a device batch.  Every reset -- the initial one, explicit ones
+    (``reset(mask)``) and auto-resets -- takes the board's next layout draw that succeeds
+    (failing draws skipped, as the device's staged layouts are); a board with none keeps
+    its state and is flagged (``no_layout``)."""
+
+    def __init__(self, L, n, mode="def", difficulty=1, np_seeds=None, py_seeds=None, cfg=None, multi=False,
+                 road_attempts=1000, threads=None):
+        from oracle.td_oracle import Config
+        self.L, self.n, self.mode, self.multi = int(L), int(n), mode, bool(multi)
+        self._cfg = cfg_values(cfg or Config())
+        nps = np.ascontiguousarray(np.asarray(np_seeds, dtype=np.int64) & 0xFFFFFFFF, dtype=np.uint32)
+        pys = np.ascontiguousarray(np.asarray(py_seeds if py_seeds is not None else np_seeds, dtype=np.int64)
+                                   & 0xFFFFFFFF, dtype=np.uint32)
+        assert nps.size == self.n and pys.size == self.n
+        self.threads = int(threads or min(16, os.cpu_count() or 1))
+        st = np.zeros(self.n, dtype=np.int32)
+        self._h = lib().tdc_batch_new(self.n, self.L, MODES[mode], int(difficulty), int(self.multi), nps.ctypes.data,
+                                      pys.ctypes.data, self._cfg.ctypes.data, int(road_attempts), self.threads,
+                                      st.ctypes.data)
+        if not self._h:
+            raise MemoryError("tdc_batch_new failed (%d envs)" % self.n)
+        self.initial_failed = np.flatnonzero(st).tolist()
+        self.reward = np.zeros(self.n, dtype=np.float64)
+        self.done = np.zeros(self.n, dtype=np.uint8)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().tdc_batch_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+    def reset(self, mask=None):
+        """Explicit reset of the masked boards (None = all); returns how many found no layout."""
+        m = None if mask is None else np.ascontiguousarray(np.asarray(mask).reshape(self.n), dtype=np.uint8)
+        return lib().tdc_batch_reset(self._h, None if m is None else m.ctypes.data)
+
+    def step(self, def_act=None, atk_act=None, obs=None, autoreset=True):
+        """One step of every board; ``obs`` (float32 [n, 45, L, L]) is filled when given.
+        Returns (reward, done) -- arrays owned by this object, overwritten by the next step."""
+        d = None if def_act is None else np.ascontiguousarray(def_act, dtype=np.int64)
+        a = None if atk_act is None else np.ascontiguousarray(atk_act, dtype=np.int64)
+        if obs is not None:
+            assert obs.dtype == np.float32 and obs.flags.c_contiguous and obs.size == self.n * 45 * self.L * self.L
+        lib().tdc_batch_step(self._h, None if d is None else d.ctypes.data, None if a is None else a.ctypes.data,
+                             self.reward.ctypes.data, self.done.ctypes.data,
+                             None if obs is None else obs.ctypes.data, int(bool(autoreset)))
+        return self.reward, self.done
+
+    def obs(self, out=None):
+        out = np.empty((self.n, 45, self.L, self.L), dtype=np.float32) if out is None else out
+        lib().tdc_batch_obs(self._h, out.ctypes.data)
+        return out
+
+    def no_layout(self):
+        f = np.zeros(self.n, dtype=np.int32)
+        lib().tdc_batch_flags(self._h, f.ctypes.data)
+        return f.astype(bool)
+
+    def state_bytes(self, b):
+        n = lib().tdc_batch_state_bytes(self._h, int(b), None, 0)
+        buf = np.zeros(n, dtype=np.uint8)
+        lib().tdc_batch_state_bytes(self._h, int(b), buf.ctypes.data, n)
+        return buf.tobytes()

@@ -582,7 +582,8 @@ class Board(object):
             elp[(2,) + i] += r
             elp[(3,) + i] += 1
         elp[0] = np.where(elp[3] > 0, elp[0], np.zeros_like(elp[0]))
-        elp[2] = np.where(elp[3] > 0, elp[2] / elp[3], np.zeros_like(elp[2]))
+        with np.errstate(invalid="ignore", divide="ignore"):  # 0/0 cells are masked by the where
+            elp[2] = np.where(elp[3] > 0, elp[2] / elp[3], np.zeros_like(elp[2]))
         elp[3] /= self.hp.max_cluster_length
         return reward
 

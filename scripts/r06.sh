@@ -1,0 +1,26 @@
+#!/bin/bash
+# Round-6 GPU sessions: bash scripts/r06.sh <session>.  Every GPU step runs under its own
+# time limit; the session stops at the first crash / timeout (pytest's 1 = failures is
+# reported and the session goes on only where noted).
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+export TMPDIR=/tmp
+S=$1
+O=gpurun_out/r06_$S
+mkdir -p $O
+run() { local name=$1 secs=$2; shift 2; echo "== $name $(date +%T)"; timeout -k 10 "$secs" "$@" > "$O/$name.log" 2>&1; local rc=$?; echo "== $name rc=$rc"; [ $rc -ne 0 ] && tail -25 "$O/$name.log"; return $rc; }
+line() { grep -h '^{' "$O/$1.log" | python3 -c "import json,sys
+for l in sys.stdin: d=json.loads(l); r=d['roofline']; print('   %-18s' % '$1', round(d['value']/1e6,1), 'M/s  step', round(d['ms_per_step']*1e3,2), 'us  kernel', r['avg_kernel_us'] and round(r['avg_kernel_us'],2), 'frac', r['frac'] and round(r['frac'],3), r['kernel'], 'n', r['kernel_samples'], 'B/gpu', d['config']['boards_per_gpu'], 'flags', d.get('board_flags'), 'eps', d['episodes']['finished'], 'ranks_us', [round(x*1e3,2) for x in d.get('per_rank_ms_per_step', [])], 'barrier_us', [round(x,1) for x in d.get('closing_barrier_us', [])])"; }
+gpusuite() { run pytest_gpu ${1:-900} python -u -m pytest tests -m gpu -q --timeout 400 --timeout-method thread -p no:cacheprovider ${2}; local rc=$?; grep -E "^(FAILED|E  )" $O/pytest_gpu.log | head -30; tail -1 $O/pytest_gpu.log; return $rc; }
+case $S in
+s1)  # round 6 first build: new steady-state test + claims, GPU suite, smoke, the driver's command, N>1 rehearsal on one GPU
+  run pytest_new 600 python -u -m pytest tests/test_gpu_steady.py tests/test_gpu_claims.py tests/test_gpu_rccl.py -m gpu -v -x --timeout 400 --timeout-method thread -p no:cacheprovider
+  rc=$?; grep -E "^(FAILED|E  )|PASSED|passed|failed" $O/pytest_new.log | head -30; [ $rc -le 1 ] || exit $rc
+  gpusuite 1000; rc=$?; [ $rc -le 1 ] || exit $rc
+  run smoke 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" || exit 1
+  run bench_driver 300 python bench.py --gpus 1 --steps 20 --warmup 5 || exit 1; line bench_driver
+  grep -h '^{' $O/bench_driver.log | cut -c1-3000
+  TD_BENCH_DIST_BACKEND=gloo TD_BENCH_SAME_DEVICE=1 run n8 400 python bench.py --gpus 8 --steps 20 --warmup 5 || exit 1; line n8
+  TD_BENCH_DIST_BACKEND=gloo TD_BENCH_SAME_DEVICE=1 run n2 300 python bench.py --gpus 2 --steps 20 --warmup 5 || exit 1; line n2
+  ;;
+*) echo "unknown session $S"; exit 2 ;;
+esac

@@ -89,17 +89,66 @@ def test_gpus_n_starts_n_ranks(monkeypatch):
 
 def test_sampling_stride_follows_the_step_time():
     # the kernel is sampled inside the timed region; the stride keeps the events' cost
-    # (EVENT_COST_US per sampled launch) under EVENT_PERTURB of the step, with >= 2 samples
-    assert bench.event_every(20, 210.0) == 2  # the driver's line: 10 samples
-    assert bench.event_every(20, 33.0) == 10  # 8,192 boards: capped at half the timed steps
+    # (EVENT_COST_US per sampled launch) under EVENT_PERTURB of the step, with >= 2 launches
+    # between samples, but never fewer than MIN_SAMPLES samples per rank
+    assert bench.event_every(20, 204.0) == 2  # the driver's line: 10 samples
+    assert bench.event_every(20, 33.0) == 5  # 8,192 boards (the N = 8 share): 4 samples per rank
     assert bench.event_every(2000, 33.0) == 10
     assert bench.event_every(2000, 21.0) == 15
-    assert bench.event_every(1, 210.0) == 2  # one timed step: one sample
-    assert bench.event_every(20, None) == bench.EVENT_EVERY  # --warmup 0
+    assert bench.event_every(1, 210.0) == 1  # one timed step: one sample
+    assert bench.event_every(20, None) == 5  # --warmup 0: EVENT_EVERY within the cap
+    assert bench.event_every(200, None) == bench.EVENT_EVERY
     assert bench.event_every(20, 210.0, override=1) == 1
-    for steps, us in ((20, 210.0), (300, 497.0), (2000, 21.0), (200, 300.0)):
+    for steps, us in ((20, 210.0), (20, 32.4), (300, 497.0), (2000, 21.0), (200, 300.0), (7, 18.0)):
         k = bench.event_every(steps, us)
-        assert bench.EVENT_COST_US / (k * us) <= bench.EVENT_PERTURB or k == (steps + 1) // 2
+        cap = max(1, steps // bench.MIN_SAMPLES)
+        assert bench.EVENT_COST_US / (k * us) <= bench.EVENT_PERTURB or k == cap
+        assert (steps + k - 1) // k >= min(steps, bench.MIN_SAMPLES)
+
+
+class _Clock(object):
+    """A fake clock that the stubbed steps / barrier advance by known amounts."""
+
+    def __init__(self):
+        self.t = 100.0
+
+    def __call__(self):
+        return self.t
+
+
+def test_timed_region_excludes_the_closing_barrier():
+    """The rank's elapsed time ends at its own synchronize after its steps: a closing barrier
+    of known delay (a rank that waits for a slower one) is not in it, and is reported on its
+    own; the opening barrier precedes the clock."""
+    clk, calls = _Clock(), []
+
+    def run():
+        calls.append("run")
+        clk.t += 0.004  # the K steps: 4 ms
+
+    def sync():
+        calls.append("sync")
+
+    def barrier():
+        calls.append("barrier")
+        clk.t += 0.0025  # 2.5 ms waiting for the other ranks
+
+    elapsed, barrier_s = bench.timed_region(run, sync, barrier, clock=clk)
+    assert elapsed == pytest.approx(0.004, abs=1e-12)
+    assert barrier_s == pytest.approx(0.0025, abs=1e-12)
+    assert calls == ["sync", "barrier", "sync", "run", "sync", "barrier", "sync"]
+    # world of one: no barrier at all, the same clock
+    calls.clear()
+    elapsed, barrier_s = bench.timed_region(run, sync, None, clock=clk)
+    assert (round(elapsed, 12), barrier_s) == (0.004, 0.0)
+    assert calls == ["sync", "sync", "run", "sync"]
+
+
+def test_timed_region_real_clock_with_a_slow_barrier():
+    """The same with the real clock and a sleeping barrier (20 ms) around 5-ms steps."""
+    import time
+    elapsed, barrier_s = bench.timed_region(lambda: time.sleep(0.005), lambda: None, lambda: time.sleep(0.02))
+    assert 0.005 <= elapsed < 0.019 and barrier_s >= 0.02
 
 
 def test_kernel_longer_than_the_step_withholds_the_fraction():

@@ -103,3 +103,61 @@ def test_cpu_matches_python_oracle(L, mode, multi, difficulty):
 def test_cpu_bench_runs():
     steps, wall = C.bench(10, "def", False, n_envs=8, seconds=0.2, threads=2)
     assert steps > 0 and wall >= 0.2
+
+
+def _skip_reset(env):
+    """The next layout draw that succeeds (the device's staged layouts skip failing draws)."""
+    for _ in range(65):
+        try:
+            return env.reset()
+        except C.RoadGenError:
+            pass
+    raise AssertionError("no layout")
+
+
+@pytest.mark.parametrize("L,mode,multi,n,steps,period", [(10, "def", False, 40, 260, 37), (20, "2p", True, 12, 150, 9),
+                                                          (10, "atk", False, 16, 120, 25)])
+def test_batch_matches_single_envs(L, mode, multi, n, steps, period):
+    """tdc_batch_* (the every-board checker of tests/test_gpu_steady.py) against one C env
+    per board stepped alone: bench.py's staggered explicit resets (bench.stagger_mask with a
+    short period), auto-reset, 1-LP bases so episodes end within the run; reward bits, done
+    and every observation byte of every board at every step, the state at the end."""
+    import bench
+    cfg = O.Config(base_LP=1)
+    seeds, envs, s = [], [], 400 + 7 * L
+    while len(envs) < n:  # boards whose first draw succeeds (C.Env raises on a failing one)
+        try:
+            envs.append(C.Env(L, mode, 1, s, s, cfg, multi=multi))
+            seeds.append(s)
+        except C.RoadGenError:
+            pass
+        s += 1
+    bt = C.Batch(L, n, mode, 1, seeds, seeds, cfg, multi=multi, threads=4)
+    assert bt.initial_failed == []
+    rng = np.random.RandomState(3)
+    obs = np.zeros((n, 45, L, L), np.float32)
+    ends = 0
+    assert np.array_equal(bt.obs(), np.stack([e.obs() for e in envs]))
+    for k in range(steps):
+        m = bench.stagger_mask(k, np.arange(n), period)
+        if m is not None:
+            assert bt.reset(m) == 0
+            for b in np.flatnonzero(m):
+                _skip_reset(envs[b])
+        d = (rng.randint(0, 3, size=(n, 6, L, L)) if multi else rng.randint(0, 6 * L * L + 1, size=n)) \
+            if mode != "atk" else None
+        a = rng.randint(0, 5, size=(n, 3, 8)) if mode != "def" else None
+        rw, dn = bt.step(d, a, obs)
+        for b, e in enumerate(envs):
+            wo, wr, wd = e.step(None if d is None else d[b], None if a is None else a[b])
+            assert canon.fhex(rw[b]) == canon.fhex(wr) and bool(dn[b]) == wd, (k, b)
+            if wd:
+                wo = _skip_reset(e)
+                ends += 1
+            assert np.array_equal(obs[b], wo), (k, b)
+    for b, e in enumerate(envs):
+        assert bt.state_bytes(b) == e.state_bytes(), b
+        e.close()
+    assert not bt.no_layout().any()
+    assert ends > 0
+    bt.close()

@@ -45,6 +45,17 @@ def test_claim_held_past_the_wait_is_flagged_not_stepped():
         assert (others == 0).all(), others[others != 0]
         st = eng.board_state(HELD)
         assert st["steps"] == ended + 1 and st["base_LP"] == 0  # the finished episode, not a new one
+        # the claim still held: neither the step (take_dry_ring) nor the guard waits for the
+        # flagged board again -- 30 more steps (two guard launches) take far less than one 1-s wait
+        import time
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(30):
+            eng.step(def_act=torch.full((B,), 6 * L * L, device="cuda", dtype=torch.int64))
+        torch.cuda.synchronize()
+        assert time.perf_counter() - t0 < 0.5, time.perf_counter() - t0
+        assert eng.board_state(HELD)["steps"] == ended + 1  # still its finished episode
+        assert eng.guard_timeouts() == 1  # counted once, not at every guard launch
         # give the claim back: the next ring guard draws the layout, the board starts over
         _lib.check(_lib.lib.td_debug_set_claim(eng._h, HELD, 0))
         for k in range(16):

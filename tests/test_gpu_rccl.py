@@ -50,9 +50,9 @@ for k in range(200):
 torch.cuda.synchronize()
 stats = eng.episode_stats(clear=False)
 recs = eng.episode_records()
-(el, ak, ss), per_rank, got = bench.collect(1.5, 2.5e-4, 3.5e-4, stats, recs, coll)
+(el, ak, ss), per_rank, got, clocks = bench.collect(1.5, 2.5e-4, 3.5e-4, stats, recs, coll, 4.5e-5)
 want = [r.cpu() for r in recs]
-out = dict(clocks=[el, ak, ss], per_rank=per_rank.cpu().numpy().tolist(), stats=stats.cpu().numpy().tolist(),
+out = dict(clocks=[el, ak, ss], rank_clocks=clocks.tolist(), per_rank=per_rank.cpu().numpy().tolist(), stats=stats.cpu().numpy().tolist(),
            recs_equal=all(torch.equal(a.cpu(), b) for a, b in zip(got, want)),
            per_rank_device=str(per_rank.device), finished=int(stats[0].item()),
            with_record=int((want[2] >= 0).sum()))
@@ -78,6 +78,7 @@ def test_nccl_world_of_one_runs_bench_collectives():
     import json
     r = json.loads(line[len("RESULT "):])
     assert r["clocks"] == [1.5, 2.5e-4, 3.5e-4]  # MAX over one rank: the values themselves
+    assert r["rank_clocks"] == [[1.5, 2.5e-4, 3.5e-4, 4.5e-5]]  # each rank's own clocks, gathered
     assert r["per_rank"] == [r["stats"]]  # gathered to rank 0 over RCCL, bit for bit
     assert r["per_rank_device"].startswith("cuda")
     assert r["recs_equal"]  # the per-board 16-B payload, gathered over RCCL

@@ -22,12 +22,29 @@ def _p(a):
     return _lib.ptr(a, U32)
 
 
-def test_header_symbols_exported():
-    hdr = open(G.GOLDEN + "/../../include/tdstep.h").read()
+DIAG = {"td_set_step_kernel", "td_board_map", "td_set_store_policy", "td_debug_set_claim"}
+
+
+@pytest.mark.parametrize("header", ["tdstep.h", "td_diag.h"])
+def test_header_symbols_exported(header):
+    """Every function include/*.h declares is exported by libtdstep.so; the test hooks are
+    declared only in td_diag.h, never in the drop-in header."""
+    hdr = open(G.GOLDEN + "/../../include/" + header).read()
     names = set(re.findall(r"\b(td_[a-z_0-9]+)\s*\(", hdr))
-    assert len(names) >= 25
+    assert len(names) >= (25 if header == "tdstep.h" else 4)
     for n in sorted(names):
         assert hasattr(lib, n), n
+    if header == "tdstep.h":
+        assert not (names & DIAG), names & DIAG
+    else:
+        assert names == DIAG, names
+
+
+def test_alloc_placement_of_unknown_block():
+    """td_alloc_is_contiguous answers -1 for memory td_alloc_device did not hand out."""
+    buf = np.zeros(16, np.uint8)
+    assert lib.td_alloc_is_contiguous(buf.ctypes.data) == -1
+    assert lib.td_alloc_is_contiguous(None) == -1
 
 
 def test_config_default_matches_reference_defaults():

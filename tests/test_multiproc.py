@@ -113,3 +113,51 @@ def test_gloo_ranks_match_one_process(world, base):
     assert per_rank.shape == (world, 2)
     assert per_rank[:, 0].sum() == float(one[0]) > 0
     assert per_rank[:, 1].sum() == pytest.approx(float(one[1]), rel=1e-12, abs=1e-9)
+
+
+def _timing_worker(rank, world, port, q):
+    """bench.py's timed region and collect() over gloo: rank r's steps take 10 + 40 r ms."""
+    import sys
+    import time
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import bench
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        elapsed, barrier_s = bench.timed_region(lambda: time.sleep(0.010 + 0.040 * rank), lambda: None, dist.barrier)
+        stats = torch.tensor([float(rank), 2.0 * rank], dtype=torch.float64)
+        recs = (torch.zeros(3, dtype=torch.float64), torch.zeros(3, dtype=torch.int32),
+                torch.full((3,), -1, dtype=torch.int32))
+        (el, ak, ws), per_rank, _, clocks = bench.collect(elapsed, 1e-5 * (rank + 1), 2e-5, stats, recs,
+                                                          torch.device("cpu"), barrier_s)
+        if rank == 0:
+            q.put((el, ak, clocks.tolist(), per_rank.numpy().tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_timed_region_and_per_rank_clocks():
+    """N > 1 timing: each rank's clock ends at its own steps, the fast
+    rank's wait for the slow one shows as its closing barrier, and the reported time is
+    the MAX over ranks -- the slowest rank's steps, not steps + barrier."""
+    world = 2
+    ctx = tmp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_timing_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        el, ak, clocks, per_rank = q.get(timeout=300)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    clocks = np.asarray(clocks)
+    assert clocks.shape == (world, 4)
+    assert 0.010 <= clocks[0, 0] < 0.045  # rank 0: its own 10-ms steps
+    assert 0.050 <= clocks[1, 0] < 0.090  # rank 1: 50 ms
+    assert clocks[0, 3] >= 0.030  # rank 0 waited for rank 1 in the closing barrier, outside its clock
+    assert el == clocks[:, 0].max() and ak == pytest.approx(2e-5)
+    assert per_rank == [[0.0, 0.0], [1.0, 2.0]]
