@@ -54,7 +54,8 @@ def test_claim_held_past_the_wait_is_flagged_not_stepped():
             eng.step(def_act=torch.full((B,), 6 * L * L, device="cuda", dtype=torch.int64))
         torch.cuda.synchronize()
         assert time.perf_counter() - t0 < 0.5, time.perf_counter() - t0
-        assert eng.board_state(HELD)["steps"] == ended + 1  # still its finished episode
+        st = eng.board_state(HELD)  # still its finished episode (stepped on, done at every step)
+        assert st["base_LP"] == 0 and st["steps"] == ended + 31, st
         assert eng.guard_timeouts() == 1  # counted once, not at every guard launch
         # give the claim back: the next ring guard draws the layout, the board starts over
         _lib.check(_lib.lib.td_debug_set_claim(eng._h, HELD, 0))
