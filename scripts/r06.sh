@@ -22,5 +22,12 @@ s1)  # round 6 first build: new steady-state test + claims, GPU suite, smoke, th
   TD_BENCH_DIST_BACKEND=gloo TD_BENCH_SAME_DEVICE=1 run n8 400 python bench.py --gpus 8 --steps 20 --warmup 5 || exit 1; line n8
   TD_BENCH_DIST_BACKEND=gloo TD_BENCH_SAME_DEVICE=1 run n2 300 python bench.py --gpus 2 --steps 20 --warmup 5 || exit 1; line n2
   ;;
+s2)  # placement probe (boards a CU writes at once contiguous?), kernel trace + PMC bytes of the driver's command on this round's sources
+  run obs_place 180 ./scripts/bin/obs_place || exit 1; cat $O/obs_place.log
+  kt() { local name=$1; shift; run kt_$name 300 timeout -s KILL 280 rocprofv3 --kernel-trace --stats -d $O/kt_$name -o kt --output-format csv -- "$@" || return 1; cp $(find $O/kt_$name -name "*kernel_stats.csv") $O/kt_${name}_kernel_stats.csv; rm -rf $O/kt_$name; grep -h td_step_kernel $O/kt_${name}_kernel_stats.csv | cut -c1-160; }
+  kt drv python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline || exit 1
+  OUT=$O/pmc NAME=def-small_65536 WL=def-small B=65536 timeout -k 10 700 bash scripts/pmc_ab.sh || exit 1
+  rm -rf $O/pmc/def-small_65536/FETCH_SIZE $O/pmc/def-small_65536/WRITE_SIZE
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
