@@ -29,5 +29,8 @@ s2)  # placement probe (boards a CU writes at once contiguous?), kernel trace + 
   OUT=$O/pmc NAME=def-small_65536 WL=def-small B=65536 timeout -k 10 700 bash scripts/pmc_ab.sh || exit 1
   rm -rf $O/pmc/def-small_65536/FETCH_SIZE $O/pmc/def-small_65536/WRITE_SIZE
   ;;
+s3)  # cooperative writer probe: the waves of a workgroup write the boards it finished together (no barrier)
+  run coop 240 ./scripts/bin/coop_writer || exit 1; cat $O/coop.log
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
