@@ -32,5 +32,8 @@ s2)  # placement probe (boards a CU writes at once contiguous?), kernel trace + 
 s3)  # cooperative writer probe: the waves of a workgroup write the boards it finished together (no barrier)
   run coop 240 ./scripts/bin/coop_writer || exit 1; cat $O/coop.log
   ;;
+s4)  # the store-shape probe again (does 16 waves per board still stream at 7 TB/s on this box?)
+  run shapes 240 ./scripts/bin/obs_ceiling shapes || exit 1; cat $O/shapes.log
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
