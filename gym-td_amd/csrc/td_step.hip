@@ -71,6 +71,7 @@ struct alignas(16) Smem {
     };
   };
   uint32_t early_go;         // td_step_kernel_small2: the binary-plane windows may be written early
+  int32_t flags0;            // the board's flags as loaded (store_board: is the header's second half dirty?)
   TdDevCfg cfg;           // constant block, staged once per board: per-lane table lookups hit LDS
 };
 
@@ -1324,6 +1325,7 @@ __device__ __forceinline__ void load_board(Smem<NC>& S, U& u, const Ctx& x, cons
   u.num_roads = (int)lane_word(P.w, 12); u.end_cell = (int)lane_word(P.w, 13);
   u.set_starts((int)lane_word(P.w, 14), (int)lane_word(P.w, 15), (int)lane_word(P.w, 16));
   u.maxdist = (int)lane_word(P.w, 17); u.flags = (int)lane_word(P.w, 18); u.episodes = (int)lane_word(P.w, 19);
+  if (x.lane == 0) S.flags0 = u.flags;
   u.max_cost = lane_f64(P.w, 20); u.max_base_LP = (int)lane_word(P.w, 22);
   u.progress = ddiv((double)u.steps, (double)x.C.max_episode_steps);
   u.cells_dirty = false;
@@ -1396,9 +1398,20 @@ __device__ __forceinline__ void store_towers(const Smem<NC>& S, int nt, bool dir
   }
 }
 
+// The header's second half (words 12-23: layout, flags, episodes, the captured max_cost /
+// max_base_LP) changes only at an episode end, a reset or a new flag: a step that did none
+// of these stores the first 48 B only (hdr_hi false; -48 B written per board and step).
 template <int NC>
-__device__ __forceinline__ void store_board(const Smem<NC>& S, const U& u, const Ctx& x, const StepArgs& a, int b) {
-  if (x.lane == 0) a.hdr[b] = hdr_of(u);
+__device__ __forceinline__ void store_board(const Smem<NC>& S, const U& u, const Ctx& x, const StepArgs& a, int b,
+                                            bool hdr_hi = true) {
+  if (x.lane == 0) {
+    static_assert(sizeof(TdHdr) == 6 * 16, "header stored as 6 x 16 B");
+    const TdHdr h = hdr_of(u);
+    const uint4* src = reinterpret_cast<const uint4*>(&h);
+    uint4* dst = reinterpret_cast<uint4*>(a.hdr + b);
+    dst[0] = src[0]; dst[1] = src[1]; dst[2] = src[2];
+    if (hdr_hi) { dst[3] = src[3]; dst[4] = src[4]; dst[5] = src[5]; }
+  }
   // cells were written back by store_cells, enemies at the end of board_step
   store_towers(S, u.nt, u.tw_dirty, x.lane, a, b);
 }
@@ -1418,6 +1431,7 @@ struct alignas(16) StepOut {
   uint32_t go;   // second wave: 0 nothing (a board never reset wrote its own outputs), 1 store and write
                  // half of the late windows, 2 store only (an auto-reset board: the stepping wave writes every window)
   uint32_t any;  // the board has enemies (enemy windows read the group statistics)
+  uint32_t hdr_hi;  // the header's second half changed (store_board): 6 lanes store it, else 3
 };
 
 __device__ __forceinline__ void store_outputs(const StepArgs& a, int b, double reward, double ep_ret, int64_t real_def,
@@ -1844,6 +1858,7 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
       so->ep_steps = ep_steps; so->fail_def = fail_def;
       so->done = done ? 1u : 0u; so->win = (uint32_t)(int32_t)win; so->allow = allow; so->cool = cool;
       so->go = was_reset ? 2u : 1u; so->any = u.n > 0 ? 1u : 0u;
+      so->hdr_hi = (was_reset || done || u.flags != S.flags0) ? 1u : 0u;
     }
     __syncthreads();
     enemy_stats(S, u, x);  // no-op for a board without enemies (e.g. just reset)
@@ -1863,7 +1878,7 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
       store_cells(S, u, x, a, b);
       pack_obs_cells(S, x);
     }
-    store_board(S, u, x, a, b);
+    store_board(S, u, x, a, b, was_reset || done || u.flags != S.flags0);
     store_outputs(a, b, reward, ep_ret, real_def, ep_steps, fail_def, done, win, allow, cool, x.lane);
     // the observation last: nothing of the step is live any more, the writer has the registers
     STAMP(6);
@@ -1966,7 +1981,7 @@ __global__ __launch_bounds__(128) TD_SMALL2_ATTR void td_step_kernel_small2(Step
     if (go) {
       static_assert(sizeof(TdHdr) == 6 * 16 && offsetof(StepOut, hdr) == 0 && alignof(StepOut) >= 16,
                     "header copied as 6 x 16-B LDS reads");
-      if (lane < 6) reinterpret_cast<uint4*>(a.hdr + b)[lane] = reinterpret_cast<const uint4*>(&SO.hdr)[lane];
+      if (lane < (SO.hdr_hi ? 6 : 3)) reinterpret_cast<uint4*>(a.hdr + b)[lane] = reinterpret_cast<const uint4*>(&SO.hdr)[lane];
       store_towers(S, SO.nt, SO.tw_dirty != 0, lane, a, b);
       store_outputs(a, b, SO, lane);
     }

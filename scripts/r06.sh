@@ -35,14 +35,14 @@ s3)  # cooperative writer probe: the waves of a workgroup write the boards it fi
 s4)  # the store-shape probe again (does 16 waves per board still stream at 7 TB/s on this box?)
   run shapes 240 ./scripts/bin/obs_ceiling shapes || exit 1; cat $O/shapes.log
   ;;
-s5)  # 4 prefetched enemy slots in the TD-def small kernels (product lib) vs 16 (libtdstep_base.so): parity, A/B, PMC bytes; store-shape probe
+s5)  # 4 prefetched enemy slots in the TD-def small kernels (pf) + the header's second half stored only when it changed (hh, product lib) vs r06 s1 (base): parity, A/B, PMC bytes; store-shape probe
   run pytest_pf 900 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_steady.py tests/test_gpu_deep.py -m gpu -q -x --timeout 400 --timeout-method thread -p no:cacheprovider
   rc=$?; grep -E "^(FAILED|E  )" $O/pytest_pf.log | head -20; tail -1 $O/pytest_pf.log; [ $rc -eq 0 ] || exit $rc
   for r in 1 2; do
     for spec in 65536:300 8192:2000 4096:2000; do
       bb=${spec%%:*}; st=${spec##*:}
-      for v in base pf; do
-        lib=$PWD/gym-td_amd/lib/libtdstep_$v.so; [ $v = pf ] && lib=$PWD/gym-td_amd/lib/libtdstep.so
+      for v in base pf hh; do
+        lib=$PWD/gym-td_amd/lib/libtdstep_$v.so; [ $v = hh ] && lib=$PWD/gym-td_amd/lib/libtdstep.so
         TDSTEP_LIB=$lib run ${v}_${bb}_$r 300 python bench.py --global-batch $bb --steps $st --no-cpu-baseline --timing none || exit 1; line ${v}_${bb}_$r
       done
     done
