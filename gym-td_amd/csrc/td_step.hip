@@ -1244,13 +1244,9 @@ struct Prefetch {
 // the large-batch kernel (HBM-bound) takes none and loads exactly the live slots once
 // the header's counts are in (one dependent round trip, hidden by the other waves).
 constexpr int PF_ACT = 24, PF_HOT = 26, PF_SMALL = 16, PF_LARGE = 0;
-// Enemy slots the small kernels prefetch in TD-def: the built-in opponent keeps boards
-// short of enemies -- in bench.py's steady state (65,536 boards, staggered episodes) 34 % of
-// the boards hold any, 0.02 % more than 4, none more than 5 (the C restatement, the same
-// recipe) -- so 4 slots cover nearly every board and the 12 more read 240 B per board for
-// nothing.  TD-atk / TD-2p (an acting attacker) keep 16.
-template <int MODE, bool SMALL>
-constexpr int pf_en() { return !SMALL ? PF_LARGE : MODE == MODE_DEF ? 4 : PF_SMALL; }
+// (Four enemy slots instead of 16 in TD-def, where 0.02 % of bench.py's steady-state boards
+// hold more than 4, read the same bytes -- each slot array's first 128-B line is fetched
+// whole either way: PMC 1,534 vs 1,535 B read per board -- in the same time, r06/s5.)
 static_assert(offsetof(TdHdr, steps) == 24 && offsetof(TdHdr, start_cell) == 56 && offsetof(TdHdr, episodes) == 76 &&
                   offsetof(TdHdr, max_cost) == 80 && offsetof(TdHdr, max_base_LP) == 88,
               "Prefetch header word map");
@@ -1661,7 +1657,7 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
   STAMP_RT(9);
   STAMP(0);
   constexpr int PF = SMALL ? PF_SMALL : PF_LARGE;
-  load_board<NC, pf_en<MODE, SMALL>(), PF>(S, u, x, a, b, P);
+  load_board<NC, PF, PF>(S, u, x, a, b, P);
   const int64_t act_in = (int64_t)(((uint64_t)lane_word(P.w, PF_ACT + 1) << 32) | lane_word(P.w, PF_ACT));
   // built-in opponent stream: position, lazy-twist boundary and the next draws
   // (pre-computed by the previous step) come from the board's hot record
@@ -1912,7 +1908,7 @@ __device__ __forceinline__ void step_kernel_body(const StepArgs& a) {
   const Ctx x{S.cfg, L, L * L, (int)(threadIdx.x & 63), a.cfgs, a.epoch};
   Prefetch P;
   constexpr int PF = SMALL ? PF_SMALL : PF_LARGE;
-  prefetch_issue<pf_en<MODE, SMALL>(), PF>(P, a, b, x.lane, x.NCr, MODE != MODE_ATK && !a.multi);
+  prefetch_issue<PF, PF>(P, a, b, x.lane, x.NCr, MODE != MODE_ATK && !a.multi);
   step_board<NC, LT, MODE, SCAN, SMALL>(S, x, a, b, P);
 }
 
@@ -1957,7 +1953,7 @@ __global__ __launch_bounds__(128) TD_SMALL2_ATTR void td_step_kernel_small2(Step
     stage_cfg(S, a.cfg);
     const Ctx x{S.cfg, LT, NC, lane, a.cfgs, a.epoch};
     Prefetch P;
-    prefetch_issue<pf_en<MODE, true>(), PF_SMALL>(P, a, b, lane, NC, MODE != MODE_ATK && !a.multi);
+    prefetch_issue<PF_SMALL, PF_SMALL>(P, a, b, lane, NC, MODE != MODE_ATK && !a.multi);
     step_board<NC, LT, MODE, SCAN, true, true>(S, x, a, b, P, &SO);
   } else {
     float* const obs = a.obs + (size_t)b * NCH * NC;
