@@ -51,5 +51,16 @@ s5)  # 4 prefetched enemy slots in the TD-def small kernels (pf) + the header's 
   rm -rf $O/pmc/def-small_65536/FETCH_SIZE $O/pmc/def-small_65536/WRITE_SIZE
   run shapes 240 ./scripts/bin/obs_ceiling shapes || exit 1; cat $O/shapes.log
   ;;
+s6)  # issue priority 2 for boards with enemies (the small-batch tail) vs the product (hh), 3 rounds
+  for r in 1 2 3; do
+    for spec in 8192:2000 4096:2000 65536:300; do
+      bb=${spec%%:*}; st=${spec##*:}
+      for v in base prio; do
+        lib=$PWD/gym-td_amd/lib/libtdstep_$v.so; [ $v = base ] && lib=$PWD/gym-td_amd/lib/libtdstep.so
+        TDSTEP_LIB=$lib run ${v}_${bb}_$r 300 python bench.py --global-batch $bb --steps $st --no-cpu-baseline --timing none || exit 1; line ${v}_${bb}_$r
+      done
+    done
+  done
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
