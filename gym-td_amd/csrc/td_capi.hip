@@ -99,7 +99,6 @@ struct td_handle {
   int32_t* d_ovr_idx = nullptr;                           // td_reset_layouts: [B] index into d_stage or -1
   uint8_t *d_scratch = nullptr, *d_mask = nullptr, *d_fail = nullptr;
   int stage_cap = 0;
-  uint64_t* d_stamps = nullptr;  // TD_STAMPS diagnostic builds only (not owned)
   double* d_epstats = nullptr;   // [2] finished episodes, sum of their returns
   td_episode_record* d_lastep = nullptr;  // [B] each board's last finished episode
   // Layout refills run on kSideStreams side streams in turn; the step stream never
@@ -213,9 +212,6 @@ int dalloc(T** p, size_t n) {
 StepArgs base_args(td_handle* h) {
   StepArgs a;
   std::memset(&a, 0, sizeof a);
-#ifdef TD_GEN_STAMPS  // diagnostic builds: the reset / refill kernels' draws count their cycles
-  a.stamps = h->d_stamps;
-#endif
   a.B = h->B; a.L = h->L; a.mode = h->mode; a.multi = h->multi; a.difficulty = h->difficulty;
   a.autoreset = h->autoreset;
   a.xcd_map = h->xcd_map;
@@ -765,7 +761,6 @@ int td_step(td_handle* h, const td_step_io* io, void* stream) {
   a.real_def = io->real_def; a.real_atk = io->real_atk; a.fail_def = io->fail_def; a.fail_atk = io->fail_atk;
   a.win = io->win; a.allow_next = io->allow_next; a.ep_return = io->ep_return; a.ep_len = io->ep_len;
   a.cooldowns = io->cooldowns;
-  a.stamps = h->d_stamps;
   a.ep_stats = h->d_epstats;
   a.last_ep = h->d_lastep;
   // the refill goes first: it waits for the previous step only, so a board whose ring
@@ -980,29 +975,7 @@ int td_get_flags(td_handle* h, int32_t* host_flags) {
   return 0;
 }
 
-#if defined(TD_STAMPS) || defined(TD_GEN_STAMPS)
-// Diagnostic builds: per-board phase timestamps ([B][16] uint64, device memory).
-int td_debug_stamps(td_handle* h, uint64_t* dev) {
-  if (!h) return fail("NULL handle");
-  h->d_stamps = dev;
-  return 0;
-}
-#endif
 
-// Diagnostic: board b's ring -- head, tail, claim, then the NSLOT slot tags: 3 + NSLOT
-// words into out[0, cap).  Returns the word count (td_debug_ring(h, 0, NULL, 0) asks for it).
-int td_debug_ring(td_handle* h, int b, uint32_t* out, int cap) {
-  if (!out && cap == 0) return 3 + NSLOT;
-  if (!h || b < 0 || b >= h->B || !out) return fail("td_debug_ring: bad arguments");
-  if (cap < 3 + NSLOT) return fail("td_debug_ring: buffer of %d words, needs %d", cap, 3 + NSLOT);
-  HIP_OK(hipDeviceSynchronize());
-  HIP_OK(hipMemcpy(out, h->d_lay_head + b, 4, hipMemcpyDeviceToHost));
-  HIP_OK(hipMemcpy(out + 1, h->d_lay_tail + b, 4, hipMemcpyDeviceToHost));
-  HIP_OK(hipMemcpy(out + 2, h->d_lay_claim + b, 4, hipMemcpyDeviceToHost));
-  for (int s = 0; s < NSLOT; ++s)
-    HIP_OK(hipMemcpy(out + 3 + s, h->d_nxt + ((size_t)b * NSLOT + s) * slot_words(h->L), 4, hipMemcpyDeviceToHost));
-  return 3 + NSLOT;
-}
 
 // Diagnostic: hold (1) or give back (0) board b's refill claim, as a refill wave drawing
 // its layouts would (tests: a claim held past the ring guard's 1-s wait).

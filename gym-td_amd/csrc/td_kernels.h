@@ -48,7 +48,6 @@ struct StepArgs {
   uint32_t* guard_to;   // [1] ring-guard claim waits that gave up (td_guard_timeouts)
   const int32_t* ovr_idx;   // reset kernel, td_reset_layouts: [B] record index in ovr_rec, or -1
   const uint32_t* ovr_rec;  // caller-supplied layout records (layout_words(L) each)
-  uint64_t* stamps;     // TD_STAMPS diagnostic builds only: [B][16] s_memtime per phase
   const TdDevCfg* cfg;   // the current constant block (= cfgs + epoch)
   const TdDevCfg* cfgs;  // [NCFG] one block per paramConfig epoch (entities keep their epoch's values)
   int epoch;

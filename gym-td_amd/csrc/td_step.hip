@@ -32,14 +32,6 @@
 
 namespace td {
 
-#ifdef TD_STAMPS
-#define STAMP(i) do { if (a.stamps && x.lane == 0) a.stamps[(size_t)b * 16 + (i)] = __builtin_amdgcn_s_memtime(); } while (0)
-// 100-MHz chip-wide clock (comparable across CUs and XCDs): wave start / end
-#define STAMP_RT(i) do { if (a.stamps && x.lane == 0) a.stamps[(size_t)b * 16 + (i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
-#else
-#define STAMP(i) do { } while (0)
-#define STAMP_RT(i) do { } while (0)
-#endif
 
 // ---------------------------------------------------------------------------
 // per-board LDS image
@@ -684,7 +676,6 @@ __device__ __forceinline__ double board_step(Smem<NC>& S, U& u, const Ctx& x, co
     }
   }
 
-  STAMP(3);
   // --- towers fire in list order (:306-313); dead enemies stay targetable.
   // Tower k lives in lane k (cool-down in a register); a fired tower is read
   // with a wave-uniform lane index (v_readlane).
@@ -802,7 +793,6 @@ __device__ __forceinline__ double board_step(Smem<NC>& S, U& u, const Ctx& x, co
   }
   if (lane < u.nt) S.tCd[lane] = tcd;
 
-  STAMP(4);
   // --- kills (:313-317): every enemy at LP 0 was hit this step
   bool dead0 = val[0] && lp[0] == 0.0, dead1 = val[1] && lp[1] == 0.0;
   const int nk = popc64(ballot(dead0)) + popc64(ballot(dead1));
@@ -1654,8 +1644,6 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
   uint32_t* const opp = a.opp_mt + (size_t)b * OPP_WORDS;
   uint32_t* const hot = a.opp_hot + (size_t)b * HOT_WORDS;
   U u;
-  STAMP_RT(9);
-  STAMP(0);
   constexpr int PF = SMALL ? PF_SMALL : PF_LARGE;
   load_board<NC, PF, PF>(S, u, x, a, b, P);
   const int64_t act_in = (int64_t)(((uint64_t)lane_word(P.w, PF_ACT + 1) << 32) | lane_word(P.w, PF_ACT));
@@ -1678,7 +1666,6 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
   constexpr bool EARLY_MT = SMALL && !SCAN && MODE != MODE_2P;
   if constexpr (EARLY_MT) R.early_issue(x.lane);
   constexpr bool SCAN2 = SPLIT && SCAN;
-  STAMP(1);
   if (u.num_roads < 1 || u.num_roads > 3) {
     // never reset (its road generation failed): nothing to step
     const int nf = NCH * x.NCr;
@@ -1738,7 +1725,6 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
       }
     }
   }
-  STAMP(11);
   // ---- attacker
   if (MODE == MODE_DEF) {
     with_opp_rng(a, b, x.lane, R, [&](auto& G) { opponent_enemy(S, u, x, G, a.difficulty); });
@@ -1750,7 +1736,6 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
     if (MODE == MODE_ATK)
       with_opp_rng(a, b, x.lane, R, [&](auto& G) { opponent_tower(S, u, x, G, a.difficulty); });
   }
-  STAMP(12);
   // the towers and map[6] are final: cell words back to HBM if they changed, then
   // packed for the rest of the step (board_step reads the packed direction and distance)
   store_cells(S, u, x, a, b);
@@ -1769,7 +1754,6 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
     if (x.lane == 0) S.early_go = 1u;
     __syncthreads();
   }
-  STAMP(2);
 
   // ---- TDBoard.step
   // (parallel targeting: +1.1-1.4 % at 8,192 / 4,096 boards, -0.7 % in the large kernel at 65,536, profiles/r03/s29)
@@ -1825,7 +1809,6 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
   // The enemy list back to HBM (after the layout poll's loads, whose wait would
   // otherwise wait for these stores too; a reset board has none).
   store_enemies(S, u, x, a, b);
-  STAMP(5);
   if constexpr (SPLIT) {
     // the new episode's layout first (the second wave stores the board next)
     if (was_reset) {
@@ -1858,18 +1841,13 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
     }
     __syncthreads();
     enemy_stats(S, u, x);  // no-op for a board without enemies (e.g. just reset)
-    STAMP(13);
     channel_scalars(S, u, x);
-    STAMP(14);
     __syncthreads();
-    STAMP(6);
     if (was_reset) write_obs_lines<NC, LT>(S, x.lane, obs, u.n > 0, wt, a.edge_wt);
     else write_obs_lines<NC, LT, 0, obs_late_half<LT>(), 4, 2>(S, x.lane, obs, u.n > 0, wt, a.edge_wt);
   } else {
     enemy_stats(S, u, x);  // no-op for a board without enemies (e.g. just reset)
-    STAMP(13);
     channel_scalars(S, u, x);
-    STAMP(14);
     if (was_reset) {  // the new episode's layout
       store_cells(S, u, x, a, b);
       pack_obs_cells(S, x);
@@ -1877,7 +1855,6 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
     store_board(S, u, x, a, b, was_reset || done || u.flags != S.flags0);
     store_outputs(a, b, reward, ep_ret, real_def, ep_steps, fail_def, done, win, allow, cool, x.lane);
     // the observation last: nothing of the step is live any more, the writer has the registers
-    STAMP(6);
     if constexpr (LT != 0) {
       if ((reinterpret_cast<uintptr_t>(a.obs) & 15u) == 0) {
         write_obs_lines<NC, LT>(S, x.lane, obs, u.n > 0, wt, a.edge_wt);
@@ -1888,9 +1865,6 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
       write_obs<NC, LT>(S, x, obs, u.n > 0);
     }
   }
-  STAMP(7);
-  STAMP(8);
-  STAMP_RT(10);
 }
 
 // One workgroup (one wave) per board.  (A persistent variant that prefetched the
@@ -2039,13 +2013,9 @@ static hipError_t launch_opponent2(const StepArgs& a, int side, int level, hipSt
 hipError_t launch_opponent(const StepArgs& a, int side, int level, hipStream_t s) {
   switch (a.L) {
     case 10: return launch_opponent2<10>(a, side, level, s);
-#ifndef TD_L10_ONLY  // diagnostic register-usage compiles (scripts/kernel_resources.sh)
     case 20: return launch_opponent2<20>(a, side, level, s);
     case 30: return launch_opponent2<30>(a, side, level, s);
     default: return launch_opponent2<0>(a, side, level, s);
-#else
-    default: return hipErrorInvalidValue;
-#endif
   }
 }
 
@@ -2074,9 +2044,6 @@ __device__ int wave_layout(LayoutSmem<NC>& G, const StepArgs& a, int b, int retr
                            int budget) {
   const int lane = (int)threadIdx.x, L = a.L, lw = LAYOUT_HDR + L * L;
   const int sbytes = (int)road_scratch_bytes(L);
-#ifdef TD_GEN_STAMPS
-  const uint64_t wl_t0 = __builtin_amdgcn_s_memtime();
-#endif
   // (the walk budget and the retry count bound the draw's loop: wave-uniform, SGPRs)
   budget = (int)__builtin_amdgcn_readfirstlane((uint32_t)budget);
   retries = (int)__builtin_amdgcn_readfirstlane((uint32_t)retries);
@@ -2109,14 +2076,6 @@ __device__ int wave_layout(LayoutSmem<NC>& G, const StepArgs& a, int b, int retr
     __syncthreads();
     g.save_maps();
     if (lane == 0) { G.mt[MT_N] = g.pos; G.mt[MT_N + 1] = g.tw; G.res = res; }
-#ifdef TD_GEN_STAMPS
-    if (a.stamps && lane == 0) {
-      uint64_t* sp = a.stamps + (size_t)b * 16;
-      for (int i = 0; i < 6; ++i) sp[i] += g.cyc[i];
-      sp[6] += __builtin_amdgcn_s_memtime() - wl_t0;  // the call so far (stream copy-in and the draw)
-      sp[7] += 1;
-    }
-#endif
   }
   __syncthreads();
   // every store below is write-through (st_relaxed = sc1): the claim release and the
@@ -2377,26 +2336,18 @@ static int resident3(const StepArgs& a, int cus, int waves) {
 int step_resident_boards(const StepArgs& a, int cus, int waves) {
   switch (a.L) {
     case 10: return resident3<10>(a, cus, waves);
-#ifndef TD_L10_ONLY  // diagnostic register-usage compiles (scripts/kernel_resources.sh)
     case 20: return resident3<20>(a, cus, waves);
     case 30: return resident3<30>(a, cus, waves);
     default: return 0;  // generic-L kernels: no small-batch build
-#else
-    default: return 0;
-#endif
   }
 }
 
 hipError_t launch_step(const StepArgs& a, hipStream_t s, bool reset, hipEvent_t ev0, hipEvent_t ev1) {
   switch (a.L) {
     case 10: return launch2<10>(a, s, reset, ev0, ev1);
-#ifndef TD_L10_ONLY  // diagnostic register-usage compiles (scripts/kernel_resources.sh)
     case 20: return launch2<20>(a, s, reset, ev0, ev1);
     case 30: return launch2<30>(a, s, reset, ev0, ev1);
     default: return launch2<0>(a, s, reset, ev0, ev1);
-#else
-    default: return hipErrorInvalidValue;
-#endif
   }
 }
 
@@ -2430,13 +2381,9 @@ static void launch_autoreset2(const StepArgs& a, hipStream_t s) {
 hipError_t launch_autoreset(const StepArgs& a, hipStream_t s) {
   switch (a.L) {
     case 10: launch_autoreset2<10>(a, s); break;
-#ifndef TD_L10_ONLY  // diagnostic register-usage compiles (scripts/kernel_resources.sh)
     case 20: launch_autoreset2<20>(a, s); break;
     case 30: launch_autoreset2<30>(a, s); break;
     default: launch_autoreset2<0>(a, s); break;
-#else
-    default: break;
-#endif
   }
   return hipGetLastError();
 }
@@ -2454,13 +2401,9 @@ static void launch_refill2(const StepArgs& a_, hipStream_t s, int guard) {
 hipError_t launch_refill(const StepArgs& a, hipStream_t s, int guard) {
   switch (a.L) {
     case 10: launch_refill2<10>(a, s, guard); break;
-#ifndef TD_L10_ONLY  // diagnostic register-usage compiles (scripts/kernel_resources.sh)
     case 20: launch_refill2<20>(a, s, guard); break;
     case 30: launch_refill2<30>(a, s, guard); break;
     default: launch_refill2<0>(a, s, guard); break;
-#else
-    default: break;
-#endif
   }
   return hipGetLastError();
 }

@@ -52,14 +52,6 @@ struct WaveRoadGen {
   int L, lane;
   uint32_t pos, tw, base, n, win;
   uint32_t field, rot;  // lane j holds cells [32j, 32j + 32)
-#ifdef TD_GEN_STAMPS  // diagnostic builds: s_memtime cycles by part of the draw (scripts/probe_draw.py)
-  uint64_t cyc[6] = {0, 0, 0, 0, 0, 0};  // walk, proof, stamp, erase, stream window, walks
-#define GEN_T0() const uint64_t gen_t0_ = __builtin_amdgcn_s_memtime()
-#define GEN_ACC(i) (cyc[i] += __builtin_amdgcn_s_memtime() - gen_t0_)
-#else
-#define GEN_T0() do { } while (0)
-#define GEN_ACC(i) do { } while (0)
-#endif
 
   // scratch carve for L*L = nc cells: picks u32[nc], r1 / r2 / rb / mainr u16[nc], field / rot
   // u32[(nc + 31) / 32] -- 12 nc + 8 (nc + 31) / 32 <= road_scratch_bytes(L) bytes
@@ -73,7 +65,6 @@ struct WaveRoadGen {
 
   // ---- the numpy-legacy stream (LazyMt semantics, 64 words per refill) ----
   __device__ void refill() {
-    GEN_T0();
     if (pos >= (uint32_t)MT_N) { pos = 0; tw = 0; }
     base = pos;
     n = (uint32_t)MT_N - pos < 64u ? (uint32_t)MT_N - pos : 64u;
@@ -93,7 +84,6 @@ struct WaveRoadGen {
     if (lazy) mt[q] = y;
     if (base + n > tw) tw = base + n;
     win = mt_temper(y);
-    GEN_ACC(4);
   }
   __device__ __forceinline__ uint32_t next() {
     if (pos - base >= n) refill();
@@ -384,9 +374,7 @@ struct WaveRoadGen {
           if (khi <= klo) { status = ROAD_ERR_RANDINT; goto failed; }
           bool hp = false;
           if (st.att == 1) {
-            GEN_T0();
             hp = hopeless(klo, khi, nm, (int)st.endc);
-            GEN_ACC(1);
           }
           if (hp) { status = ROAD_ERR_BOUND; goto failed; }  // RoadGen::branch_hopeless
           k = np_randint(klo, khi);
@@ -400,12 +388,7 @@ struct WaveRoadGen {
         int n = 0, e = 0;
         int ok;
         {
-          GEN_T0();
           ok = walk(r0, c0, d, out, &n, &e);
-          GEN_ACC(0);
-#ifdef TD_GEN_STAMPS
-          cyc[5] += 1;
-#endif
         }
         bool accept = ok != 0;
         if (phase == RP_ROAD1) {
@@ -420,9 +403,7 @@ struct WaveRoadGen {
           accept = accept && iabs(e / L - endc / L) + iabs(e % L - endc % L) >= L * 3 / 4;
         }
         if (!accept) {
-          GEN_T0();
           erase(out, n);
-          GEN_ACC(3);
           continue;
         }
         if (phase == RP_ROAD1) {
@@ -472,9 +453,7 @@ struct WaveRoadGen {
         }
         uint32_t maxdist = st.maxdist;
         {
-          GEN_T0();
           stamp(cv, tot, phase == RP_ROAD2 ? 0 : (int)st.ri, &maxdist);
-          GEN_ACC(2);
         }
         st.maxdist = maxdist;
         if (phase == RP_ROAD2) { st.phase = RP_BRANCH; st.ri = 1; }

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Per-kernel registers / scratch / occupancy / LDS of td_step.hip (a device-only compile
 # with the kernel-resource-usage remarks):
-#   bash scripts/kernel_resources.sh [extra hipcc flags, e.g. -DTD_L10_ONLY]
+#   bash scripts/kernel_resources.sh [extra hipcc flags]
 cd "$(dirname "$0")/../gym-td_amd/csrc"
 obj=$(mktemp /tmp/tdres_XXXXXX.o)
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -w --cuda-device-only "$@" \

@@ -7,7 +7,6 @@ export TMPDIR=/tmp
 WL=${WL:-def-small}
 B=${B:-65536}
 run() { local name=$1 secs=$2; shift 2; echo "== $name" >&2; timeout -k 10 "$secs" "$@" > "$P/$name.log" 2>&1; local rc=$?; echo "== $name rc=$rc" >&2; tail -3 "$P/$name.log" >&2; return $rc; }
-[ -n "$NO_PHASES" ] || run phases 300 env TDSTEP_LIB=$PWD/gym-td_amd/lib/libtdstep_stamps.so python scripts/probe_phases.py $B 10 600 || exit $?
 BENCH="python bench.py --workload $WL --steps 20 --warmup 2 --burnin 100 --no-cpu-baseline --boards $B"
 # kernel trace of the bench line's run (default steps; the CPU baseline legs are left out: their
 # pool workers are killed at exit under the profiler)

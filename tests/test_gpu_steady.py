@@ -1,7 +1,8 @@
 """Every board of the state bench.py times.
 
-bench.py times the metric's 65,536 TD-def 10x10 boards (and the 8,192-board N = 8 share)
-after its burn-in recipe: explicit resets staggered over the first 1,200 steps
+bench.py times the metric's 65,536 TD-def 10x10 boards (and the 8,192-board N = 8 share,
+configs[1]'s 4,096, configs[2]'s 16,384 TD-2p 20x20 multi-action and configs[4]'s 16,384
+30x30 per GPU) after its burn-in recipe: explicit resets staggered over the first 1,200 steps
 (bench.stagger_mask: board i is reset before step i mod 1,200), 1,200 steps with
 auto-reset, uniform random defender actions.  In that steady state every episode phase is
 present, about B / 1,200 boards auto-reset per step and enemies are upgraded past progress
@@ -37,22 +38,33 @@ def _threads():
     return max(1, min(t, 32))
 
 
-@pytest.mark.parametrize("B,want", [(65536, "small2"), (8192, "small")])
-def test_steady_state_every_board(B, want):
-    L, period = 10, P.hyper_parameters.max_episode_steps
+# the metric's N = 1 line, the N = 8 share, configs[1], configs[2] (TD-2p 20x20 multi-action)
+# and configs[4] per GPU (30x30), each on the kernel td_create picks on a 256-CU MI355X
+@pytest.mark.parametrize("L,B,mode,multi,want", [
+    (10, 65536, "def", False, "small2"), (10, 8192, "def", False, "small"), (10, 4096, "def", False, "small2"),
+    (20, 16384, "2p", True, "small2"), (30, 16384, "def", False, "small2")])
+def test_steady_state_every_board(L, B, mode, multi, want):
+    period = P.hyper_parameters.max_episode_steps
     burnin = period
     seeds = shard.shard_seeds(0, 0, B)  # bench.py's seeds at N = 1 (base 0 + global index)
-    eng = TDEngine(L, B, "def", False, 1, np_seeds=seeds, py_seeds=seeds, autoreset=True, info=True)
+    eng = TDEngine(L, B, mode, multi, 1, np_seeds=seeds, py_seeds=seeds, autoreset=True, info=not multi)
     bt = None
     try:
         if torch.cuda.get_device_properties(0).multi_processor_count == 256:
             assert eng.step_kernel == want, eng.step_kernel_name  # the kernel the bench line times
         eng.reset_all()  # failing first draws skipped (bench.py)
-        bt = C.Batch(L, B, "def", 1, seeds, seeds, threads=_threads())
+        bt = C.Batch(L, B, mode, 1, seeds, seeds, multi=multi, threads=_threads())
         assert bt.initial_failed == []
         assert np.array_equal(eng.obs.cpu().numpy(), bt.obs()), "initial observations differ"
         gidx = np.arange(B)
         rng = np.random.RandomState(20260)
+        # the multi-action shape cycles bench.py's N_ACTION_BUFS pre-drawn batches (host + device)
+        pool = []
+        if multi:
+            for _ in range(bench.N_ACTION_BUFS):
+                d = rng.randint(0, 3, size=(B, 6, L, L)).astype(np.int64)
+                a = rng.randint(0, 5, size=(B, 3, 8)).astype(np.int64)
+                pool.append((d, a, torch.from_numpy(d).to(eng.device), torch.from_numpy(a).to(eng.device)))
         obs_c = np.empty((B, 45, L, L), dtype=np.float32)
         finished, resets = 0, 0
         for k in range(burnin + WINDOW):
@@ -61,12 +73,16 @@ def test_steady_state_every_board(B, want):
                 eng.reset(m)
                 assert bt.reset(m) == 0
                 resets += int(m.sum())
-            acts = rng.randint(0, 6 * L * L + 1, size=B).astype(np.int64)
-            eng.step(def_act=torch.from_numpy(acts).to(eng.device))
+            if multi:
+                acts, atk, dd, ad = pool[k % len(pool)]
+                eng.step(def_act=dd, atk_act=ad)
+            else:
+                acts, atk = rng.randint(0, 6 * L * L + 1, size=B).astype(np.int64), None
+                eng.step(def_act=torch.from_numpy(acts).to(eng.device))
             if k < burnin:
-                bt.step(acts)  # (the burn-in's observations are not built on the CPU side)
+                bt.step(acts, atk)  # (the burn-in's observations are not built on the CPU side)
                 continue
-            rw_c, dn_c = bt.step(acts, obs=obs_c)
+            rw_c, dn_c = bt.step(acts, atk, obs=obs_c)
             rw = eng.reward.cpu().numpy()
             dn = eng.done.cpu().numpy()
             bad = np.flatnonzero(rw.view(np.uint64) != rw_c.view(np.uint64))
