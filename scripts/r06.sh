@@ -62,5 +62,12 @@ s6)  # issue priority 2 for boards with enemies (the small-batch tail) vs the pr
     done
   done
   ;;
+s7)  # the cleaned tree (no diagnostic paths, header half store): steady-state tests over the five configs, GPU suite, smoke, the driver's command twice
+  run pytest_steady 900 python -u -m pytest tests/test_gpu_steady.py -m gpu -v -x --timeout 600 --timeout-method thread -p no:cacheprovider
+  rc=$?; grep -E "^(FAILED|E  )|PASSED|passed|failed" $O/pytest_steady.log | head -20; [ $rc -le 1 ] || exit $rc
+  gpusuite 1100 "--deselect tests/test_gpu_steady.py"; rc=$?; [ $rc -le 1 ] || exit $rc
+  run smoke 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" || exit 1
+  for r in 1 2; do run bench_driver_$r 300 python bench.py --gpus 1 --steps 20 --warmup 5 || exit 1; line bench_driver_$r; done
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
