@@ -89,5 +89,9 @@ s8)  # the final build: every line with the bench's defaults, kernel traces, PMC
     rm -rf $O/pmc/${wl}_$bb/FETCH_SIZE $O/pmc/${wl}_$bb/WRITE_SIZE
   done
   ;;
+s9)  # bench.py --gpus 2 end to end (gloo, both ranks on cuda:0) as a GPU test
+  run pytest_ranks 400 python -u -m pytest tests/test_gpu_bench_ranks.py -m gpu -v -x --timeout 350 --timeout-method thread -p no:cacheprovider
+  rc=$?; grep -E "^(FAILED|E  )|PASSED|passed|failed" $O/pytest_ranks.log | head -20; [ $rc -le 1 ] || exit $rc
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
