@@ -93,5 +93,8 @@ s9)  # bench.py --gpus 2 end to end (gloo, both ranks on cuda:0) as a GPU test
   run pytest_ranks 400 python -u -m pytest tests/test_gpu_bench_ranks.py -m gpu -v -x --timeout 350 --timeout-method thread -p no:cacheprovider
   rc=$?; grep -E "^(FAILED|E  )|PASSED|passed|failed" $O/pytest_ranks.log | head -20; [ $rc -le 1 ] || exit $rc
   ;;
+s10)  # the 7-TB/s shape: narrow address band or few boards per CU? (scripts/obs_span.hip)
+  run span 240 ./scripts/bin/obs_span || exit 1; cat $O/span.log
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
