@@ -96,5 +96,12 @@ s9)  # bench.py --gpus 2 end to end (gloo, both ranks on cuda:0) as a GPU test
 s10)  # the 7-TB/s shape: narrow address band or few boards per CU? (scripts/obs_span.hip)
   run span 240 ./scripts/bin/obs_span || exit 1; cat $O/span.log
   ;;
+s11)  # closing check on the final tree: build() on the box (no recompile expected), GPU suite, smoke, the driver's command twice
+  run build 400 python -c "import time, __graft_entry__ as g; t = time.time(); g.build(); print('build() %.1f s' % (time.time() - t))" || exit 1; grep -E "build\(\)|Nothing|hipcc" $O/build.log | head -5
+  gpusuite 1100; rc=$?; [ $rc -le 1 ] || exit $rc
+  run smoke 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" || exit 1
+  for r in 1 2; do run bench_driver_$r 300 python bench.py --gpus 1 --steps 20 --warmup 5 || exit 1; line bench_driver_$r; done
+  grep -h '"traffic"' $O/bench_driver_1.log | grep -o '"traffic": [^,]*' | head -1
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
