@@ -103,5 +103,14 @@ s11)  # closing check on the final tree: build() on the box (no recompile expect
   for r in 1 2; do run bench_driver_$r 300 python bench.py --gpus 1 --steps 20 --warmup 5 || exit 1; line bench_driver_$r; done
   grep -h '"traffic"' $O/bench_driver_1.log | grep -o '"traffic": [^,]*' | head -1
   ;;
+s12)  # kernel choice at configs[1] (4,096 boards) and the N = 8 share (8,192) on the final build: small / small2 / large
+  for r in 1 2; do
+    for spec in 4096 8192; do
+      for k in small small2 large; do
+        run ${k}_${spec}_$r 300 python bench.py --global-batch $spec --steps 2000 --no-cpu-baseline --timing none --step-kernel $k || exit 1; line ${k}_${spec}_$r
+      done
+    done
+  done
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
