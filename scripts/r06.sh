@@ -112,5 +112,16 @@ s12)  # kernel choice at configs[1] (4,096 boards) and the N = 8 share (8,192) o
     done
   done
   ;;
+s13)  # issue priority by launch order (the last-launched quarter of a one-round grid at 3; lp) vs the product, 3 rounds
+  for r in 1 2 3; do
+    for spec in 8192:2000 4096:2000 65536:300; do
+      bb=${spec%%:*}; st=${spec##*:}
+      for v in base lp; do
+        lib=$PWD/gym-td_amd/lib/libtdstep_$v.so; [ $v = base ] && lib=$PWD/gym-td_amd/lib/libtdstep.so
+        TDSTEP_LIB=$lib run ${v}_${bb}_$r 300 python bench.py --global-batch $bb --steps $st --no-cpu-baseline --timing none || exit 1; line ${v}_${bb}_$r
+      done
+    done
+  done
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
