@@ -79,6 +79,16 @@ __device__ __forceinline__ void stage_cfg(Smem<NC>& S, const TdDevCfg* g, int l 
   if (l < (int)(sizeof(TdDevCfg) / 16))
     reinterpret_cast<uint4*>(&S.cfg)[l] = reinterpret_cast<const uint4*>(g)[l];
 }
+// The same in two halves, so that a step kernel issues the board's loads between them:
+// staged in one piece, the block's load was waited for (vmcnt(0)) before any of the
+// board's loads went out -- one L2 round trip in front of every board's step.
+__device__ __forceinline__ uint4 load_cfg(const TdDevCfg* g, int l) {
+  return l < (int)(sizeof(TdDevCfg) / 16) ? reinterpret_cast<const uint4*>(g)[l] : uint4{0u, 0u, 0u, 0u};
+}
+template <int NC>
+__device__ __forceinline__ void store_cfg(Smem<NC>& S, uint4 v, int l) {
+  if (l < (int)(sizeof(TdDevCfg) / 16)) reinterpret_cast<uint4*>(&S.cfg)[l] = v;
+}
 
 // Wave-uniform scalar board state (identical in every lane).
 struct U {
@@ -1877,12 +1887,14 @@ __device__ __forceinline__ void step_kernel_body(const StepArgs& a) {
   const int i = (int)blockIdx.x;
   if (i >= a.B) return;
   const int b = a.xcd_map ? xcd_board(i, a.B) : i;
-  stage_cfg(S, a.cfg);
   const int L = LT ? LT : a.L;
   const Ctx x{S.cfg, L, L * L, (int)(threadIdx.x & 63), a.cfgs, a.epoch};
+  const uint4 cfgv = load_cfg(a.cfg, x.lane);
   Prefetch P;
   constexpr int PF = SMALL ? PF_SMALL : PF_LARGE;
   prefetch_issue<PF, PF>(P, a, b, x.lane, x.NCr, MODE != MODE_ATK && !a.multi);
+  store_cfg(S, cfgv, x.lane);  // (its load issued first: this wait leaves the board's loads in flight)
+  wsync();  // every lane reads the block: no LDS access may move above its store
   step_board<NC, LT, MODE, SCAN, SMALL>(S, x, a, b, P);
 }
 
@@ -1924,10 +1936,12 @@ __global__ __launch_bounds__(128) TD_SMALL2_ATTR void td_step_kernel_small2(Step
   const int b = a.xcd_map ? xcd_board((int)blockIdx.x, a.B) : (int)blockIdx.x;
   const int lane = (int)threadIdx.x & 63;
   if (threadIdx.x < 64) {
-    stage_cfg(S, a.cfg);
     const Ctx x{S.cfg, LT, NC, lane, a.cfgs, a.epoch};
+    const uint4 cfgv = load_cfg(a.cfg, lane);
     Prefetch P;
     prefetch_issue<PF_SMALL, PF_SMALL>(P, a, b, lane, NC, MODE != MODE_ATK && !a.multi);
+    store_cfg(S, cfgv, lane);  // (see load_cfg)
+    wsync();  // every lane reads the block: no LDS access may move above its store
     step_board<NC, LT, MODE, SCAN, true, true>(S, x, a, b, P, &SO);
   } else {
     float* const obs = a.obs + (size_t)b * NCH * NC;

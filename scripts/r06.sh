@@ -123,5 +123,23 @@ s13)  # issue priority by launch order (the last-launched quarter of a one-round
     done
   done
   ;;
+s14)  # the constant block's load issued with the board's loads (one L2 round trip fewer in front of each board; product) vs base: parity, A/B 3 rounds
+  run pytest_cf 900 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_steady.py tests/test_gpu_deep.py tests/test_gpu_envs.py -m gpu -q -x --timeout 600 --timeout-method thread -p no:cacheprovider
+  rc=$?; grep -E "^(FAILED|E  )" $O/pytest_cf.log | head -20; tail -1 $O/pytest_cf.log; [ $rc -eq 0 ] || exit $rc
+  for r in 1 2 3; do
+    for spec in 8192:2000 4096:2000 65536:300 32768:600; do
+      bb=${spec%%:*}; st=${spec##*:}
+      for v in base cf; do
+        lib=$PWD/gym-td_amd/lib/libtdstep_$v.so; [ $v = cf ] && lib=$PWD/gym-td_amd/lib/libtdstep.so
+        TDSTEP_LIB=$lib run ${v}_${bb}_$r 300 python bench.py --global-batch $bb --steps $st --no-cpu-baseline --timing none || exit 1; line ${v}_${bb}_$r
+      done
+    done
+  done
+  for v in base cf; do
+    lib=$PWD/gym-td_amd/lib/libtdstep_$v.so; [ $v = cf ] && lib=$PWD/gym-td_amd/lib/libtdstep.so
+    TDSTEP_LIB=$lib run ${v}_p2 300 python bench.py --workload 2p-middle-multi --steps 200 --no-cpu-baseline --timing none || exit 1; line ${v}_p2
+    TDSTEP_LIB=$lib run ${v}_l30 300 python bench.py --workload def-large --global-batch 16384 --steps 200 --no-cpu-baseline --timing none || exit 1; line ${v}_l30
+  done
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
