@@ -1880,11 +1880,20 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
 // One workgroup (one wave) per board.  (A persistent variant that prefetched the
 // next board while stepping the current one measured slower: its static board
 // assignment leaves a one-board tail, and the step is bound by HBM writes.)
+// The kernel arguments a step needs before its board's loads go out, read together at the
+// top: read where each is used they were six dependent scalar loads, each waited for, in
+// front of every board's first load.
+__device__ __forceinline__ void prologue_args(const StepArgs& a) {
+  asm volatile("" ::"s"(a.B), "s"(a.xcd_map), "s"(a.multi), "s"(a.cfg), "s"(a.hdr), "s"(a.en_lp), "s"(a.en_mg),
+               "s"(a.en_inf), "s"(a.tw_cd), "s"(a.tw_inf), "s"(a.cells), "s"(a.opp_hot), "s"(a.def_act));
+}
+
 template <int LT, int MODE, bool SCAN, bool SMALL>
 __device__ __forceinline__ void step_kernel_body(const StepArgs& a) {
   constexpr int NC = LT ? LT * LT : MAX_KERNEL_L * MAX_KERNEL_L;
   __shared__ Smem<NC> S;
   const int i = (int)blockIdx.x;
+  prologue_args(a);
   if (i >= a.B) return;
   const int b = a.xcd_map ? xcd_board(i, a.B) : i;
   const int L = LT ? LT : a.L;
@@ -1932,6 +1941,7 @@ __global__ __launch_bounds__(128) TD_SMALL2_ATTR void td_step_kernel_small2(Step
   constexpr int NC = LT * LT;
   __shared__ Smem<NC> S;
   __shared__ StepOut SO;
+  prologue_args(a);
   if ((int)blockIdx.x >= a.B) return;
   const int b = a.xcd_map ? xcd_board((int)blockIdx.x, a.B) : (int)blockIdx.x;
   const int lane = (int)threadIdx.x & 63;

@@ -141,5 +141,23 @@ s14)  # the constant block's load issued with the board's loads (one L2 round tr
     TDSTEP_LIB=$lib run ${v}_l30 300 python bench.py --workload def-large --global-batch 16384 --steps 200 --no-cpu-baseline --timing none || exit 1; line ${v}_l30
   done
   ;;
+s15)  # the kernel arguments the prologue needs read in one scalar round trip (pa, product) vs cf: parity, A/B 3 rounds
+  run pytest_pa 900 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_steady.py tests/test_gpu_deep.py tests/test_gpu_envs.py -m gpu -q -x --timeout 600 --timeout-method thread -p no:cacheprovider
+  rc=$?; grep -E "^(FAILED|E  )" $O/pytest_pa.log | head -20; tail -1 $O/pytest_pa.log; [ $rc -eq 0 ] || exit $rc
+  for r in 1 2 3; do
+    for spec in 8192:2000 4096:2000 65536:300 32768:600; do
+      bb=${spec%%:*}; st=${spec##*:}
+      for v in cf pa; do
+        lib=$PWD/gym-td_amd/lib/libtdstep_$v.so; [ $v = pa ] && lib=$PWD/gym-td_amd/lib/libtdstep.so
+        TDSTEP_LIB=$lib run ${v}_${bb}_$r 300 python bench.py --global-batch $bb --steps $st --no-cpu-baseline --timing none || exit 1; line ${v}_${bb}_$r
+      done
+    done
+  done
+  for v in cf pa; do
+    lib=$PWD/gym-td_amd/lib/libtdstep_$v.so; [ $v = pa ] && lib=$PWD/gym-td_amd/lib/libtdstep.so
+    TDSTEP_LIB=$lib run ${v}_p2 300 python bench.py --workload 2p-middle-multi --steps 200 --no-cpu-baseline --timing none || exit 1; line ${v}_p2
+    TDSTEP_LIB=$lib run ${v}_l30 300 python bench.py --workload def-large --global-batch 16384 --steps 200 --no-cpu-baseline --timing none || exit 1; line ${v}_l30
+  done
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
