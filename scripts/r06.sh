@@ -159,5 +159,18 @@ s15)  # the kernel arguments the prologue needs read in one scalar round trip (p
     TDSTEP_LIB=$lib run ${v}_l30 300 python bench.py --workload def-large --global-batch 16384 --steps 200 --no-cpu-baseline --timing none || exit 1; line ${v}_l30
   done
   ;;
+s16)  # the output pointers read together before the outputs are stored (po, product) vs pa: parity, A/B 3 rounds
+  run pytest_po 900 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_steady.py tests/test_gpu_envs.py -m gpu -q -x --timeout 600 --timeout-method thread -p no:cacheprovider
+  rc=$?; grep -E "^(FAILED|E  )" $O/pytest_po.log | head -20; tail -1 $O/pytest_po.log; [ $rc -eq 0 ] || exit $rc
+  for r in 1 2 3; do
+    for spec in 8192:2000 4096:2000 65536:300 32768:600; do
+      bb=${spec%%:*}; st=${spec##*:}
+      for v in pa po; do
+        lib=$PWD/gym-td_amd/lib/libtdstep_$v.so; [ $v = po ] && lib=$PWD/gym-td_amd/lib/libtdstep.so
+        TDSTEP_LIB=$lib run ${v}_${bb}_$r 300 python bench.py --global-batch $bb --steps $st --no-cpu-baseline --timing none || exit 1; line ${v}_${bb}_$r
+      done
+    done
+  done
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
