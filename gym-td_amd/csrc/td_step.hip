@@ -1433,10 +1433,6 @@ struct alignas(16) StepOut {
 __device__ __forceinline__ void store_outputs(const StepArgs& a, int b, double reward, double ep_ret, int64_t real_def,
                                               int32_t ep_steps, int32_t fail_def, bool done, int win, uint32_t allow,
                                               uint32_t cool, int lane) {
-  // the output pointers read together (one scalar round trip; each tested where it is
-  // stored, they were a chain of dependent kernel-argument loads in front of the writer)
-  asm volatile("" ::"s"(a.reward), "s"(a.done), "s"(a.win), "s"(a.allow_next), "s"(a.cooldowns), "s"(a.fail_def),
-               "s"(a.real_def), "s"(a.ep_return), "s"(a.ep_len), "s"(a.last_ep), "s"(a.ep_stats), "s"(a.multi));
   if (lane != 0) return;
   sst(&a.reward[b], reward);
   sst(&a.done[b], (uint8_t)(done ? 1 : 0));
