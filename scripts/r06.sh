@@ -172,5 +172,28 @@ s16)  # the output pointers read together before the outputs are stored (po, pro
     done
   done
   ;;
+s17)  # the final build (constant block + argument prologue): GPU suite, smoke, the driver's command twice, every line, kernel traces, PMC bytes
+  gpusuite 1100; rc=$?; [ $rc -le 1 ] || exit $rc
+  run smoke 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" || exit 1
+  for r in 1 2; do run bench_driver_$r 300 python bench.py --gpus 1 --steps 20 --warmup 5 || exit 1; line bench_driver_$r; done
+  run line_65536 300 python bench.py --steps 300 --no-cpu-baseline || exit 1; line line_65536
+  run line_32768 300 python bench.py --global-batch 32768 --steps 600 --no-cpu-baseline || exit 1; line line_32768
+  run line_16384 300 python bench.py --global-batch 16384 --steps 1000 --no-cpu-baseline || exit 1; line line_16384
+  run line_8192 300 python bench.py --global-batch 8192 --steps 2000 --no-cpu-baseline || exit 1; line line_8192
+  run line_4096 300 python bench.py --global-batch 4096 --steps 2000 --no-cpu-baseline || exit 1; line line_4096
+  run line_p2 300 python bench.py --workload 2p-middle-multi --steps 200 --no-cpu-baseline || exit 1; line line_p2
+  run line_l30 300 python bench.py --workload def-large --global-batch 16384 --steps 200 --no-cpu-baseline || exit 1; line line_l30
+  kt() { local name=$1; shift; run kt_$name 300 timeout -s KILL 280 rocprofv3 --kernel-trace --stats -d $O/kt_$name -o kt --output-format csv -- "$@" || return 1; cp $(find $O/kt_$name -name "*kernel_stats.csv") $O/kt_${name}_kernel_stats.csv; rm -rf $O/kt_$name; grep -h td_step_kernel $O/kt_${name}_kernel_stats.csv | cut -c1-160; }
+  kt drv python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline || exit 1
+  kt b8192 python bench.py --global-batch 8192 --steps 300 --no-cpu-baseline || exit 1
+  kt b4096 python bench.py --global-batch 4096 --steps 300 --no-cpu-baseline || exit 1
+  kt p2 python bench.py --workload 2p-middle-multi --steps 100 --no-cpu-baseline || exit 1
+  kt l30 python bench.py --workload def-large --global-batch 16384 --steps 100 --no-cpu-baseline || exit 1
+  for spec in def-small:65536 def-small:8192 def-small:4096 2p-middle-multi:16384 def-large:16384; do
+    wl=${spec%%:*}; bb=${spec##*:}
+    OUT=$O/pmc NAME=${wl}_$bb WL=$wl B=$bb timeout -k 10 700 bash scripts/pmc_ab.sh || exit 1
+    rm -rf $O/pmc/${wl}_$bb/FETCH_SIZE $O/pmc/${wl}_$bb/WRITE_SIZE
+  done
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
