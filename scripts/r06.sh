@@ -195,5 +195,14 @@ s17)  # the final build (constant block + argument prologue): GPU suite, smoke, 
     rm -rf $O/pmc/${wl}_$bb/FETCH_SIZE $O/pmc/${wl}_$bb/WRITE_SIZE
   done
   ;;
+s18)  # what do episode ends cost at small batches?  auto-reset on (the metric) vs off (diagnostic: finished boards keep stepping)
+  for r in 1 2; do
+    for bb in 8192 4096; do
+      for ar in 1 0; do
+        run ar${ar}_${bb}_$r 300 python bench.py --global-batch $bb --steps 2000 --no-cpu-baseline --timing none --autoreset $ar || exit 1; line ar${ar}_${bb}_$r
+      done
+    done
+  done
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
