@@ -1244,6 +1244,8 @@ struct Prefetch {
 // the large-batch kernel (HBM-bound) takes none and loads exactly the live slots once
 // the header's counts are in (one dependent round trip, hidden by the other waves).
 constexpr int PF_ACT = 24, PF_HOT = 26, PF_SMALL = 16, PF_LARGE = 0;
+constexpr int PF_LAYHEAD = PF_HOT + HOT_WORDS;  // lane of lay_head[b] (the next staged layout's number)
+static_assert(PF_LAYHEAD < 64, "prefetch word lanes");
 // (Four enemy slots instead of 16 in TD-def, where 0.02 % of bench.py's steady-state boards
 // hold more than 4, read the same bytes -- each slot array's first 128-B line is fetched
 // whole either way: PMC 1,534 vs 1,535 B read per board -- in the same time, r06/s5.)
@@ -1273,6 +1275,7 @@ __device__ __forceinline__ void prefetch_issue(Prefetch& P, const StepArgs& a, i
   if (lane < PF_ACT) src = reinterpret_cast<const uint32_t*>(a.hdr + b) + lane;
   else if (lane < PF_HOT) src = want_act ? reinterpret_cast<const uint32_t*>(a.def_act + b) + (lane - PF_ACT) : nullptr;
   else if (lane < PF_HOT + HOT_WORDS) src = a.opp_hot + (size_t)b * HOT_WORDS + (lane - PF_HOT);
+  else if (lane == PF_LAYHEAD) src = a.lay_head + b;  // (written only by this board's step / reset waves)
   else src = nullptr;
   P.w = src ? *src : 0u;
 }
@@ -1358,6 +1361,25 @@ __device__ __forceinline__ void reset_board(Smem<NC>& S, U& u, const Ctx& x, con
   u.cost_def = C.def_init_cost; u.cost_atk = C.atk_init_cost;
   u.base_LP = C.base_LP; u.steps = 0; u.progress = 0.0;
   u.max_cost = C.max_cost; u.max_base_LP = C.base_LP;  // TDBoard(max_cost, base_LP) from config at reset
+  u.atk_cd = 0; u.def_cd = 0; u.n = 0; u.nt = 0; u.ep_ret = 0.0;
+  u.cells_dirty = true;
+  u.tw_dirty = true;
+  wsync();
+}
+
+// The same from a record already in registers (L*L <= 128: lane l holds header word l % 8,
+// cell l and cell l + 64), loaded during the step by the early layout hand-off (step_board).
+template <int NC>
+__device__ __forceinline__ void reset_board_regs(Smem<NC>& S, U& u, const Ctx& x, uint32_t hw, uint32_t c0, uint32_t c1) {
+  static_assert(NC <= 128, "two cell words per lane");
+  const TdDevCfg& C = x.C;
+  if (x.lane < NC) S.cell[x.lane] = c0;
+  if (x.lane + 64 < NC) S.cell[x.lane + 64] = c1;
+  u.num_roads = (int)rdl(hw, 1); u.end_cell = (int)rdl(hw, 2); u.maxdist = (int)rdl(hw, 3);
+  u.set_starts(rdl(hw, 4), rdl(hw, 5), rdl(hw, 6));
+  u.cost_def = C.def_init_cost; u.cost_atk = C.atk_init_cost;
+  u.base_LP = C.base_LP; u.steps = 0; u.progress = 0.0;
+  u.max_cost = C.max_cost; u.max_base_LP = C.base_LP;
   u.atk_cd = 0; u.def_cd = 0; u.n = 0; u.nt = 0; u.ep_ret = 0.0;
   u.cells_dirty = true;
   u.tw_dirty = true;
@@ -1709,6 +1731,24 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
   float* const obs = a.obs + (size_t)b * NCH * x.NCr;
   const bool wt = a.obs_wt != 0;
 
+  // Early layout hand-off (L = 10, the discrete small kernels).  A board that may finish
+  // this step -- it reaches the step limit, or holds at least as many enemies as its base
+  // has LP (a leak costs one LP each: a necessary condition; 1.2 % of bench.py's
+  // steady-state boards, every one that finishes) -- polls its next staged layout's tag
+  // now, and once the tag has come back (before the board step) takes the acquire and
+  // loads the record into registers: the episode end then resets from them, instead of
+  // three dependent round trips and the acquire after the step.  A board that does not
+  // finish drops them; a ring still dry then is served by the late path below.
+  constexpr bool EARLY_LAY = SMALL && LT == 10 && !SCAN;
+  const uint32_t lay_head0 = lane_word(P.w, PF_LAYHEAD);
+  const uint32_t* const lay_rec = a.nxt + ((size_t)b * NSLOT + lay_head0 % NSLOT) * a.slot_words;
+  bool el_try = false, el_ok = false;
+  uint32_t el_tag = 0u, el_hw = 0u, el_c0 = 0u, el_c1 = 0u;
+  if constexpr (EARLY_LAY) {
+    el_try = a.autoreset && !a.opp_np && (u.steps + 1 >= C.max_episode_steps || u.n >= u.base_LP);
+    if (el_try) el_tag = ld_relaxed(lay_rec);  // (its value is looked at before the board step)
+  }
+
   u.atk_cd = u.atk_cd - 1 > 0 ? u.atk_cd - 1 : 0;
   u.def_cd = u.def_cd - 1 > 0 ? u.def_cd - 1 : 0;
   const int64_t empty_def = (int64_t)6 * x.NCr;
@@ -1765,6 +1805,16 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
     __syncthreads();
   }
 
+  if constexpr (EARLY_LAY) {  // the early poll has come back: acquire and load the record (used at the episode end)
+    if (el_try && __builtin_amdgcn_readfirstlane(el_tag) == slot_tag(lay_head0)) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      el_hw = lay_rec[x.lane & (LAYOUT_HDR - 1)];
+      el_c0 = lay_rec[LAYOUT_HDR + (x.lane < x.NCr ? x.lane : 0)];
+      el_c1 = lay_rec[LAYOUT_HDR + (x.lane + 64 < x.NCr ? x.lane + 64 : 0)];
+      el_ok = true;
+    }
+  }
+
   // ---- TDBoard.step
   // (parallel targeting: +1.1-1.4 % at 8,192 / 4,096 boards, -0.7 % in the large kernel at 65,536, profiles/r03/s29)
   double reward = board_step<NC, SMALL && !(SPLIT && LT == 20 && MODE == MODE_DEF && !SCAN)>(S, u, x, a, b);
@@ -1802,18 +1852,23 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
     // stream while this grid may be running: relaxed sc1 poll of its tag, then one
     // agent-scope acquire before the plain vector loads of the record
     // (MI355X_MICROARCH.md § visibility, "Valid forms"; producer side: wave_layout)
-    lay_head = a.lay_head[b];
-    const uint32_t* rec = a.nxt + ((size_t)b * NSLOT + lay_head % NSLOT) * a.slot_words;
-    const uint32_t want = slot_tag(lay_head);
-    bool ready = ld_relaxed(rec) == want;
-    // a dry ring: wait for the refill drawing this layout, or draw it now
-    if (!ready) ready = take_dry_ring(a, b, lay_head, &u.flags);
-    if (ready) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      reset_board(S, u, x, rec);
+    lay_head = lay_head0;
+    if (EARLY_LAY && el_ok) {  // loaded during the step (above)
+      if constexpr (EARLY_LAY) reset_board_regs(S, u, x, el_hw, el_c0, el_c1);
       was_reset = true;
     } else {
-      u.flags |= FLAG_NO_LAYOUT;  // 65 failing draws in a row (the reference raises): the board keeps its finished episode
+      const uint32_t* rec = lay_rec;
+      const uint32_t want = slot_tag(lay_head);
+      bool ready = ld_relaxed(rec) == want;
+      // a dry ring: wait for the refill drawing this layout, or draw it now
+      if (!ready) ready = take_dry_ring(a, b, lay_head, &u.flags);
+      if (ready) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        reset_board(S, u, x, rec);
+        was_reset = true;
+      } else {
+        u.flags |= FLAG_NO_LAYOUT;  // 65 failing draws in a row (the reference raises): the board keeps its finished episode
+      }
     }
   }
   // The enemy list back to HBM (after the layout poll's loads, whose wait would

@@ -204,5 +204,22 @@ s18)  # what do episode ends cost at small batches?  auto-reset on (the metric) 
     done
   done
   ;;
+s19)  # early layout hand-off (el, product) vs pa: full GPU suite on it, then A/B 3 rounds; then the auto-reset cost probe on both
+  gpusuite 1100; rc=$?; [ $rc -eq 0 ] || exit 1
+  for r in 1 2 3; do
+    for spec in 8192:2000 4096:2000 65536:300 32768:600; do
+      bb=${spec%%:*}; st=${spec##*:}
+      for v in pa el; do
+        lib=$PWD/gym-td_amd/lib/libtdstep_$v.so; [ $v = el ] && lib=$PWD/gym-td_amd/lib/libtdstep.so
+        TDSTEP_LIB=$lib run ${v}_${bb}_$r 300 python bench.py --global-batch $bb --steps $st --no-cpu-baseline --timing none || exit 1; line ${v}_${bb}_$r
+      done
+    done
+  done
+  for v in pa el; do
+    lib=$PWD/gym-td_amd/lib/libtdstep_$v.so; [ $v = el ] && lib=$PWD/gym-td_amd/lib/libtdstep.so
+    TDSTEP_LIB=$lib run ${v}_ar0_8192 300 python bench.py --global-batch 8192 --steps 2000 --no-cpu-baseline --timing none --autoreset 0 || exit 1; line ${v}_ar0_8192
+    TDSTEP_LIB=$lib run ${v}_ar0_4096 300 python bench.py --global-batch 4096 --steps 2000 --no-cpu-baseline --timing none --autoreset 0 || exit 1; line ${v}_ar0_4096
+  done
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
