@@ -64,6 +64,7 @@ struct alignas(16) Smem {
   };
   uint32_t early_go;         // td_step_kernel_small2: the binary-plane windows may be written early
   int32_t flags0;            // the board's flags as loaded (store_board: is the header's second half dirty?)
+  uint32_t lay_head0;        // lay_head[b] as loaded: the next staged layout's number (kept here, not in SGPRs)
   TdDevCfg cfg;           // constant block, staged once per board: per-lane table lookups hit LDS
 };
 
@@ -1324,7 +1325,7 @@ __device__ __forceinline__ void load_board(Smem<NC>& S, U& u, const Ctx& x, cons
   u.num_roads = (int)lane_word(P.w, 12); u.end_cell = (int)lane_word(P.w, 13);
   u.set_starts((int)lane_word(P.w, 14), (int)lane_word(P.w, 15), (int)lane_word(P.w, 16));
   u.maxdist = (int)lane_word(P.w, 17); u.flags = (int)lane_word(P.w, 18); u.episodes = (int)lane_word(P.w, 19);
-  if (x.lane == 0) S.flags0 = u.flags;
+  if (x.lane == 0) { S.flags0 = u.flags; S.lay_head0 = lane_word(P.w, PF_LAYHEAD); }
   u.max_cost = lane_f64(P.w, 20); u.max_base_LP = (int)lane_word(P.w, 22);
   u.progress = ddiv((double)u.steps, (double)x.C.max_episode_steps);
   u.cells_dirty = false;
@@ -1734,20 +1735,14 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
   // Early layout hand-off (L = 10, the discrete small kernels).  A board that may finish
   // this step -- it reaches the step limit, or holds at least as many enemies as its base
   // has LP (a leak costs one LP each: a necessary condition; 1.2 % of bench.py's
-  // steady-state boards, every one that finishes) -- polls its next staged layout's tag
-  // now, and once the tag has come back (before the board step) takes the acquire and
-  // loads the record into registers: the episode end then resets from them, instead of
-  // three dependent round trips and the acquire after the step.  A board that does not
-  // finish drops them; a ring still dry then is served by the late path below.
+  // steady-state boards, every one that finishes) -- polls its next staged layout before
+  // the board step, and if it is there takes the acquire and loads the record into
+  // registers: the episode end then resets from them instead of polling, acquiring and
+  // loading after the step.  A board that does not finish drops them; a ring still dry is
+  // served by the late path below.  Nothing of it is carried in SGPRs across the step (the
+  // small kernels' SGPRs are at their 8-wave limit: a pointer kept live spilled).
   constexpr bool EARLY_LAY = SMALL && LT == 10 && !SCAN;
-  const uint32_t lay_head0 = lane_word(P.w, PF_LAYHEAD);
-  const uint32_t* const lay_rec = a.nxt + ((size_t)b * NSLOT + lay_head0 % NSLOT) * a.slot_words;
-  bool el_try = false, el_ok = false;
-  uint32_t el_tag = 0u, el_hw = 0u, el_c0 = 0u, el_c1 = 0u;
-  if constexpr (EARLY_LAY) {
-    el_try = a.autoreset && !a.opp_np && (u.steps + 1 >= C.max_episode_steps || u.n >= u.base_LP);
-    if (el_try) el_tag = ld_relaxed(lay_rec);  // (its value is looked at before the board step)
-  }
+  uint32_t el_hw = 0u, el_c0 = 0u, el_c1 = 0u;  // el_hw in lane 0 = the record's tag (non-zero) once loaded
 
   u.atk_cd = u.atk_cd - 1 > 0 ? u.atk_cd - 1 : 0;
   u.def_cd = u.def_cd - 1 > 0 ? u.def_cd - 1 : 0;
@@ -1805,13 +1800,17 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
     __syncthreads();
   }
 
-  if constexpr (EARLY_LAY) {  // the early poll has come back: acquire and load the record (used at the episode end)
-    if (el_try && __builtin_amdgcn_readfirstlane(el_tag) == slot_tag(lay_head0)) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      el_hw = lay_rec[x.lane & (LAYOUT_HDR - 1)];
-      el_c0 = lay_rec[LAYOUT_HDR + (x.lane < x.NCr ? x.lane : 0)];
-      el_c1 = lay_rec[LAYOUT_HDR + (x.lane + 64 < x.NCr ? x.lane + 64 : 0)];
-      el_ok = true;
+  if constexpr (EARLY_LAY) {
+    if (a.autoreset && !a.opp_np && (u.steps + 1 >= C.max_episode_steps || u.n >= u.base_LP)) {
+      const uint32_t h = __builtin_amdgcn_readfirstlane(S.lay_head0);
+      const uint32_t* rec = a.nxt + ((size_t)b * NSLOT + h % NSLOT) * a.slot_words;
+      if (__builtin_amdgcn_readfirstlane(ld_relaxed(rec)) == slot_tag(h)) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        el_hw = rec[x.lane & (LAYOUT_HDR - 1)];
+        el_c0 = rec[LAYOUT_HDR + (x.lane < x.NCr ? x.lane : 0)];
+        el_c1 = rec[LAYOUT_HDR + (x.lane + 64 < x.NCr ? x.lane + 64 : 0)];
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): (in flight, the registers' reuse waited in every writer)
+      }
     }
   }
 
@@ -1852,12 +1851,12 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
     // stream while this grid may be running: relaxed sc1 poll of its tag, then one
     // agent-scope acquire before the plain vector loads of the record
     // (MI355X_MICROARCH.md § visibility, "Valid forms"; producer side: wave_layout)
-    lay_head = lay_head0;
-    if (EARLY_LAY && el_ok) {  // loaded during the step (above)
+    lay_head = __builtin_amdgcn_readfirstlane(S.lay_head0);
+    if (EARLY_LAY && rdl(el_hw, 0) != 0u) {  // loaded before the board step (above)
       if constexpr (EARLY_LAY) reset_board_regs(S, u, x, el_hw, el_c0, el_c1);
       was_reset = true;
     } else {
-      const uint32_t* rec = lay_rec;
+      const uint32_t* rec = a.nxt + ((size_t)b * NSLOT + lay_head % NSLOT) * a.slot_words;
       const uint32_t want = slot_tag(lay_head);
       bool ready = ld_relaxed(rec) == want;
       // a dry ring: wait for the refill drawing this layout, or draw it now
