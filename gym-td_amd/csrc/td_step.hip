@@ -1368,25 +1368,6 @@ __device__ __forceinline__ void reset_board(Smem<NC>& S, U& u, const Ctx& x, con
   wsync();
 }
 
-// The same from a record already in registers (L*L <= 128: lane l holds header word l % 8,
-// cell l and cell l + 64), loaded during the step by the early layout hand-off (step_board).
-template <int NC>
-__device__ __forceinline__ void reset_board_regs(Smem<NC>& S, U& u, const Ctx& x, uint32_t hw, uint32_t c0, uint32_t c1) {
-  static_assert(NC <= 128, "two cell words per lane");
-  const TdDevCfg& C = x.C;
-  if (x.lane < NC) S.cell[x.lane] = c0;
-  if (x.lane + 64 < NC) S.cell[x.lane + 64] = c1;
-  u.num_roads = (int)rdl(hw, 1); u.end_cell = (int)rdl(hw, 2); u.maxdist = (int)rdl(hw, 3);
-  u.set_starts(rdl(hw, 4), rdl(hw, 5), rdl(hw, 6));
-  u.cost_def = C.def_init_cost; u.cost_atk = C.atk_init_cost;
-  u.base_LP = C.base_LP; u.steps = 0; u.progress = 0.0;
-  u.max_cost = C.max_cost; u.max_base_LP = C.base_LP;
-  u.atk_cd = 0; u.def_cd = 0; u.n = 0; u.nt = 0; u.ep_ret = 0.0;
-  u.cells_dirty = true;
-  u.tw_dirty = true;
-  wsync();
-}
-
 // Cell words back to HBM when map[6] changed or a new layout was loaded (before
 // pack_obs_cells reuses the LDS copy).
 template <int NC>
@@ -1732,17 +1713,21 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
   float* const obs = a.obs + (size_t)b * NCH * x.NCr;
   const bool wt = a.obs_wt != 0;
 
-  // Early layout hand-off (L = 10, the discrete small kernels).  A board that may finish
-  // this step -- it reaches the step limit, or holds at least as many enemies as its base
-  // has LP (a leak costs one LP each: a necessary condition; 1.2 % of bench.py's
-  // steady-state boards, every one that finishes) -- polls its next staged layout before
-  // the board step, and if it is there takes the acquire and loads the record into
-  // registers: the episode end then resets from them instead of polling, acquiring and
-  // loading after the step.  A board that does not finish drops them; a ring still dry is
-  // served by the late path below.  Nothing of it is carried in SGPRs across the step (the
-  // small kernels' SGPRs are at their 8-wave limit: a pointer kept live spilled).
+  // Early layout poll (L = 10, the discrete small kernels).  A board that may finish this
+  // step -- it reaches the step limit, or holds at least as many enemies as its base has
+  // LP (a leak costs one LP each: a necessary condition; 1.2 % of bench.py's steady-state
+  // boards, every one that finishes) -- loads its next staged layout's tag now; the episode
+  // end looks at it instead of polling then.  (Taking the acquire and loading the record
+  // before the board step as well made those boards wait for both in the middle of their
+  // step: slower, r06/s19.)
   constexpr bool EARLY_LAY = SMALL && LT == 10 && !SCAN;
-  uint32_t el_hw = 0u, el_c0 = 0u, el_c1 = 0u;  // el_hw in lane 0 = the record's tag (non-zero) once loaded
+  uint32_t el_tag = 0u;
+  if constexpr (EARLY_LAY) {
+    if (a.autoreset && !a.opp_np && (u.steps + 1 >= C.max_episode_steps || u.n >= u.base_LP)) {
+      const uint32_t h = __builtin_amdgcn_readfirstlane(S.lay_head0);
+      el_tag = ld_relaxed(a.nxt + ((size_t)b * NSLOT + h % NSLOT) * a.slot_words);
+    }
+  }
 
   u.atk_cd = u.atk_cd - 1 > 0 ? u.atk_cd - 1 : 0;
   u.def_cd = u.def_cd - 1 > 0 ? u.def_cd - 1 : 0;
@@ -1800,20 +1785,6 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
     __syncthreads();
   }
 
-  if constexpr (EARLY_LAY) {
-    if (a.autoreset && !a.opp_np && (u.steps + 1 >= C.max_episode_steps || u.n >= u.base_LP)) {
-      const uint32_t h = __builtin_amdgcn_readfirstlane(S.lay_head0);
-      const uint32_t* rec = a.nxt + ((size_t)b * NSLOT + h % NSLOT) * a.slot_words;
-      if (__builtin_amdgcn_readfirstlane(ld_relaxed(rec)) == slot_tag(h)) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        el_hw = rec[x.lane & (LAYOUT_HDR - 1)];
-        el_c0 = rec[LAYOUT_HDR + (x.lane < x.NCr ? x.lane : 0)];
-        el_c1 = rec[LAYOUT_HDR + (x.lane + 64 < x.NCr ? x.lane + 64 : 0)];
-        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): (in flight, the registers' reuse waited in every writer)
-      }
-    }
-  }
-
   // ---- TDBoard.step
   // (parallel targeting: +1.1-1.4 % at 8,192 / 4,096 boards, -0.7 % in the large kernel at 65,536, profiles/r03/s29)
   double reward = board_step<NC, SMALL && !(SPLIT && LT == 20 && MODE == MODE_DEF && !SCAN)>(S, u, x, a, b);
@@ -1851,23 +1822,19 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
     // stream while this grid may be running: relaxed sc1 poll of its tag, then one
     // agent-scope acquire before the plain vector loads of the record
     // (MI355X_MICROARCH.md § visibility, "Valid forms"; producer side: wave_layout)
-    lay_head = __builtin_amdgcn_readfirstlane(S.lay_head0);
-    if (EARLY_LAY && rdl(el_hw, 0) != 0u) {  // loaded before the board step (above)
-      if constexpr (EARLY_LAY) reset_board_regs(S, u, x, el_hw, el_c0, el_c1);
+    lay_head = __builtin_amdgcn_readfirstlane(S.lay_head0);  // (prefetched with the board)
+    const uint32_t* rec = a.nxt + ((size_t)b * NSLOT + lay_head % NSLOT) * a.slot_words;
+    const uint32_t want = slot_tag(lay_head);
+    // the early poll's tag if it was taken and found the layout, else a poll now
+    bool ready = (EARLY_LAY && __builtin_amdgcn_readfirstlane(el_tag) == want) || ld_relaxed(rec) == want;
+    // a dry ring: wait for the refill drawing this layout, or draw it now
+    if (!ready) ready = take_dry_ring(a, b, lay_head, &u.flags);
+    if (ready) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      reset_board(S, u, x, rec);
       was_reset = true;
     } else {
-      const uint32_t* rec = a.nxt + ((size_t)b * NSLOT + lay_head % NSLOT) * a.slot_words;
-      const uint32_t want = slot_tag(lay_head);
-      bool ready = ld_relaxed(rec) == want;
-      // a dry ring: wait for the refill drawing this layout, or draw it now
-      if (!ready) ready = take_dry_ring(a, b, lay_head, &u.flags);
-      if (ready) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        reset_board(S, u, x, rec);
-        was_reset = true;
-      } else {
-        u.flags |= FLAG_NO_LAYOUT;  // 65 failing draws in a row (the reference raises): the board keeps its finished episode
-      }
+      u.flags |= FLAG_NO_LAYOUT;  // 65 failing draws in a row (the reference raises): the board keeps its finished episode
     }
   }
   // The enemy list back to HBM (after the layout poll's loads, whose wait would
