@@ -64,7 +64,6 @@ struct alignas(16) Smem {
   };
   uint32_t early_go;         // td_step_kernel_small2: the binary-plane windows may be written early
   int32_t flags0;            // the board's flags as loaded (store_board: is the header's second half dirty?)
-  uint32_t lay_head0;        // lay_head[b] as loaded: the next staged layout's number (kept here, not in SGPRs)
   TdDevCfg cfg;           // constant block, staged once per board: per-lane table lookups hit LDS
 };
 
@@ -1245,8 +1244,6 @@ struct Prefetch {
 // the large-batch kernel (HBM-bound) takes none and loads exactly the live slots once
 // the header's counts are in (one dependent round trip, hidden by the other waves).
 constexpr int PF_ACT = 24, PF_HOT = 26, PF_SMALL = 16, PF_LARGE = 0;
-constexpr int PF_LAYHEAD = PF_HOT + HOT_WORDS;  // lane of lay_head[b] (the next staged layout's number)
-static_assert(PF_LAYHEAD < 64, "prefetch word lanes");
 // (Four enemy slots instead of 16 in TD-def, where 0.02 % of bench.py's steady-state boards
 // hold more than 4, read the same bytes -- each slot array's first 128-B line is fetched
 // whole either way: PMC 1,534 vs 1,535 B read per board -- in the same time, r06/s5.)
@@ -1276,7 +1273,6 @@ __device__ __forceinline__ void prefetch_issue(Prefetch& P, const StepArgs& a, i
   if (lane < PF_ACT) src = reinterpret_cast<const uint32_t*>(a.hdr + b) + lane;
   else if (lane < PF_HOT) src = want_act ? reinterpret_cast<const uint32_t*>(a.def_act + b) + (lane - PF_ACT) : nullptr;
   else if (lane < PF_HOT + HOT_WORDS) src = a.opp_hot + (size_t)b * HOT_WORDS + (lane - PF_HOT);
-  else if (lane == PF_LAYHEAD) src = a.lay_head + b;  // (written only by this board's step / reset waves)
   else src = nullptr;
   P.w = src ? *src : 0u;
 }
@@ -1325,7 +1321,7 @@ __device__ __forceinline__ void load_board(Smem<NC>& S, U& u, const Ctx& x, cons
   u.num_roads = (int)lane_word(P.w, 12); u.end_cell = (int)lane_word(P.w, 13);
   u.set_starts((int)lane_word(P.w, 14), (int)lane_word(P.w, 15), (int)lane_word(P.w, 16));
   u.maxdist = (int)lane_word(P.w, 17); u.flags = (int)lane_word(P.w, 18); u.episodes = (int)lane_word(P.w, 19);
-  if (x.lane == 0) { S.flags0 = u.flags; S.lay_head0 = lane_word(P.w, PF_LAYHEAD); }
+  if (x.lane == 0) S.flags0 = u.flags;
   u.max_cost = lane_f64(P.w, 20); u.max_base_LP = (int)lane_word(P.w, 22);
   u.progress = ddiv((double)u.steps, (double)x.C.max_episode_steps);
   u.cells_dirty = false;
@@ -1713,22 +1709,6 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
   float* const obs = a.obs + (size_t)b * NCH * x.NCr;
   const bool wt = a.obs_wt != 0;
 
-  // Early layout poll (L = 10, the discrete small kernels).  A board that may finish this
-  // step -- it reaches the step limit, or holds at least as many enemies as its base has
-  // LP (a leak costs one LP each: a necessary condition; 1.2 % of bench.py's steady-state
-  // boards, every one that finishes) -- loads its next staged layout's tag now; the episode
-  // end looks at it instead of polling then.  (Taking the acquire and loading the record
-  // before the board step as well made those boards wait for both in the middle of their
-  // step: slower, r06/s19.)
-  constexpr bool EARLY_LAY = SMALL && LT == 10 && !SCAN;
-  uint32_t el_tag = 0u;
-  if constexpr (EARLY_LAY) {
-    if (a.autoreset && !a.opp_np && (u.steps + 1 >= C.max_episode_steps || u.n >= u.base_LP)) {
-      const uint32_t h = __builtin_amdgcn_readfirstlane(S.lay_head0);
-      el_tag = ld_relaxed(a.nxt + ((size_t)b * NSLOT + h % NSLOT) * a.slot_words);
-    }
-  }
-
   u.atk_cd = u.atk_cd - 1 > 0 ? u.atk_cd - 1 : 0;
   u.def_cd = u.def_cd - 1 > 0 ? u.def_cd - 1 : 0;
   const int64_t empty_def = (int64_t)6 * x.NCr;
@@ -1822,11 +1802,10 @@ __device__ __forceinline__ void step_board(Smem<NC>& S, const Ctx& x, const Step
     // stream while this grid may be running: relaxed sc1 poll of its tag, then one
     // agent-scope acquire before the plain vector loads of the record
     // (MI355X_MICROARCH.md § visibility, "Valid forms"; producer side: wave_layout)
-    lay_head = __builtin_amdgcn_readfirstlane(S.lay_head0);  // (prefetched with the board)
+    lay_head = a.lay_head[b];
     const uint32_t* rec = a.nxt + ((size_t)b * NSLOT + lay_head % NSLOT) * a.slot_words;
     const uint32_t want = slot_tag(lay_head);
-    // the early poll's tag if it was taken and found the layout, else a poll now
-    bool ready = (EARLY_LAY && __builtin_amdgcn_readfirstlane(el_tag) == want) || ld_relaxed(rec) == want;
+    bool ready = ld_relaxed(rec) == want;
     // a dry ring: wait for the refill drawing this layout, or draw it now
     if (!ready) ready = take_dry_ring(a, b, lay_head, &u.flags);
     if (ready) {
