@@ -221,5 +221,11 @@ s19)  # early layout hand-off (el, product) vs pa: full GPU suite on it, then A/
     TDSTEP_LIB=$lib run ${v}_ar0_4096 300 python bench.py --global-batch 4096 --steps 2000 --no-cpu-baseline --timing none --autoreset 0 || exit 1; line ${v}_ar0_4096
   done
   ;;
+s20)  # long runs on the final build: no board flag, no guard timeout over 20,000 steps (8,192 / 4,096) and 3,000 (65,536)
+  run long_8192 400 python bench.py --global-batch 8192 --steps 20000 --no-cpu-baseline || exit 1; line long_8192
+  run long_4096 400 python bench.py --global-batch 4096 --steps 20000 --no-cpu-baseline || exit 1; line long_4096
+  run long_65536 400 python bench.py --steps 3000 --no-cpu-baseline || exit 1; line long_65536
+  grep -ho '"board_flags_nonzero": [0-9]*, "guard_timeouts_rank0": [0-9]*' $O/long_*.log
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
