@@ -227,5 +227,9 @@ s20)  # long runs on the final build: no board flag, no guard timeout over 20,00
   run long_65536 400 python bench.py --steps 3000 --no-cpu-baseline || exit 1; line long_65536
   grep -ho '"board_flags_nonzero": [0-9]*, "guard_timeouts_rank0": [0-9]*' $O/long_*.log
   ;;
+s21)  # steady-state every-board tests incl. TD-atk / TD-2p discrete at 10x10
+  run pytest_steady 900 python -u -m pytest tests/test_gpu_steady.py -m gpu -v -x --timeout 600 --timeout-method thread -p no:cacheprovider
+  rc=$?; grep -E "^(FAILED|E  )|PASSED|passed|failed" $O/pytest_steady.log | head -20; [ $rc -le 1 ] || exit $rc
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac

@@ -42,7 +42,10 @@ def _threads():
 # and configs[4] per GPU (30x30), each on the kernel td_create picks on a 256-CU MI355X
 @pytest.mark.parametrize("L,B,mode,multi,want", [
     (10, 65536, "def", False, "small2"), (10, 8192, "def", False, "small"), (10, 4096, "def", False, "small2"),
-    (20, 16384, "2p", True, "small2"), (30, 16384, "def", False, "small2")])
+    (20, 16384, "2p", True, "small2"), (30, 16384, "def", False, "small2"),
+    # the other modes at 10x10 (not BASELINE lines): TD-atk (a random attacker against the
+    # built-in random_tower_lv1) and TD-2p discrete, on whatever kernel td_create picks
+    (10, 16384, "atk", False, None), (10, 4096, "2p", False, None)])
 def test_steady_state_every_board(L, B, mode, multi, want):
     period = P.hyper_parameters.max_episode_steps
     burnin = period
@@ -50,7 +53,7 @@ def test_steady_state_every_board(L, B, mode, multi, want):
     eng = TDEngine(L, B, mode, multi, 1, np_seeds=seeds, py_seeds=seeds, autoreset=True, info=not multi)
     bt = None
     try:
-        if torch.cuda.get_device_properties(0).multi_processor_count == 256:
+        if want and torch.cuda.get_device_properties(0).multi_processor_count == 256:
             assert eng.step_kernel == want, eng.step_kernel_name  # the kernel the bench line times
         eng.reset_all()  # failing first draws skipped (bench.py)
         bt = C.Batch(L, B, mode, 1, seeds, seeds, multi=multi, threads=_threads())
@@ -77,8 +80,10 @@ def test_steady_state_every_board(L, B, mode, multi, want):
                 acts, atk, dd, ad = pool[k % len(pool)]
                 eng.step(def_act=dd, atk_act=ad)
             else:
-                acts, atk = rng.randint(0, 6 * L * L + 1, size=B).astype(np.int64), None
-                eng.step(def_act=torch.from_numpy(acts).to(eng.device))
+                acts = rng.randint(0, 6 * L * L + 1, size=B).astype(np.int64) if mode != "atk" else None
+                atk = rng.randint(0, 5, size=(B, 3, 8)).astype(np.int64) if mode != "def" else None
+                eng.step(def_act=None if acts is None else torch.from_numpy(acts).to(eng.device),
+                         atk_act=None if atk is None else torch.from_numpy(atk).to(eng.device))
             if k < burnin:
                 bt.step(acts, atk)  # (the burn-in's observations are not built on the CPU side)
                 continue
