@@ -231,5 +231,18 @@ s21)  # steady-state every-board tests incl. TD-atk / TD-2p discrete at 10x10
   run pytest_steady 900 python -u -m pytest tests/test_gpu_steady.py -m gpu -v -x --timeout 600 --timeout-method thread -p no:cacheprovider
   rc=$?; grep -E "^(FAILED|E  )|PASSED|passed|failed" $O/pytest_steady.log | head -20; [ $rc -le 1 ] || exit $rc
   ;;
+s22)  # convergent f64 divisions in channel_scalars (cs, product) vs pa: parity subset, A/B 3 rounds
+  run pytest_cs 900 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_steady.py tests/test_gpu_envs.py -m gpu -q -x --timeout 600 --timeout-method thread -p no:cacheprovider
+  rc=$?; grep -E "^(FAILED|E  )" $O/pytest_cs.log | head -20; tail -1 $O/pytest_cs.log; [ $rc -eq 0 ] || exit $rc
+  for r in 1 2 3; do
+    for spec in 8192:2000 4096:2000 65536:300 32768:600; do
+      bb=${spec%%:*}; st=${spec##*:}
+      for v in pa cs; do
+        lib=$PWD/gym-td_amd/lib/libtdstep_$v.so; [ $v = cs ] && lib=$PWD/gym-td_amd/lib/libtdstep.so
+        TDSTEP_LIB=$lib run ${v}_${bb}_$r 300 python bench.py --global-batch $bb --steps $st --no-cpu-baseline --timing none || exit 1; line ${v}_${bb}_$r
+      done
+    done
+  done
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
