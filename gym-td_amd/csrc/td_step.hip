@@ -946,20 +946,13 @@ __device__ __forceinline__ void channel_scalars(Smem<NC>& S, const U& u, const C
   const TdDevCfg& C = x.C;
   const int l = x.lane;
   if (l < 48) {
-    // Every division of the broadcast channels in one convergent pass: each lane selects
-    // its own operands (dummies 0 / 1 elsewhere) and the wave runs the f64 division
-    // sequence twice, where one branch per channel ran it six times one after the other.
-    const bool en4 = l >= 41 && l < 45;
-    const double num = l == 5 ? (double)u.base_LP : l == 12 ? u.cost_atk : (l == 11 || en4) ? u.cost_def : 0.0;
-    const double den = l == 5 ? (double)u.max_base_LP : (l == 11 || l == 12) ? u.max_cost
-                       : en4 ? C.e_cost[(l - 41) & 3][0] : 1.0;
-    const double q = ddiv(num, den);
-    const double q2 = ddiv(q, en4 ? (double)C.max_cluster_length : 1.0);  // (:137-139: cost / price / max cluster)
     float v = 0.0f;
-    if (l == 5 || l == 11 || l == 12) v = f32(q);
+    if (l == 5) v = f32(ddiv((double)u.base_LP, (double)u.max_base_LP));
+    else if (l == 11) v = f32(ddiv(u.cost_def, u.max_cost));
+    else if (l == 12) v = f32(ddiv(u.cost_atk, u.max_cost));
     else if (l == 13) v = f32(u.progress);
     else if (l >= 21 && l < 25) v = (u.cost_def >= C.t_price[l - 21][0]) ? 1.0f : 0.0f;
-    else if (en4) v = f32(q2);
+    else if (l >= 41 && l < 45) v = f32(ddiv(ddiv(u.cost_def, C.e_cost[l - 41][0]), (double)C.max_cluster_length));
     S.chv[l] = v;
   }
   d9_table(S, u.maxdist, l);
