@@ -244,5 +244,13 @@ s22)  # convergent f64 divisions in channel_scalars (cs, product) vs pa: parity 
     done
   done
   ;;
+s23)  # closing check on the final tree: build() on the box, GPU suite, smoke, the driver's command twice, bench.py's defaults
+  run build 400 python -c "import time, __graft_entry__ as g; t = time.time(); g.build(); print('build() %.1f s' % (time.time() - t))" || exit 1; grep -E "build\(\)|Nothing|hipcc" $O/build.log | head -5
+  gpusuite 1100; rc=$?; [ $rc -le 1 ] || exit $rc
+  run smoke 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" || exit 1
+  for r in 1 2; do run bench_driver_$r 300 python bench.py --gpus 1 --steps 20 --warmup 5 || exit 1; line bench_driver_$r; done
+  run bench_default 400 python bench.py || exit 1; line bench_default
+  grep -h '"traffic"' $O/bench_driver_1.log | grep -o '"traffic": [^,]*' | head -1
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
