@@ -252,5 +252,9 @@ s23)  # closing check on the final tree: build() on the box, GPU suite, smoke, t
   run bench_default 400 python bench.py || exit 1; line bench_default
   grep -h '"traffic"' $O/bench_driver_1.log | grep -o '"traffic": [^,]*' | head -1
   ;;
+s24)  # the placement-report test
+  run pytest_alloc 300 python -u -m pytest tests/test_gpu_store_policy.py -m gpu -v -x --timeout 250 --timeout-method thread -p no:cacheprovider
+  rc=$?; grep -E "^(FAILED|E  )|PASSED|passed|failed" $O/pytest_alloc.log | head -20; [ $rc -le 1 ] || exit $rc
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac

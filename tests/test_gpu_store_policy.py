@@ -18,6 +18,7 @@ pytestmark = pytest.mark.gpu
 if not torch.cuda.is_available():  # collected on CPU too, so skip cleanly
     pytest.skip("needs a GPU", allow_module_level=True)
 
+from gym_TD import _lib  # noqa: E402
 from gym_TD.engine import TDEngine  # noqa: E402
 
 # (xcd_map, edge_wt): the product first, then the reference form and the split pairs
@@ -81,3 +82,29 @@ def test_engine_observation_block():
         b.close()
     torch.cuda.synchronize()
     assert torch.equal(view, keep)  # a view keeps the block alive after the engine closed
+
+
+def test_alloc_reports_the_granted_placement():
+    """td_alloc_is_contiguous answers how a td_alloc_device block was placed (a
+    refused contiguous request falls back to a plain allocation, and TDEngine.obs_alloc --
+    the key bench.py quotes PMC traffic records by -- must say so), -1 once it is freed."""
+    from gym_TD.engine import device_zeros
+    for want in (True, False):
+        t = device_zeros((1 << 20,), torch.float32, "cuda", contiguous=want)
+        assert getattr(t, "_td_block", False)
+        got = _lib.lib.td_alloc_is_contiguous(t.data_ptr())
+        assert got in (0, 1) and t._td_contig == (got == 1)
+        if not want:
+            assert got == 0  # a plain request is never contiguous
+        ptr = t.data_ptr()
+        del t
+        import gc
+        gc.collect()
+        torch.cuda.synchronize()
+        assert _lib.lib.td_alloc_is_contiguous(ptr) == -1
+    eng = TDEngine(10, 64, "def", False, 1, np_seeds=np.arange(64), py_seeds=np.arange(64))
+    try:
+        got = _lib.lib.td_alloc_is_contiguous(eng.obs.data_ptr())
+        assert eng.obs_alloc == {1: "contiguous", 0: "plain"}[got]
+    finally:
+        eng.close()
