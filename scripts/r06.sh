@@ -256,5 +256,15 @@ s24)  # the placement-report test
   run pytest_alloc 300 python -u -m pytest tests/test_gpu_store_policy.py -m gpu -v -x --timeout 250 --timeout-method thread -p no:cacheprovider
   rc=$?; grep -E "^(FAILED|E  )|PASSED|passed|failed" $O/pytest_alloc.log | head -20; [ $rc -le 1 ] || exit $rc
   ;;
+s25)  # layout draws only in the ring guard on the step stream (refill interval 0 in the timed steps) vs side-stream refills every 64th step, 3 rounds
+  for r in 1 2 3; do
+    for spec in 8192:3000 4096:3000 65536:300 16384:1500; do
+      bb=${spec%%:*}; st=${spec##*:}
+      run ri64_${bb}_$r 300 python bench.py --global-batch $bb --steps $st --no-cpu-baseline --timing none || exit 1; line ri64_${bb}_$r
+      run ri0_${bb}_$r 300 python bench.py --global-batch $bb --steps $st --no-cpu-baseline --timing none --refill-interval 0 || exit 1; line ri0_${bb}_$r
+    done
+  done
+  grep -ho '"board_flags_nonzero": [0-9]*, "guard_timeouts_rank0": [0-9]*' $O/ri0_*.log | sort | uniq -c
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
